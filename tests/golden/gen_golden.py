@@ -1,0 +1,274 @@
+"""Generate the golden fixtures by running the REFERENCE render path in this container.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [--ref /root/reference]
+
+Only this script reads ``/root/reference``; it runs here (the build container),
+never on the GPU box.  It imports the reference's ``models/spnerf.py`` and
+``modules/rendering.py`` (pure torch/numpy), records every
+random tensor the reference draws (``torch.rand``/``rand_like``/``randn``
+are wrapped, not replaced), and stores inputs, recorded randoms, outputs and
+gradients as small ``.npz`` files next to this script.  Weights are NOT
+stored: they are rebuilt from ``oracle/weights.make_weights(dims, seed)``.
+
+Gradients are taken of a fixed random-projection loss
+``L = Σ_k <out_k, R_k>`` over every differentiable output ``k`` of
+``render_rays`` (``R_k`` drawn from ``numpy.random.default_rng(1234)`` in
+sorted key order, see ``projection_weights``), which exercises the backward
+of every returned tensor.  For W=512 the full gradients would be too large,
+so those cases store per-parameter projections ``<∂L/∂θ, Q_θ>`` instead.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle.weights import ModelDims, make_weights  # noqa: E402
+
+
+# ------------------------------------------------------------------ helpers shared with the tests
+
+def synthetic_rays(n: int, seed: int, far_scale: float = 0.21) -> np.ndarray:
+    """JAX_269-like normalised rays (n, 11): origins inside the unit scene box, unit
+    directions within ~6 deg of the local down vector at Jacksonville (lat 30.3, lon
+    -81.7) expressed in ECEF, near = 0, far ≈ 28 m / 141.2 m, sun_d = (0, 1, 0)
+    (JAX_269 JSONs carry sun_elevation = sun_azimuth = 0, satellite_scene.py:449-473)."""
+    rng = np.random.default_rng(seed)
+    down = np.array([-0.124, 0.855, -0.505])
+    down /= np.linalg.norm(down)
+    o = rng.uniform(-0.8, 0.8, size=(n, 3))
+    d = down + rng.normal(scale=0.05, size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    far = far_scale * rng.uniform(0.95, 1.1, size=n)
+    rays = np.zeros((n, 11), np.float64)
+    rays[:, 0:3], rays[:, 3:6], rays[:, 7] = o, d, far
+    rays[:, 9] = 1.0
+    return rays.astype(np.float32)
+
+
+def projection_weights(shapes: dict, seed: int = 1234) -> dict:
+    rng = np.random.default_rng(seed)
+    return {k: rng.standard_normal(shapes[k]).astype(np.float32) for k in sorted(shapes)}
+
+
+def param_projections(names_shapes: list, seed: int = 4321) -> dict:
+    rng = np.random.default_rng(seed)
+    return {n: rng.standard_normal(s).astype(np.float32) for n, s in names_shapes}
+
+
+# ------------------------------------------------------------------ reference driver
+
+class Recorder:
+    """Wraps torch's RNG entry points used by the reference and records outputs."""
+
+    def __init__(self):
+        self.draws = []
+        self._orig = {}
+
+    def __enter__(self):
+        for name in ("rand", "rand_like", "randn"):
+            fn = getattr(torch, name)
+            self._orig[name] = fn
+
+            def wrapped(*a, __fn=fn, __name=name, **kw):
+                t = __fn(*a, **kw)
+                self.draws.append(("randn" if __name == "randn" else "rand", t.detach().clone()))
+                return t
+            setattr(torch, name, wrapped)
+        return self
+
+    def __exit__(self, *exc):
+        for name, fn in self._orig.items():
+            setattr(torch, name, fn)
+
+
+def load_reference(ref: str):
+    sys.path.insert(0, ref)
+    sys.dont_write_bytecode = True
+    import models.spnerf as ref_spnerf  # noqa
+    import modules.rendering as ref_rendering  # noqa
+    return ref_spnerf, ref_rendering
+
+
+def build_model(ref_spnerf, dims: ModelDims, seed: int):
+    m = ref_spnerf.SPNeRF(num_sem_classes=dims.num_sem_classes, s_embedding_factor=dims.s_embedding_factor,
+                          layers=dims.layers, feat=dims.width, mapping=dims.mapping, t_embedding_dims=dims.t_dim,
+                          beta=dims.beta, sem=dims.sem)
+    w = make_weights(dims, seed)
+    sd = m.state_dict()
+    assert list(sd.keys()) == list(w.keys()), (list(sd.keys()), list(w.keys()))
+    m.load_state_dict({k: torch.tensor(v) for k, v in w.items()})
+    return m
+
+
+def make_args(**kw):
+    base = dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=False, sc_lambda=0.0,
+                margin=0.0001, stdscale=1.0, chunk=5120, noise_std=0.0)
+    base.update(kw)
+    return types.SimpleNamespace(**base)
+
+
+def run_case(ref_spnerf, ref_rendering, name: str, dims: ModelDims, args, n_rays: int, mode: str,
+             full_grads: bool, seed: int = 0, with_depth: bool = False, torch_seed: int = 0,
+             t_vocab: int = 30):
+    torch.manual_seed(torch_seed)
+    model = build_model(ref_spnerf, dims, seed)
+    models = {"coarse": model}
+    rays = torch.tensor(synthetic_rays(n_rays, seed=100 + seed))
+    rng = np.random.default_rng(7 + seed)
+    sem = ts = None
+    extra = {}
+    if dims.sem:
+        labels = rng.choice([0, 1, 2, -100], size=n_rays, p=[0.35, 0.3, 0.25, 0.10]).astype(np.int64)
+        labels[labels >= dims.num_sem_classes] = -100
+        sem = torch.tensor(labels)
+        extra["semantics"] = labels
+    if dims.beta:
+        emb_t = torch.nn.Embedding(t_vocab, dims.t_dim)
+        with torch.no_grad():
+            emb_t.weight.copy_(torch.tensor(np.random.default_rng(99).standard_normal((t_vocab, dims.t_dim)).astype(np.float32)))
+        models["t"] = emb_t
+        ts_np = rng.integers(0, t_vocab, size=n_rays).astype(np.int64)
+        ts = torch.tensor(ts_np)
+        extra["ts"] = ts_np
+        extra["t_embedding"] = emb_t.weight.detach().numpy().copy()
+    kw = {}
+    if with_depth:
+        valid = (rng.uniform(size=n_rays) < 0.68).astype(np.int64)
+        far = rays[:, 7].numpy()
+        gt = (far * rng.uniform(0.3, 0.7, size=n_rays)).astype(np.float32)
+        corr = rng.uniform(0.2, 1.0, size=n_rays).astype(np.float32)
+        std = ((1.0 - rng.uniform(0, 1, size=n_rays)) * 0.05 + 1e-4).astype(np.float32)
+        kw = dict(valid_depth=torch.tensor(valid), target_depths=torch.tensor(np.stack([gt, corr], 1)),
+                  target_std=torch.tensor(std))
+        extra.update(valid_depth=valid, target_depths=np.stack([gt, corr], 1), target_std=std)
+    with Recorder() as rec:
+        res = ref_rendering.render_rays(models, args, rays, ts, semantics=sem, mode=mode, **kw)
+    outs = {k: v for k, v in res.items()}
+    shapes = {k: tuple(v.shape) for k, v in outs.items() if v.requires_grad}
+    R = projection_weights(shapes)
+    loss = sum((outs[k] * torch.tensor(R[k])).sum() for k in sorted(R))
+    params = list(model.named_parameters())
+    if dims.beta:
+        params += [("t.weight", models["t"].weight)]
+    loss.backward()
+    data = {"rays": rays.numpy()}
+    for k, v in extra.items():
+        data["in_" + k] = v
+    for i, (kind, t) in enumerate(rec.draws):
+        data[f"rng{i:02d}_{kind}"] = t.numpy()
+    for k, v in outs.items():
+        data["out_" + k] = v.detach().numpy()
+    if full_grads:
+        for n, p in params:
+            data["grad_" + n] = p.grad.numpy()
+    else:
+        Q = param_projections([(n, tuple(p.shape)) for n, p in params])
+        for n, p in params:
+            data["gproj_" + n] = np.array((p.grad.double() * torch.tensor(Q[n]).double()).sum().item())
+            data["gnorm_" + n] = np.array(p.grad.double().norm().item())
+    data["loss"] = np.array(loss.item())
+    meta = dict(dims=dims.__dict__, args=args.__dict__, mode=mode, seed=seed, n_rays=n_rays)
+    data["meta"] = np.array(repr(meta))
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **data)
+    print(f"{name}: {len(rec.draws)} draws, {os.path.getsize(path) / 1e3:.1f} kB")
+
+
+def unit_sampling(ref_rendering):
+    """sample_pdf / sample_3sigma on edge-case windows (clamped, tiny std, wide)."""
+    torch.manual_seed(5)
+    B, N = 48, 64
+    rng = np.random.default_rng(11)
+    depth = rng.uniform(0.0, 0.25, size=B).astype(np.float32)
+    std = np.concatenate([rng.uniform(1e-4, 2e-3, 16), rng.uniform(0.01, 0.05, 16), rng.uniform(0.1, 0.5, 16)]).astype(np.float32)
+    low, high = torch.tensor(depth - 3 * std), torch.tensor(depth + 3 * std)
+    near, far = torch.tensor(0.0), torch.tensor(0.21)
+    with Recorder() as rec:
+        s3 = ref_rendering.sample_3sigma(low, high, N, False, near, far)
+    bins = torch.sort(torch.rand(B, 33), -1)[0]
+    w = torch.rand(B, 32) ** 4
+    w[:4] = 0.0
+    with Recorder() as rec2:
+        sp = ref_rendering.sample_pdf(bins, w, 40, det=False)
+    # NOTE: det=True raises in the reference (1-D linspace u vs (B, S_+1) cdf in
+    # torch.searchsorted, rendering.py:33,38); perturb is hard-coded to 1 so it never runs.
+    np.savez_compressed(os.path.join(HERE, "unit_sampling.npz"), low=low.numpy(), high=high.numpy(), near=0.0, far=0.21,
+                        u3=rec.draws[0][1].numpy(), s3=s3.numpy(), bins=bins.numpy(), w=w.numpy(),
+                        u_pdf=rec2.draws[0][1].numpy(), s_pdf=sp.numpy())
+    print("unit_sampling written")
+
+
+def unit_composite(ref_spnerf):
+    """inference() compositing driven by a stub model returning chosen raw outputs, covering
+    opaque (σ≫1), empty (σ≈0) and mixed rays; full gradients w.r.t. the raw outputs."""
+    B, S, C = 40, 64, 3
+    rng = np.random.default_rng(21)
+    raw = rng.uniform(0, 1, size=(B, S, 8 + C)).astype(np.float32)
+    sig = rng.exponential(2.0, size=(B, S)).astype(np.float32)
+    sig[:8] *= 1e3        # opaque
+    sig[8:16] *= 1e-6     # empty
+    sig[16:20] = 0.0
+    raw[..., 3] = sig
+    raw[..., 8:] = rng.standard_normal((B, S, C))
+    z = np.sort(rng.uniform(0, 0.2, size=(B, S)).astype(np.float32), -1)
+    raw_t = torch.tensor(raw.reshape(B * S, -1), requires_grad=True)
+
+    class Stub(torch.nn.Module):
+        number_of_outputs, beta, sem = 8 + C, False, True
+
+        def forward(self, x, **kw):
+            return raw_t[: x.shape[0]]
+
+    args = make_args(chunk=B * S, noise_std=0.3)
+    torch.manual_seed(3)
+    with Recorder() as rec:
+        res = ref_spnerf.inference(Stub(), args, torch.zeros(B, S, 3), torch.tensor(z),
+                                   sun_d=torch.zeros(B, 3))
+    shapes = {k: tuple(v.shape) for k, v in res.items() if v.requires_grad}
+    R = projection_weights(shapes)
+    sum((res[k] * torch.tensor(R[k])).sum() for k in sorted(R)).backward()
+    np.savez_compressed(os.path.join(HERE, "unit_composite.npz"), raw=raw, z=z, noise=rec.draws[0][1].numpy(),
+                        noise_std=0.3, **{"out_" + k: v.detach().numpy() for k, v in res.items()},
+                        grad_raw=raw_t.grad.numpy())
+    print("unit_composite written")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    a = ap.parse_args()
+    torch.set_num_threads(8)
+    ref_spnerf, ref_rendering = load_reference(a.ref)
+    # config 1: 256 rays x 64 samples, coarse, mapping, W=512, no sem/guided/sc
+    run_case(ref_spnerf, ref_rendering, "c1_w512", ModelDims(width=512), make_args(), 256, "test", full_grads=False)
+    # small full-gradient case of the same path
+    run_case(ref_spnerf, ref_rendering, "c1_w64", ModelDims(width=64), make_args(), 64, "train", full_grads=True, seed=1)
+    # README recipe path (config 3 flags): guided + solar correction + semantics, train mode with depth priors
+    c3 = make_args(guidedsample=True, sc_lambda=0.1)
+    run_case(ref_spnerf, ref_rendering, "c3_w64", ModelDims(width=64, sem=True), c3, 64, "train",
+             full_grads=True, seed=2, with_depth=True)
+    run_case(ref_spnerf, ref_rendering, "c3_w512", ModelDims(width=512, sem=True), c3, 48, "train",
+             full_grads=False, seed=3, with_depth=True)
+    run_case(ref_spnerf, ref_rendering, "c3_test_w64", ModelDims(width=64, sem=True), c3, 32, "test",
+             full_grads=True, seed=4)
+    # beta head + time embedding, noise on
+    run_case(ref_spnerf, ref_rendering, "beta_w64", ModelDims(width=64, sem=True, beta=True),
+             make_args(beta=True, sc_lambda=0.05, noise_std=0.5), 32, "train", full_grads=True, seed=5)
+    # no positional encoding (mapping off), n_samples=32
+    run_case(ref_spnerf, ref_rendering, "nomap_w64", ModelDims(width=64, mapping=False),
+             make_args(n_samples=32), 40, "test", full_grads=True, seed=6)
+    unit_sampling(ref_rendering)
+    unit_composite(ref_spnerf)
+
+
+if __name__ == "__main__":
+    main()
