@@ -1,0 +1,133 @@
+/*
+ * spnerf_amd.h — C ABI of the MI355X (gfx950) SP-NeRF volumetric render path.
+ *
+ * Plain pointers, sizes and an opaque `void* stream` (a hipStream_t; NULL = the
+ * default stream).  No torch types cross this boundary.  Every device pointer is
+ * owned by the caller: the library NEVER allocates device memory — callers size
+ * buffers with the *_bytes() queries below and pass them in.  Every entry point
+ * is stream-ordered and returns 0 on success or a negative error code; the text
+ * of the last error on the calling thread is spnerf_last_error().
+ *
+ * Each entry point replaces a reference interface (file:line in the reference
+ * ShiningFeng/SP-NeRF tree).  The Python mirror of those interfaces lives in
+ * sp-nerf_amd/ (rendering.py, spnerf.py); INTEGRATION.md shows the ctypes binding.
+ */
+#ifndef SPNERF_AMD_H
+#define SPNERF_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ---------------------------------------------------------------------- */
+#define SPNERF_OK 0
+#define SPNERF_E_ARG -1       /* bad shape / flag / null pointer                         */
+#define SPNERF_E_HIP -2       /* a HIP runtime call failed                               */
+#define SPNERF_E_UNSUPPORTED -3
+
+/* ---- model description: the SPNeRF construction flags (models/__init__.py:6-13,
+ *      models/spnerf.py:162-271) ---------------------------------------------------------- */
+typedef struct spnerf_model_cfg {
+    int32_t width;        /* --fc_units W (spnerf.py:163 `feat`)                              */
+    int32_t layers;       /* --fc_layers (8)                                                  */
+    int32_t skip;         /* skip-connection layer (skips=[4]); -1 = none                     */
+    int32_t n_freq;       /* positional-encoding frequencies (10); 0 = --mapping off          */
+    int32_t sem_classes;  /* --num_sem_classes C when --sem, else 0                           */
+    int32_t sem_dim;      /* C * --s_embedding_factor when --sem, else 0                      */
+    int32_t beta;         /* --beta: uncertainty head on                                      */
+    int32_t t_dim;        /* --t_embbeding_tau (beta only)                                    */
+    int32_t dtype;        /* 0 = fp32 everywhere; 1 = bf16 MFMA trunk (fp32 encode + layer 0) */
+    int32_t reserved[7];
+} spnerf_model_cfg;
+
+/* mlp flags */
+#define SPNERF_MLP_SAVE 1        /* keep activations for spnerf_mlp_backward (training)      */
+#define SPNERF_MLP_SIGMA_ONLY 2  /* trunk + sigma head only (pass 1 of guided sampling)      */
+#define SPNERF_MLP_SUN_ONLY 4    /* sigma + sun-visibility heads (solar-correction pass)     */
+
+/* composite flags */
+#define SPNERF_COMP_WEIGHTS_ONLY 1  /* weights, transparency, depth only (no rgb / sem)      */
+
+/* ---- library ---------------------------------------------------------------------------- */
+const char* spnerf_last_error(void);
+int32_t spnerf_abi_version(void);
+
+/* ---- parameters: canonical order == SPNeRF.named_parameters() (spnerf.py:162-264) ------ */
+int32_t spnerf_param_count(const spnerf_model_cfg* cfg);
+/* name of parameter `idx` (state-dict key) and its torch shape (cols = 0 for 1-D tensors) */
+int32_t spnerf_param_info(const spnerf_model_cfg* cfg, int32_t idx, char* name, int32_t name_cap,
+                          int64_t* rows, int64_t* cols);
+int64_t spnerf_packed_bytes(const spnerf_model_cfg* cfg);
+/* Re-lays the torch parameters (device pointers, canonical order) into the kernel layout:
+ * padded K, pre-transposed copies for the backward, concatenated sibling heads.
+ * `packed` must be zero-filled once when allocated (padding is never written). */
+int32_t spnerf_pack_params(const spnerf_model_cfg* cfg, const float* const* params, void* packed, void* stream);
+
+/* ---- per-point network: SPNeRF.forward (spnerf.py:273-369) over the points of
+ *      `n_rays` rays x `n_samples` depths, xyz = rays[:,0:3] + rays[:,dir:dir+3] * z
+ *      (rendering.py:147,168,172).  out is (P, n_outputs) [rgb3, sigma, sun, sky3, (beta), sem]. */
+int64_t spnerf_mlp_workspace_bytes(const spnerf_model_cfg* cfg, int64_t n_rays, int32_t n_samples, int32_t flags);
+int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed,
+                           const float* rays, int32_t ray_stride, int32_t dir_offset,
+                           int64_t n_rays, int32_t n_samples, const float* z,
+                           const int64_t* labels, const float* t_emb, int32_t flags,
+                           void* workspace, float* out, void* stream);
+/* Gradients of sum(d_out * out) w.r.t. every parameter, written (overwritten) into
+ * `grad_flat` (canonical order, torch shapes, contiguous) and w.r.t. t_emb (n_rays, t_dim). */
+int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed,
+                            const float* rays, int32_t ray_stride, int64_t n_rays, int32_t n_samples,
+                            const int64_t* labels, const float* t_emb, int32_t flags,
+                            void* workspace, const float* d_out, float* grad_flat, float* grad_t_emb,
+                            void* stream);
+
+/* ---- compositing: inference() (spnerf.py:109-157) --------------------------------------- */
+int32_t spnerf_composite_forward(int64_t n_rays, int32_t n_samples, const float* z, const float* out,
+                                 int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
+                                 int32_t n_sem, int32_t flags, float* rgb, float* depth, float* weights,
+                                 float* transparency, float* sem_logits, void* stream);
+/* d_out (P, n_out) receives the gradient w.r.t. out (sigma, albedo, sun, sky, sem columns;
+ * other columns are zeroed).  Any upstream gradient pointer may be NULL (= zero). */
+int32_t spnerf_composite_backward(int64_t n_rays, int32_t n_samples, const float* z, const float* out,
+                                  int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
+                                  int32_t n_sem, int32_t flags, const float* g_rgb, const float* g_depth,
+                                  const float* g_weights, const float* g_transparency, const float* g_sem,
+                                  float* d_out, void* stream);
+
+/* ---- sample generation (rendering.py) --------------------------------------------------- */
+/* stratified jittered depths, perturb = 1 (rendering.py:131-144); u (n_rays, n) in [0,1) */
+int32_t spnerf_sample_stratified(int64_t n_rays, int32_t n_samples, const float* rays, int32_t ray_stride,
+                                 const float* u, float* z, void* stream);
+/* GenerateGuidedSamples + sort + merge (rendering.py:92-116,165-167): 3-sigma window around
+ * the pass-1 depth, replaced by the GT window on rays with valid_depth > 0 (valid_depth may be
+ * NULL = test mode), clamped to clamp_nf[0..1] (device; the chunk's first-ray near/far,
+ * rendering.py:95,113).  u_pred / u_gt are (n_rays, n).  Writes z_sorted = sort([z, z2]) and
+ * z_unsort = [z, sort(z2)], both (n_rays, 2n). */
+int32_t spnerf_sample_guided(int64_t n_rays, int32_t n_samples, const float* z, const float* depth,
+                             const float* weights, const float* clamp_nf, const int64_t* valid_depth,
+                             const float* target_depths, int32_t td_stride, const float* target_std,
+                             const float* u_pred, const float* u_gt, float* z_sorted, float* z_unsort,
+                             void* stream);
+/* sample_pdf (rendering.py:14-55): bins (n_rays, n_bins+1), weights (n_rays, n_bins),
+ * u (n_rays, n_imp) → samples (n_rays, n_imp). n_bins+1 <= 256, n_imp <= 256. */
+int32_t spnerf_sample_pdf(int64_t n_rays, int32_t n_bins, const float* bins, const float* weights,
+                          int32_t n_imp, const float* u, float eps, float* samples, void* stream);
+/* sample_3sigma (rendering.py:58-73): low/high (n_rays), u (n_rays, n) → (n_rays, n) */
+int32_t spnerf_sample_3sigma(int64_t n_rays, int32_t n, const float* low, const float* high,
+                             const float* clamp_nf, const float* u, float* out, void* stream);
+/* row-wise ascending sort of (n_rays, n) floats, n <= 256 (torch.sort(-1) values) */
+int32_t spnerf_sort_rows(int64_t n_rays, int32_t n, const float* in, float* out, void* stream);
+
+/* ---- in-library kernel timing (HIP events on the launch stream) ------------------------- */
+int32_t spnerf_prof_enable(int32_t on);
+int32_t spnerf_prof_reset(void);
+/* Totals over the recorded launches of one kernel class ("gemm_nt_f32", "gemm_tn_f32",
+ * "composite_fwd", ...).  Synchronises the recorded events. */
+int32_t spnerf_prof_read(const char* kernel_class, int64_t* launches, double* total_ms, double* total_flop,
+                         double* total_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPNERF_AMD_H */

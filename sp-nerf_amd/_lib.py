@@ -1,0 +1,119 @@
+"""ctypes binding of libspnerf_amd.so (the C ABI declared in include/spnerf_amd.h).
+
+The library is built in-tree (``make -C sp-nerf_amd`` or ``__graft_entry__.build()``).  There
+is no fallback: every compute entry point raises if the library is missing or if it is handed
+CPU tensors — the render path runs on the MI355X HIP kernels or not at all.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libspnerf_amd.so")
+
+SPNERF_MLP_SAVE = 1
+SPNERF_MLP_SIGMA_ONLY = 2
+SPNERF_MLP_SUN_ONLY = 4
+SPNERF_COMP_WEIGHTS_ONLY = 1
+
+
+class ModelCfg(ctypes.Structure):
+    """spnerf_model_cfg (include/spnerf_amd.h)."""
+    _fields_ = [("width", c_int32), ("layers", c_int32), ("skip", c_int32), ("n_freq", c_int32),
+                ("sem_classes", c_int32), ("sem_dim", c_int32), ("beta", c_int32), ("t_dim", c_int32),
+                ("dtype", c_int32), ("reserved", c_int32 * 7)]
+
+    def key(self):
+        return tuple(getattr(self, f) for f, _ in self._fields_[:-1])
+
+
+# name → (restype, argtypes); the exact export list of include/spnerf_amd.h
+SIGNATURES = {
+    "spnerf_last_error": (c_char_p, []),
+    "spnerf_abi_version": (c_int32, []),
+    "spnerf_param_count": (c_int32, [POINTER(ModelCfg)]),
+    "spnerf_param_info": (c_int32, [POINTER(ModelCfg), c_int32, c_char_p, c_int32, POINTER(c_int64), POINTER(c_int64)]),
+    "spnerf_packed_bytes": (c_int64, [POINTER(ModelCfg)]),
+    "spnerf_pack_params": (c_int32, [POINTER(ModelCfg), POINTER(c_void_p), c_void_p, c_void_p]),
+    "spnerf_mlp_workspace_bytes": (c_int64, [POINTER(ModelCfg), c_int64, c_int32, c_int32]),
+    "spnerf_mlp_forward": (c_int32, [POINTER(ModelCfg), c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p,
+                                     c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "spnerf_mlp_backward": (c_int32, [POINTER(ModelCfg), c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p,
+                                      c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "spnerf_composite_forward": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_int32,
+                                           c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "spnerf_composite_backward": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_int32,
+                                            c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p]),
+    "spnerf_sample_stratified": (c_int32, [c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "spnerf_sample_guided": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "spnerf_sample_pdf": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_void_p, c_void_p]),
+    "spnerf_sample_3sigma": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "spnerf_sort_rows": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
+    "spnerf_prof_enable": (c_int32, [c_int32]),
+    "spnerf_prof_reset": (c_int32, []),
+    "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
+}
+
+_lib = None
+
+
+class SpnerfError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the HIP library (once).  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SpnerfError(f"{LIB_PATH} is missing: build it with `make -C sp-nerf_amd` "
+                              "(or __graft_entry__.build()); there is no CPU fallback")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().spnerf_last_error().decode(errors="replace")
+        raise SpnerfError(f"spnerf_amd {what}: error {rc}: {msg}")
+
+
+def ptr(t) -> c_void_p:
+    return c_void_p(0) if t is None else c_void_p(t.data_ptr())
+
+
+def stream_of(t) -> c_void_p:
+    import torch
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors) -> None:
+    """The product path runs only on the GPU; CPU tensors are an error, not a fallback."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise SpnerfError("spnerf_amd runs the render path on the MI355X (HIP) only; got a tensor on "
+                              f"{t.device}. Move rays / models to the GPU.")
+
+
+def prof_enable(on: bool = True) -> None:
+    check(lib().spnerf_prof_enable(1 if on else 0), "prof_enable")
+
+
+def prof_reset() -> None:
+    check(lib().spnerf_prof_reset(), "prof_reset")
+
+
+def prof_read(kernel_class: str) -> dict:
+    n, ms, fl, by = c_int64(), c_double(), c_double(), c_double()
+    check(lib().spnerf_prof_read(kernel_class.encode(), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(fl),
+                                 ctypes.byref(by)), "prof_read")
+    return {"launches": n.value, "ms": ms.value, "flop": fl.value, "bytes": by.value}

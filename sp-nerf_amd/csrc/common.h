@@ -1,0 +1,70 @@
+// Shared host/device helpers of the SP-NeRF gfx950 library.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/spnerf_amd.h"
+
+namespace spn {
+
+// ---- errors (thread-local last-error text, see spnerf_last_error) -------------------------
+void set_error(const char* fmt, ...);
+
+#define SPN_ARG(cond, ...)                 \
+    do {                                   \
+        if (!(cond)) {                     \
+            ::spn::set_error(__VA_ARGS__); \
+            return SPNERF_E_ARG;           \
+        }                                  \
+    } while (0)
+
+#define SPN_HIP(call)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            ::spn::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),      \
+                             __FILE__, __LINE__);                                       \
+            return SPNERF_E_HIP;                                                        \
+        }                                                                               \
+    } while (0)
+
+#define SPN_TRY(expr)              \
+    do {                           \
+        int32_t rc_ = (expr);      \
+        if (rc_ != SPNERF_OK)      \
+            return rc_;            \
+    } while (0)
+
+// ---- profiling: HIP events around each launch of a kernel class, on the launch stream ----
+struct ProfScope {
+    ProfScope(const char* cls, hipStream_t s, double flop, double bytes);
+    ~ProfScope();
+    void* rec_;
+    hipStream_t s_;
+};
+
+// ---- small device helpers -----------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Bijective XCD-aware remap of a 1-D grid: blocks b and b+8 share an XCD (round-robin
+// dispatch), so hand each XCD a contiguous run of tiles (cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_remap(int id, int nb) {
+    const int xcd = id & 7, loc = id >> 3;
+    const int q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// torch-compatible elementwise pieces (ATen CPU formulas)
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float softplusf_(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float softplus_grad(float g, float x) {
+    if (x > 20.0f) return g;
+    const float z = expf(x);
+    return g * z / (z + 1.0f);
+}
+
+}  // namespace spn

@@ -1,0 +1,274 @@
+// σ→α volumetric compositing with the solar-visibility irradiance term
+// (inference(), models/spnerf.py:115-134,156), forward and backward, one wavefront per ray.
+//
+// Lane l holds the EPL consecutive samples l*EPL .. l*EPL+EPL-1 (S ≤ 64*EPL); the exclusive
+// cumprod of (1-α+1e-10) is a lane-local product + a 6-step wavefront scan, the backward's
+// reversed cumsum a lane-local suffix sum + a 6-step suffix scan.  The backward follows torch
+// autograd's formulas exactly where they differ from the textbook derivative: cumprod's
+// no-zero fast path  dIn_m = (Σ_{j≥m} out_j·gOut_j) / In_m  (FunctionsManual cumprod_backward),
+// clamp's inclusive pass-through mask, relu's result>0 mask, mean's division by S.
+#include "common.h"
+#include "wave.h"
+
+namespace spn {
+
+struct CompArgs {
+    int64_t B;
+    int S, NO, sem_col, n_sem, weights_only;
+    const float *z, *out, *noise;
+    float noise_std;
+    float *rgb, *depth, *w, *T, *sem;
+    const float *g_rgb, *g_depth, *g_w, *g_T, *g_sem;
+    float* d_out;
+};
+
+__device__ __forceinline__ float relu_t(float x) { return x != x ? x : (x > 0.f ? x : 0.f); }
+
+template <int EPL>
+struct RayState {
+    float z[EPL], al[EPL], t[EPL], T[EPL], w[EPL], r[EPL], E[EPL], dl[EPL];
+};
+
+// per-sample alpha / transparency / weights of one ray (spnerf.py:116-128)
+template <int EPL>
+__device__ __forceinline__ void march(const CompArgs& a, int64_t ray, int lane, RayState<EPL>& st) {
+    const int S = a.S;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int e = lane * EPL + j;
+        st.z[j] = e < S ? a.z[ray * S + e] : 0.f;
+    }
+    const float zn0 = __shfl_down(st.z[0], 1, 64);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int e = lane * EPL + j;
+        if (e < S) {
+            const int64_t p = ray * S + e;
+            float sg = a.out[p * a.NO + 3];
+            if (a.noise) sg = sg + a.noise[p] * a.noise_std;
+            const float zn = j + 1 < EPL ? st.z[j + 1] : zn0;
+            const float dl = e == S - 1 ? 1e10f : zn - st.z[j];
+            const float r = relu_t(sg);
+            const float E = expf(-dl * r);
+            const float al = 1.f - E;
+            st.dl[j] = dl;
+            st.r[j] = r;
+            st.E[j] = E;
+            st.al[j] = al;
+            st.t[j] = (1.f - al) + 1e-10f;
+        } else {
+            st.dl[j] = st.r[j] = st.E[j] = st.al[j] = 0.f;
+            st.t[j] = 1.f;
+        }
+    }
+    // exclusive cumprod in double (torch's CPU cumprod accumulates in double), rounded once
+    double run = 1.0, excl[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        excl[j] = run;
+        run *= (double)st.t[j];
+    }
+    const double incl = wave_scan_mul(run, lane);
+    double lane_excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) lane_excl = 1.0;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        st.T[j] = (float)(lane_excl * excl[j]);
+        st.w[j] = st.al[j] * st.T[j];
+    }
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void k_composite_fwd(CompArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (ray >= a.B) return;
+    RayState<EPL> st;
+    march<EPL>(a, ray, lane, st);
+    const int S = a.S;
+    float dsum = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int e = lane * EPL + j;
+        if (e >= S) continue;
+        const int64_t p = ray * S + e;
+        a.w[p] = st.w[j];
+        a.T[p] = st.T[j];
+        dsum += st.w[j] * st.z[j];
+        if (!a.weights_only) {
+            const float* o = a.out + p * a.NO;
+            const float sun = o[4], om = 1.f - sun;
+            c0 += (st.w[j] * o[0]) * (sun + om * o[5]);
+            c1 += (st.w[j] * o[1]) * (sun + om * o[6]);
+            c2 += (st.w[j] * o[2]) * (sun + om * o[7]);
+        }
+    }
+    dsum = wave_sum(dsum);
+    if (lane == 0) a.depth[ray] = dsum;
+    if (a.weights_only) return;
+    c0 = wave_sum(c0);
+    c1 = wave_sum(c1);
+    c2 = wave_sum(c2);
+    if (lane == 0) {
+        a.rgb[ray * 3 + 0] = fminf(fmaxf(c0, 0.f), 1.f);
+        a.rgb[ray * 3 + 1] = fminf(fmaxf(c1, 0.f), 1.f);
+        a.rgb[ray * 3 + 2] = fminf(fmaxf(c2, 0.f), 1.f);
+    }
+    for (int c = 0; c < a.n_sem; ++c) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) {
+            const int e = lane * EPL + j;
+            if (e < S) s += a.out[(ray * S + e) * a.NO + a.sem_col + c];
+        }
+        s = wave_sum(s);
+        if (lane == 0) a.sem[ray * a.n_sem + c] = s / (float)S;
+    }
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (ray >= a.B) return;
+    RayState<EPL> st;
+    march<EPL>(a, ray, lane, st);
+    const int S = a.S;
+    const bool col = !a.weights_only;
+    // clamp mask of rgb = clamp(Σ w·albedo·irr, 0, 1) (recomputed pre-clamp value)
+    float gp[3] = {0.f, 0.f, 0.f};
+    if (col && a.g_rgb) {
+        float c[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) {
+            const int e = lane * EPL + j;
+            if (e >= S) continue;
+            const float* o = a.out + (ray * S + e) * a.NO;
+            const float sun = o[4], om = 1.f - sun;
+            for (int q = 0; q < 3; ++q) c[q] += (st.w[j] * o[q]) * (sun + om * o[5 + q]);
+        }
+        for (int q = 0; q < 3; ++q) {
+            const float v = wave_sum(c[q]);
+            const float g = a.g_rgb[ray * 3 + q];
+            gp[q] = (v >= 0.f && v <= 1.f) ? g : 0.f;
+        }
+    }
+    const float gd = a.g_depth ? a.g_depth[ray] : 0.f;
+    float dal[EPL], q[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int e = lane * EPL + j;
+        dal[j] = 0.f;
+        q[j] = 0.f;
+        if (e >= S) continue;
+        const int64_t p = ray * S + e;
+        float* dO = a.d_out + p * a.NO;
+        float dw = gd * st.z[j] + (a.g_w ? a.g_w[p] : 0.f);
+        if (col) {
+            const float* o = a.out + p * a.NO;
+            const float sun = o[4], om = 1.f - sun;
+            float dsun = 0.f, dsun2 = 0.f;
+            for (int c = 0; c < 3; ++c) {
+                const float sky = o[5 + c];
+                const float irr = sun + om * sky;
+                const float du = gp[c] * irr;
+                dw += du * o[c];
+                dO[c] = du * st.w[j];
+                const float dirr = gp[c] * (st.w[j] * o[c]);
+                dsun += dirr;
+                dsun2 += dirr * sky;
+                dO[5 + c] = dirr * om;
+            }
+            dO[4] = dsun - dsun2;
+        } else {
+            dO[0] = dO[1] = dO[2] = dO[4] = dO[5] = dO[6] = dO[7] = 0.f;
+        }
+        for (int c = 8; c < a.NO; ++c) dO[c] = 0.f;
+        if (col && a.g_sem)
+            for (int c = 0; c < a.n_sem; ++c) dO[a.sem_col + c] = a.g_sem[ray * a.n_sem + c] / (float)S;
+        const float dT = dw * st.al[j] + (a.g_T ? a.g_T[p] : 0.f);
+        dal[j] = dw * st.T[j];
+        q[j] = st.T[j] * dT;
+    }
+    // reversed cumsum R_e = Σ_{j≥e} q_j (double accumulation like torch's CPU cumsum)
+    double suf[EPL];
+    double run = 0.0;
+#pragma unroll
+    for (int j = EPL - 1; j >= 0; --j) {
+        run += (double)q[j];
+        suf[j] = run;
+    }
+    const double incl = wave_suffix_add(run, lane);
+    double nxt = __shfl_down(incl, 1, 64);
+    if (lane == 63) nxt = 0.0;
+    float R[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) R[j] = (float)(suf[j] + nxt);
+    const float Rn0 = __shfl_down(R[0], 1, 64);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+        const int e = lane * EPL + j;
+        if (e >= S) continue;
+        const float Rnext = e == S - 1 ? 0.f : (j + 1 < EPL ? R[j + 1] : Rn0);
+        const float dt = Rnext / st.t[j];
+        const float da = dal[j] - dt;
+        const float dX = (-da) * st.E[j];
+        const float dr = dX * (-st.dl[j]);
+        a.d_out[(ray * S + e) * a.NO + 3] = st.r[j] > 0.f ? dr : 0.f;
+    }
+}
+
+template <int EPL>
+static int32_t launch_comp(const CompArgs& a, bool fwd, hipStream_t s) {
+    const dim3 grid((unsigned)((a.B + 3) / 4)), block(256);
+    if (fwd) hipLaunchKernelGGL(k_composite_fwd<EPL>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_composite_bwd<EPL>, grid, block, 0, s, a);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+static int32_t run_comp(const CompArgs& a, bool fwd, hipStream_t s) {
+    SPN_ARG(a.S > 0 && a.S <= 256, "composite: n_samples %d must be in [1, 256]", a.S);
+    SPN_ARG(a.NO >= 8 && a.sem_col + a.n_sem <= a.NO, "composite: bad output layout");
+    if (a.B == 0) return SPNERF_OK;
+    const double P = (double)a.B * a.S;
+    ProfScope prof(fwd ? "composite_fwd" : "composite_bwd", s, 0.0,
+                   fwd ? P * (a.weights_only ? 16.0 : 44.0) + a.B * 16.0 : P * (a.NO * 8.0 + 24.0));
+    if (a.S <= 64) return launch_comp<1>(a, fwd, s);
+    if (a.S <= 128) return launch_comp<2>(a, fwd, s);
+    return launch_comp<4>(a, fwd, s);
+}
+
+}  // namespace spn
+
+using namespace spn;
+
+extern "C" int32_t spnerf_composite_forward(int64_t n_rays, int32_t n_samples, const float* z, const float* out,
+                                            int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
+                                            int32_t n_sem, int32_t flags, float* rgb, float* depth, float* weights,
+                                            float* transparency, float* sem_logits, void* stream) {
+    const bool wo = flags & SPNERF_COMP_WEIGHTS_ONLY;
+    SPN_ARG(z && out && depth && weights && transparency, "composite_forward: NULL pointer");
+    SPN_ARG(wo || rgb, "composite_forward: rgb is NULL");
+    SPN_ARG(wo || n_sem == 0 || sem_logits, "composite_forward: sem_logits is NULL");
+    CompArgs a{};
+    a.B = n_rays; a.S = n_samples; a.NO = n_out; a.sem_col = sem_col; a.n_sem = wo ? 0 : n_sem; a.weights_only = wo;
+    a.z = z; a.out = out; a.noise = noise; a.noise_std = noise_std;
+    a.rgb = rgb; a.depth = depth; a.w = weights; a.T = transparency; a.sem = sem_logits;
+    return run_comp(a, true, (hipStream_t)stream);
+}
+
+extern "C" int32_t spnerf_composite_backward(int64_t n_rays, int32_t n_samples, const float* z, const float* out,
+                                             int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
+                                             int32_t n_sem, int32_t flags, const float* g_rgb, const float* g_depth,
+                                             const float* g_weights, const float* g_transparency, const float* g_sem,
+                                             float* d_out, void* stream) {
+    const bool wo = flags & SPNERF_COMP_WEIGHTS_ONLY;
+    SPN_ARG(z && out && d_out, "composite_backward: NULL pointer");
+    CompArgs a{};
+    a.B = n_rays; a.S = n_samples; a.NO = n_out; a.sem_col = sem_col; a.n_sem = wo ? 0 : n_sem; a.weights_only = wo;
+    a.z = z; a.out = out; a.noise = noise; a.noise_std = noise_std;
+    a.g_rgb = g_rgb; a.g_depth = g_depth; a.g_w = g_weights; a.g_T = g_transparency; a.g_sem = g_sem;
+    a.d_out = d_out;
+    return run_comp(a, false, (hipStream_t)stream);
+}

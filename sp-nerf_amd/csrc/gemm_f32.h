@@ -1,0 +1,51 @@
+// Launch descriptors of the fp32 MFMA GEMMs (gemm_f32.hip).
+#pragma once
+#include "common.h"
+
+namespace spn {
+
+// C[M,N] = epi(A[M,K] · B[N,K]^T).  A may be split along K into two sources: columns [0,K1)
+// from A, [K1,K) from A2 (the skip-layer input [h | x0], spnerf.py:326-327).
+struct NTArgs {
+    const float* A = nullptr; int lda = 0;
+    const float* A2 = nullptr; int lda2 = 0; int K1 = 0;
+    const float* B = nullptr; int ldb = 0;
+    float* C = nullptr; int ldc = 0;
+    int M = 0, N = 0, K = 0;
+    // epilogue, in order: + bias[col] + rowbias[row/rows_per_ray][col] + r1_a[row]*r1_v[col];
+    // act==1 and col>=n_lin: y = sin(w0*v), Dout = w0*cos(w0*v) (else y = v, Dout = 1); y *= Dmul
+    const float* bias = nullptr;
+    const float* rowbias = nullptr; int ld_rb = 0; int rows_per_ray = 1;
+    const float* r1_a = nullptr; int r1_lda = 0; const float* r1_v = nullptr;
+    int act = 0; float w0 = 1.f; int n_lin = 0;
+    float* Dout = nullptr; int ld_dout = 0;
+    const float* Dmul = nullptr; int ld_dmul = 0;
+};
+
+// slab[s][n][k] = Σ_{p in split s} A[p][n] · B[p][k]  (B split along K at K1 like NTArgs.A);
+// slab_b[s][n] = Σ_{p in split s} A[p][n]  (bias gradient), if slab_b != nullptr.
+struct TNArgs {
+    const float* A = nullptr; int lda = 0;
+    const float* B = nullptr; int ldb = 0;
+    const float* B2 = nullptr; int ldb2 = 0; int K1 = 0;
+    float* slab = nullptr; int ld_slab = 0; int64_t slab_stride = 0;
+    float* slab_b = nullptr;
+    int P = 0, N = 0, K = 0;
+    int p_per_split = 0;  // set by gemm_tn
+};
+
+struct ReduceArgs {
+    const float* slab = nullptr; int ld_slab = 0; int64_t slab_stride = 0; int splits = 0; int N = 0;
+    const float* slab_b = nullptr;
+    int row0 = 0, nrows = 0, ncols = 0;
+    float* dst = nullptr; int ld_dst = 0;
+    float* dst_b = nullptr;
+    int accumulate = 0;
+};
+
+int32_t gemm_nt(const NTArgs& a, hipStream_t s);
+int tn_splits(int P, int N, int K);
+int32_t gemm_tn(const TNArgs& a, int splits, hipStream_t s);
+int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s);
+
+}  // namespace spn

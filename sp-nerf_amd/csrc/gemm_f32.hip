@@ -1,0 +1,281 @@
+// fp32 MFMA GEMMs for the SIREN MLP on gfx950 (v_mfma_f32_32x32x2_f32: exact f32 fmaf
+// chains at the 157 TF/s f32 matrix rate, MI355X_MICROARCH.md "Matrix cores").
+//
+//  * k_gemm_nt  C[M,N] = epi( A[M,K] · B[N,K]^T )   forward layers (B = torch weight, K-contig)
+//                                                    and backward dX (B = pre-transposed weight)
+//  * k_gemm_tn  slab[s][N,K] = Σ_{p in split s} A[p,N]^T · B[p,K]   weight gradients, split over
+//                                                    the point dimension, partial slabs reduced in
+//                                                    a fixed order (deterministic) by k_reduce_slabs
+//
+// Tiles: 128x128 per 256-thread workgroup, 4 waves each owning 64x64 = 2x2 MFMA 32x32 tiles,
+// BK = 32 staged through LDS with a register prefetch of the next K-step.  K is walked in
+// groups of 8 with lane-half h handling k = 8g+4h+s at MFMA step s: that permutation lets a
+// lane fetch its 4 operands of 4 consecutive MFMAs with one ds_read_b128 (the sum over k is
+// order-free up to rounding).  LDS rows padded to 36 floats → conflict-free b128 reads.
+#include "common.h"
+#include "gemm_f32.h"
+
+namespace spn {
+
+constexpr int BM = 128, BN = 128, BK = 32, LDK = BK + 4;
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+__global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
+    __shared__ __attribute__((aligned(16))) float sA[BM * LDK];
+    __shared__ __attribute__((aligned(16))) float sB[BN * LDK];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nN = (g.N + BN - 1) / BN;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int bm = (t / nN) * BM, bn = (t % nN) * BN;
+    const int lr = tid >> 3, lk = (tid & 7) * 4;
+
+    f32x4 ra[4], rb[4];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = bm + lr + 32 * i;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (row < g.M) {
+                if (k0 < g.K1) v = ld4(g.A + (int64_t)row * g.lda + k0 + lk);
+                else v = ld4(g.A2 + (int64_t)row * g.lda2 + (k0 - g.K1) + lk);
+            }
+            ra[i] = v;
+            const int col = bn + lr + 32 * i;
+            f32x4 w = {0.f, 0.f, 0.f, 0.f};
+            if (col < g.N) w = ld4(g.B + (int64_t)col * g.ldb + k0 + lk);
+            rb[i] = w;
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int wr = wid >> 1, wc = wid & 1, r32 = lane & 31, h = lane >> 5;
+    const float* pa0 = sA + (wr * 64 + r32) * LDK + 4 * h;
+    const float* pa1 = pa0 + 32 * LDK;
+    const float* pb0 = sB + (wc * 64 + r32) * LDK + 4 * h;
+    const float* pb1 = pb0 + 32 * LDK;
+
+    gload(0);
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            *reinterpret_cast<f32x4*>(sA + (lr + 32 * i) * LDK + lk) = ra[i];
+            *reinterpret_cast<f32x4*>(sB + (lr + 32 * i) * LDK + lk) = rb[i];
+        }
+        __syncthreads();
+        if (k0 + BK < g.K) gload(k0 + BK);
+#pragma unroll
+        for (int kg = 0; kg < BK / 8; ++kg) {
+            const f32x4 a0 = ld4(pa0 + kg * 8), a1 = ld4(pa1 + kg * 8);
+            const f32x4 b0 = ld4(pb0 + kg * 8), b1 = ld4(pb1 + kg * 8);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
+            }
+        }
+    }
+
+    // epilogue: each wave stages one 32x32 accumulator tile at a time in LDS (acc reg r sits at
+    // row (r&3)+8(r>>2)+4h, column lane&31) and walks it back row-major, so every global access
+    // of the epilogue (rowbias, Dmul, Dout, C) is a 128-B row segment and sincos is not unrolled.
+    float* stage = sA + wid * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + r32] = acc[i][j][r];
+            __syncthreads();
+            const int col = bn + wc * 64 + j * 32 + r32;
+            if (col >= g.N) continue;
+            const float bias = g.bias ? g.bias[col] : 0.f;
+            const bool sine = g.act == 1 && col >= g.n_lin;
+            const float r1v = g.r1_a ? g.r1_v[col] : 0.f;
+#pragma unroll 2
+            for (int e = 0; e < 16; ++e) {
+                const int rr = 2 * e + h;
+                const int row = bm + wr * 64 + i * 32 + rr;
+                if (row >= g.M) continue;
+                float v = stage[rr * 32 + r32] + bias;
+                if (g.rowbias) v += g.rowbias[(int64_t)(row / g.rows_per_ray) * g.ld_rb + col];
+                if (g.r1_a) v += g.r1_a[(int64_t)row * g.r1_lda] * r1v;
+                float y = v, dv = 1.f;
+                if (sine) {
+                    const float a = g.w0 * v;
+                    float sn, cs;
+                    sincosf(a, &sn, &cs);
+                    y = sn;
+                    dv = g.w0 * cs;
+                }
+                if (g.Dout) g.Dout[(int64_t)row * g.ld_dout + col] = dv;
+                if (g.Dmul) y *= g.Dmul[(int64_t)row * g.ld_dmul + col];
+                g.C[(int64_t)row * g.ldc + col] = y;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
+    constexpr int LDN = 128;
+    __shared__ __attribute__((aligned(16))) float sA[BK * LDN];
+    __shared__ __attribute__((aligned(16))) float sB[BK * LDN];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nK = (g.K + 127) / 128;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int n0 = (t / nK) * 128, k0 = (t % nK) * 128;
+    const int split = blockIdx.y;
+    const int p_beg = split * g.p_per_split;
+    const int p_end = min(g.P, p_beg + g.p_per_split);
+    const int lr = tid >> 5, lc = (tid & 31) * 4;
+
+    f32x4 ra[4], rb[4];
+    auto gload = [&](int p0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = p0 + lr + 8 * i;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
+            if (p < p_end) {
+                if (n0 + lc < g.N) v = ld4(g.A + (int64_t)p * g.lda + n0 + lc);
+                const int k = k0 + lc;
+                if (k < g.K) {
+                    if (k < g.K1) w = ld4(g.B + (int64_t)p * g.ldb + k);
+                    else w = ld4(g.B2 + (int64_t)p * g.ldb2 + (k - g.K1));
+                }
+            }
+            ra[i] = v;
+            rb[i] = w;
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const bool do_bias = g.slab_b != nullptr && k0 == 0 && tid < 128;
+    float bsum = 0.f;
+    const int wr = wid >> 1, wc = wid & 1, r32 = lane & 31, h = lane >> 5;
+
+    if (p_beg < p_end) gload(p_beg);
+    for (int p0 = p_beg; p0 < p_end; p0 += BK) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            *reinterpret_cast<f32x4*>(sA + (lr + 8 * i) * LDN + lc) = ra[i];
+            *reinterpret_cast<f32x4*>(sB + (lr + 8 * i) * LDN + lc) = rb[i];
+        }
+        __syncthreads();
+        if (p0 + BK < p_end) gload(p0 + BK);
+        if (do_bias) {
+#pragma unroll 8
+            for (int q = 0; q < BK; ++q) bsum += sA[q * LDN + tid];
+        }
+#pragma unroll
+        for (int kg = 0; kg < BK / 8; ++kg) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int q = kg * 8 + 4 * h + s;
+                const float a0 = sA[q * LDN + wr * 64 + r32], a1 = sA[q * LDN + wr * 64 + 32 + r32];
+                const float b0 = sB[q * LDN + wc * 64 + r32], b1 = sB[q * LDN + wc * 64 + 32 + r32];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            }
+        }
+    }
+
+    float* slab = g.slab + (int64_t)split * g.slab_stride;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int k = k0 + wc * 64 + j * 32 + r32;
+        if (k >= g.K) continue;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (n < g.N) slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
+            }
+    }
+    if (do_bias && n0 + tid < g.N) g.slab_b[(int64_t)split * g.N + n0 + tid] = bsum;
+}
+
+// dst[r][c] (+)= Σ_s slab[s][row0+r][c] for c < ncols; dst_b[r] = Σ_s slab_b[s][row0+r]
+__global__ void k_reduce_slabs(ReduceArgs g) {
+    const int r = blockIdx.y;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = g.row0 + r;
+    if (c < g.ncols) {
+        float s = 0.f;
+        for (int k = 0; k < g.splits; ++k) s += g.slab[(int64_t)k * g.slab_stride + (int64_t)n * g.ld_slab + c];
+        float* d = g.dst + (int64_t)r * g.ld_dst + c;
+        *d = g.accumulate ? *d + s : s;
+    } else if (c == g.ncols && g.dst_b) {
+        float s = 0.f;
+        for (int k = 0; k < g.splits; ++k) s += g.slab_b[(int64_t)k * g.N + n];
+        g.dst_b[r] = g.accumulate ? g.dst_b[r] + s : s;
+    }
+}
+
+int32_t gemm_nt(const NTArgs& a, hipStream_t s) {
+    SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
+    SPN_ARG(a.K % BK == 0 && a.K1 % BK == 0 && a.K1 <= a.K, "gemm_nt: K=%d/K1=%d must be multiples of %d", a.K, a.K1, BK);
+    SPN_ARG(a.K1 == a.K || a.A2 != nullptr, "gemm_nt: second A segment missing");
+    SPN_ARG(a.lda % 4 == 0 && a.ldb % 4 == 0 && (a.K1 == a.K || a.lda2 % 4 == 0), "gemm_nt: leading dims must be /4");
+    SPN_ARG(a.rowbias == nullptr || a.rows_per_ray > 0, "gemm_nt: rows_per_ray");
+    if (a.M == 0) return SPNERF_OK;
+    const int nb = cdiv(a.M, BM) * cdiv(a.N, BN);
+    ProfScope prof("gemm_nt_f32", s, 2.0 * a.M * a.N * a.K, 4.0 * ((double)a.M * a.K + (double)a.N * a.K + 2.0 * a.M * a.N));
+    hipLaunchKernelGGL(k_gemm_nt, dim3(nb), dim3(256), 0, s, a);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+int tn_splits(int P, int N, int K) {
+    const int tiles = cdiv(N, 128) * cdiv(K, 128);
+    int splits = cdiv(1024, tiles);
+    const int max_splits = cdiv(P, 256);
+    if (splits > max_splits) splits = max_splits;
+    return splits < 1 ? 1 : splits;
+}
+
+int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s) {
+    TNArgs a = a0;
+    SPN_ARG(a.N > 0 && a.K > 0 && a.P >= 0, "gemm_tn: bad shape");
+    SPN_ARG(a.N % 4 == 0 && a.K % 4 == 0 && a.K1 % 4 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm_tn: dims must be /4");
+    SPN_ARG(a.K1 == a.K || a.B2 != nullptr, "gemm_tn: second B segment missing");
+    int pps = cdiv(a.P, splits);
+    pps = ((pps + BK - 1) / BK) * BK;
+    a.p_per_split = pps < BK ? BK : pps;
+    const int nb = cdiv(a.N, 128) * cdiv(a.K, 128);
+    ProfScope prof("gemm_tn_f32", s, 2.0 * a.P * a.N * a.K, 4.0 * ((double)a.P * (a.N + a.K) + (double)splits * a.N * a.K));
+    hipLaunchKernelGGL(k_gemm_tn, dim3(nb, splits), dim3(256), 0, s, a);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s) {
+    if (a.nrows <= 0) return SPNERF_OK;
+    const int cols = a.ncols + 1;
+    hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(cols, 128), a.nrows), dim3(128), 0, s, a);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+}  // namespace spn

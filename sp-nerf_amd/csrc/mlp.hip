@@ -1,0 +1,914 @@
+// SP-NeRF per-point network on gfx950: SPNeRF.forward (models/spnerf.py:273-369) and its
+// backward, as a sequence of fp32 MFMA GEMMs (gemm_f32.hip) with fused epilogues plus small
+// per-point / per-ray kernels.
+//
+// Algebraic re-layout (exact up to fp32 summation order):
+//  * the semantic embedding, the sun direction and the time embedding are constant along a
+//    ray, so their input columns of fc_net.0 / fc_net.<2*skip> / sun_v_net.0 / beta_from_xyz.0
+//    become per-RAY bias rows (k_ray_fwd) added in the GEMM epilogue — no repeat_interleave,
+//    no K padding for 63/575/515 wide inputs;
+//  * sky_color depends only on sun_d → evaluated once per ray, broadcast to the points;
+//  * sibling heads that read the same activation are one GEMM: G = H_L·[feat; sem hidden]^T,
+//    Q = feat·[sun hidden 1; rgb hidden; beta hidden]^T;
+//  * N ≤ C-wide output heads (σ, rgb, sun, β, semantic logits) are per-point dot products.
+#include <algorithm>
+#include <vector>
+
+#include "common.h"
+#include "gemm_f32.h"
+#include "mlp_layout.h"
+
+namespace spn {
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+
+struct PackPiece {
+    const float* src;
+    int src_ld, src_c0, rows, cols, dst_ld, transpose;
+    int64_t dst;
+};
+constexpr int kMaxPieces = 24;
+struct PackArgs {
+    PackPiece p[kMaxPieces];
+    float* packed;
+};
+
+__global__ void k_pack(PackArgs a) {
+    const PackPiece pc = a.p[blockIdx.y];
+    const int64_t n = (int64_t)pc.rows * pc.cols;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(i / pc.cols), c = (int)(i % pc.cols);
+        const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
+        if (pc.transpose) a.packed[pc.dst + (int64_t)c * pc.dst_ld + r] = v;
+        else a.packed[pc.dst + (int64_t)r * pc.dst_ld + c] = v;
+    }
+}
+
+// X0[p][c]: positional encoding of xyz = o + dir*z (rendering.py:147; spnerf.py:32-37), one
+// output element per thread.  o + dir*z is evaluated as two rounded ops like the reference
+// (no FMA contraction: sin(2^9 x) amplifies a 1-ulp difference in x by 512).
+__global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, const float* __restrict__ z, int S,
+                         int64_t P, int n_freq, int K0, int K0p, float* __restrict__ X0) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= P * K0p) return;
+    const int64_t p = i / K0p;
+    const int c = (int)(i % K0p);
+    float v = 0.f;
+    if (c < K0) {
+        const float* ray = rays + (p / S) * rs;
+        const float zz = z[p];
+        if (n_freq == 0) {
+            v = __fadd_rn(ray[c], __fmul_rn(ray[dir_off + c], zz));
+        } else {
+            const int k = c / 6, j = c % 6, dim = j % 3;
+            const float x = __fadd_rn(ray[dim], __fmul_rn(ray[dir_off + dim], zz));
+            const float arg = __fmul_rn((float)(1 << k), x);
+            v = j < 3 ? sinf(arg) : cosf(arg);
+        }
+    }
+    X0[i] = v;
+}
+
+struct RayFwdArgs {
+    const float* rays; int rs;
+    const int64_t* labels; const float* temb;
+    const float* packed; Packed k; Dims d;
+    float *rb0, *rb4, *rbQ, *skyh, *sky;
+    int sem_on, need_q, need_sky;
+};
+
+// Per-ray terms: semantic bias rows of fc_net.0 / fc_net.<skip>, sun / t bias rows of the Q
+// GEMM, and the sky_color MLP (spnerf.py:244-249,355).  One 256-thread block per ray.
+__global__ __launch_bounds__(256) void k_ray_fwd(RayFwdArgs a) {
+    const int64_t ray = blockIdx.x;
+    const int tid = threadIdx.x;
+    const Dims& d = a.d;
+    const float* P = a.packed;
+    const float* r = a.rays + ray * a.rs;
+    const float s0 = r[8], s1 = r[9], s2 = r[10];
+    if (a.sem_on) {
+        int64_t lab = a.labels[ray];
+        if (lab == -100) lab = d.C;
+        const float* e = P + a.k.emb + lab * d.sd;
+        for (int n = tid; n < d.W; n += blockDim.x) {
+            float v0 = 0.f, v4 = 0.f;
+            for (int j = 0; j < d.sd; ++j) {
+                v0 += P[a.k.Wsem0 + (int64_t)n * d.sd + j] * e[j];
+                v4 += P[a.k.Wsem4 + (int64_t)n * d.sd + j] * e[j];
+            }
+            a.rb0[ray * d.W + n] = v0;
+            a.rb4[ray * d.W + n] = v4;
+        }
+    }
+    if (a.need_q) {
+        for (int n = tid; n < d.NQ; n += blockDim.x) {
+            float v = 0.f;
+            if (n < d.H) {
+                const float* w = P + a.k.Wsun + n * 3;
+                v = w[0] * s0 + w[1] * s1 + w[2] * s2;
+            } else if (n >= 2 * d.H) {
+                const float* w = P + a.k.Wtt + (int64_t)(n - 2 * d.H) * d.td;
+                const float* t = a.temb + ray * d.td;
+                for (int j = 0; j < d.td; ++j) v += w[j] * t[j];
+            }
+            a.rbQ[ray * d.NQ + n] = v;
+        }
+    }
+    if (a.need_sky) {
+        __shared__ float red[3][256];
+        float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
+        for (int n = tid; n < d.H; n += blockDim.x) {
+            const float* w = P + a.k.Wk1 + n * 3;
+            const float hv = fmaxf(P[a.k.bk1 + n] + (w[0] * s0 + w[1] * s1 + w[2] * s2), 0.f);
+            a.skyh[ray * d.H + n] = hv;
+            acc0 += P[a.k.Wk2 + n] * hv;
+            acc1 += P[a.k.Wk2 + d.H + n] * hv;
+            acc2 += P[a.k.Wk2 + 2 * d.H + n] * hv;
+        }
+        red[0][tid] = acc0;
+        red[1][tid] = acc1;
+        red[2][tid] = acc2;
+        __syncthreads();
+        for (int st = 128; st > 0; st >>= 1) {
+            if (tid < st)
+                for (int c = 0; c < 3; ++c) red[c][tid] += red[c][tid + st];
+            __syncthreads();
+        }
+        if (tid < 3) a.sky[ray * 4 + tid] = sigmoidf_(red[tid][0] + P[a.k.bk2 + tid]);
+    }
+}
+
+__device__ __forceinline__ float dotv(const float* __restrict__ x, const float* __restrict__ w, int n) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (int k = 0; k < n; k += 4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(x + k);
+        s0 += a[0] * w[k];
+        s1 += a[1] * w[k + 1];
+        s2 += a[2] * w[k + 2];
+        s3 += a[3] * w[k + 3];
+    }
+    return (s0 + s1) + (s2 + s3);
+}
+
+struct HeadsArgs {
+    const float* packed; Packed k; Dims d;
+    const float *HL, *G, *Q, *S3, *sky;
+    float* out; float* hsave;
+    int64_t P; int S; int mode;  // mode: 0 full, 1 sigma only, 2 sigma + sun
+};
+
+// Narrow output heads, one thread per point (spnerf.py:333-367): σ = softplus, albedo =
+// sigmoid·1.002−0.001, sun = sigmoid, β = softplus, semantic logits; sky broadcast per ray.
+__global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs a) {
+    const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (p >= a.P) return;
+    const Dims& d = a.d;
+    const float* Pk = a.packed;
+    float* o = a.out + p * d.NO;
+    float* hs = a.hsave + p * 8;
+    const float spre = dotv(a.HL + p * d.W, Pk + a.k.wsig, d.W) + Pk[a.k.bsig];
+    o[3] = softplusf_(spre);
+    hs[0] = spre;
+    if (a.mode == 1) return;
+    const float sun = sigmoidf_(dotv(a.S3 + p * d.H, Pk + a.k.ws4, d.H) + Pk[a.k.bs4]);
+    o[4] = sun;
+    hs[4] = sun;
+    if (a.mode == 2) {
+        o[0] = o[1] = o[2] = o[5] = o[6] = o[7] = 0.f;
+        for (int c = 8; c < d.NO; ++c) o[c] = 0.f;
+        return;
+    }
+    const float* R1 = a.Q + p * d.NQ + d.H;
+    for (int c = 0; c < 3; ++c) {
+        const float s = sigmoidf_(dotv(R1, Pk + a.k.Wr2 + c * d.H, d.H) + Pk[a.k.br2 + c]);
+        hs[1 + c] = s;
+        o[c] = __fsub_rn(__fmul_rn(s, 1.002f), 0.001f);
+    }
+    const float* sk = a.sky + (p / a.S) * 4;
+    o[5] = sk[0];
+    o[6] = sk[1];
+    o[7] = sk[2];
+    if (d.beta) {
+        const float bpre = dotv(a.Q + p * d.NQ + 2 * d.H, Pk + a.k.wb2, d.H) + Pk[a.k.bb2];
+        hs[5] = bpre;
+        o[8] = softplusf_(bpre);
+    }
+    if (d.sem) {
+        const float* M1 = a.G + p * d.NG + d.W;
+        for (int c = 0; c < d.C; ++c) o[d.sem_col + c] = dotv(M1, Pk + a.k.Wm2 + c * d.H, d.H) + Pk[a.k.bm2 + c];
+    }
+}
+
+struct HeadsBwdArgs {
+    const float* packed; Packed k; Dims d;
+    const float *d_out, *hsave, *DQ, *DG, *DS3;
+    float *hpre, *dZQ, *dZG, *dS3;
+    int64_t P; int mode;
+};
+
+// Backward of the narrow heads, one thread per point: per-point pre-activation gradients
+// (hpre, reduced over points into the head weights by k_tn_skinny) and the gradients of the
+// wide hidden layers that feed them (torch: Linear → dX = dY·W, then × sin' saved in D*).
+__global__ __launch_bounds__(256) void k_heads_bwd(HeadsBwdArgs a) {
+    const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (p >= a.P) return;
+    const Dims& d = a.d;
+    const float* Pk = a.packed;
+    const float* g = a.d_out + p * d.NO;
+    const float* hs = a.hsave + p * 8;
+    float* hp = a.hpre + p * d.HP;
+    for (int c = 0; c < d.HP; ++c) hp[c] = 0.f;
+    hp[0] = softplus_grad(g[3], hs[0]);
+    if (a.mode == 1) return;
+    {
+        const float s = hs[4];
+        const float dys = g[4] * (1.f - s) * s;
+        hp[4] = dys;
+        const float* D = a.DS3 + p * d.H;
+        float* o = a.dS3 + p * d.H;
+        const float* w = Pk + a.k.ws4;
+        for (int k = 0; k < d.H; k += 4) {
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(D + k);
+            f32x4 r;
+            for (int q = 0; q < 4; ++q) r[q] = dys * w[k + q] * dv[q];
+            *reinterpret_cast<f32x4*>(o + k) = r;
+        }
+    }
+    if (a.mode == 2) return;
+    float dy[3];
+    for (int c = 0; c < 3; ++c) {
+        const float s = hs[1 + c];
+        dy[c] = g[c] * 1.002f * (1.f - s) * s;
+        hp[1 + c] = dy[c];
+    }
+    {
+        const float* D = a.DQ + p * d.NQ + d.H;
+        float* o = a.dZQ + p * d.NQ + d.H;
+        const float* w = Pk + a.k.Wr2;
+        for (int k = 0; k < d.H; k += 4) {
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(D + k);
+            f32x4 r;
+            for (int q = 0; q < 4; ++q)
+                r[q] = (dy[0] * w[k + q] + dy[1] * w[d.H + k + q] + dy[2] * w[2 * d.H + k + q]) * dv[q];
+            *reinterpret_cast<f32x4*>(o + k) = r;
+        }
+    }
+    if (d.beta) {
+        const float db = softplus_grad(g[8], hs[5]);
+        hp[5] = db;
+        const float* D = a.DQ + p * d.NQ + 2 * d.H;
+        float* o = a.dZQ + p * d.NQ + 2 * d.H;
+        const float* w = Pk + a.k.wb2;
+        for (int k = 0; k < d.H; k += 4) {
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(D + k);
+            f32x4 r;
+            for (int q = 0; q < 4; ++q) r[q] = db * w[k + q] * dv[q];
+            *reinterpret_cast<f32x4*>(o + k) = r;
+        }
+    }
+    if (d.sem) {
+        float gs[32];
+        for (int c = 0; c < d.C; ++c) {
+            gs[c] = g[d.sem_col + c];
+            hp[6 + c] = gs[c];
+        }
+        const float* D = a.DG + p * d.NG + d.W;
+        float* o = a.dZG + p * d.NG + d.W;
+        const float* w = Pk + a.k.Wm2;
+        for (int k = 0; k < d.H; ++k) {
+            float v = 0.f;
+            for (int c = 0; c < d.C; ++c) v += gs[c] * w[c * d.H + k];
+            o[k] = v * D[k];
+        }
+    }
+}
+
+// slab[chunk][m][k] = Σ_{p in chunk} A[p*lda + m] * B[p*ldb + k]   (m < Ma ≤ 8)
+// slab_b[chunk][m]  = Σ_{p in chunk} A[p*lda + m]
+__global__ __launch_bounds__(256) void k_tn_skinny(const float* __restrict__ A, int lda, int Ma,
+                                                   const float* __restrict__ B, int ldb, int K, int64_t P,
+                                                   int chunk, float* __restrict__ slab, float* __restrict__ slab_b) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t p0 = (int64_t)blockIdx.y * chunk;
+    const int64_t p1 = min(P, p0 + chunk);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (k < K) {
+        for (int64_t p = p0; p < p1; ++p) {
+            const float b = B[p * ldb + k];
+            const float* ar = A + p * lda;
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+                if (m < Ma) acc[m] += ar[m] * b;
+        }
+        for (int m = 0; m < Ma; ++m) slab[((int64_t)blockIdx.y * Ma + m) * K + k] = acc[m];
+    }
+    if (blockIdx.x == 0 && threadIdx.x < Ma) {
+        float s = 0.f;
+        for (int64_t p = p0; p < p1; ++p) s += A[p * lda + threadIdx.x];
+        slab_b[(int64_t)blockIdx.y * Ma + threadIdx.x] = s;
+    }
+}
+
+// out[ray][n] = Σ_{s<S} in[(ray*S + s)*ld + c0 + n]
+__global__ void k_ray_rowsum(const float* __restrict__ in, int ld, int c0, int N, int S, float* __restrict__ out,
+                             int ldo) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ray = blockIdx.y;
+    if (n >= N) return;
+    const float* p = in + ray * S * (int64_t)ld + c0 + n;
+    float s = 0.f;
+    for (int i = 0; i < S; ++i) s += p[(int64_t)i * ld];
+    out[ray * ldo + n] = s;
+}
+
+struct RayBwdArgs {
+    const float* packed; Packed k; Dims d;
+    const float *sky, *skyh, *dsky, *R0, *R4, *RQ;
+    float *skyd, *skydh, *gemb, *grad_t;
+    int sem_on, beta_on, sky_on;
+};
+
+// Per-ray backward pieces: sky MLP pre-activation grads, the semantic-embedding input grad
+// and the time-embedding input grad.  One 256-thread block per ray.
+__global__ __launch_bounds__(256) void k_ray_bwd(RayBwdArgs a) {
+    const int64_t ray = blockIdx.x;
+    const int tid = threadIdx.x;
+    const Dims& d = a.d;
+    const float* P = a.packed;
+    if (a.sky_on) {
+        float dp[3];
+        for (int c = 0; c < 3; ++c) {
+            const float s = a.sky[ray * 4 + c];
+            dp[c] = a.dsky[ray * 4 + c] * (1.f - s) * s;
+        }
+        if (tid < 3) a.skyd[ray * 4 + tid] = dp[tid];
+        for (int n = tid; n < d.H; n += blockDim.x) {
+            const float hv = a.skyh[ray * d.H + n];
+            const float g = dp[0] * P[a.k.Wk2 + n] + dp[1] * P[a.k.Wk2 + d.H + n] + dp[2] * P[a.k.Wk2 + 2 * d.H + n];
+            a.skydh[ray * d.H + n] = hv > 0.f ? g : 0.f;
+        }
+    }
+    __shared__ float red[256];
+    if (a.sem_on) {
+        for (int j = 0; j < d.sd; ++j) {
+            float acc = 0.f;
+            for (int n = tid; n < d.W; n += blockDim.x)
+                acc += a.R0[ray * d.W + n] * P[a.k.Wsem0 + (int64_t)n * d.sd + j] +
+                       a.R4[ray * d.W + n] * P[a.k.Wsem4 + (int64_t)n * d.sd + j];
+            red[tid] = acc;
+            __syncthreads();
+            for (int st = 128; st > 0; st >>= 1) {
+                if (tid < st) red[tid] += red[tid + st];
+                __syncthreads();
+            }
+            if (tid == 0) a.gemb[ray * d.sd + j] = red[0];
+            __syncthreads();
+        }
+    }
+    if (a.beta_on && a.grad_t) {
+        for (int j = 0; j < d.td; ++j) {
+            float acc = 0.f;
+            for (int n = tid; n < d.H; n += blockDim.x)
+                acc += a.RQ[ray * d.NQ + 2 * d.H + n] * P[a.k.Wtt + (int64_t)n * d.td + j];
+            red[tid] = acc;
+            __syncthreads();
+            for (int st = 128; st > 0; st >>= 1) {
+                if (tid < st) red[tid] += red[tid + st];
+                __syncthreads();
+            }
+            if (tid == 0) a.grad_t[ray * d.td + j] = red[0];
+            __syncthreads();
+        }
+    }
+}
+
+// out[n*ldo + j] = Σ_ray X[ray*ldx + n] * Y[row(ray)*ldy + j]   (Y == nullptr → Σ_ray X[ray][n])
+// row(ray) = ray, or the embedding row of the ray's label when `labels` is given.
+__global__ void k_ray_outer(int64_t B, const float* __restrict__ X, int ldx, int N, const float* __restrict__ Y,
+                            int ldy, int J, const int64_t* __restrict__ labels, int pad_row, float* __restrict__ out,
+                            int ldo) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int Jn = Y ? J : 1;
+    if (i >= N * Jn) return;
+    const int n = i / Jn, j = i % Jn;
+    float s = 0.f;
+    for (int64_t r = 0; r < B; ++r) {
+        float y = 1.f;
+        if (Y) {
+            int64_t row = r;
+            if (labels) {
+                row = labels[r];
+                if (row == -100) row = pad_row;
+            }
+            y = Y[row * ldy + j];
+        }
+        s += X[r * ldx + n] * y;
+    }
+    out[(int64_t)n * ldo + j] = s;
+}
+
+// d_emb[c][j] = Σ_{rays with label c} gemb[ray][j]; the padding row (−100 → C) gets none
+// (nn.Embedding padding_idx, spnerf.py:191-194).
+__global__ void k_class_sum(int64_t B, const float* __restrict__ gemb, int sd, const int64_t* __restrict__ labels,
+                            int C, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (C + 1) * sd) return;
+    const int c = i / sd, j = i % sd;
+    float s = 0.f;
+    if (c < C)
+        for (int64_t r = 0; r < B; ++r)
+            if (labels[r] == c) s += gemb[r * sd + j];
+    out[i] = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// host orchestration
+// ------------------------------------------------------------------------------------------
+
+static int32_t launch_pack(const std::vector<PackPiece>& pieces, float* packed, hipStream_t s) {
+    for (size_t b = 0; b < pieces.size(); b += kMaxPieces) {
+        PackArgs a{};
+        a.packed = packed;
+        int n = 0;
+        int64_t maxe = 1;
+        for (size_t i = b; i < pieces.size() && n < kMaxPieces; ++i, ++n) {
+            a.p[n] = pieces[i];
+            maxe = std::max(maxe, (int64_t)pieces[i].rows * pieces[i].cols);
+        }
+        const int gx = (int)std::min<int64_t>((maxe + 255) / 256, 1024);
+        hipLaunchKernelGGL(k_pack, dim3(gx, n), dim3(256), 0, s, a);
+        SPN_HIP(hipGetLastError());
+    }
+    return SPNERF_OK;
+}
+
+static int32_t pack_params(const Dims& d, const float* const* prm, float* packed, hipStream_t s) {
+    PIdx x;
+    auto specs = param_specs(d, &x);
+    const Packed k = packed_layout(d);
+    std::vector<PackPiece> v;
+    auto piece = [&](int pi, int c0, int rows, int cols, int64_t dst, int dst_ld, int tr) {
+        SPN_ARG(prm[pi] != nullptr, "parameter %s is NULL", specs[pi].name.c_str());
+        v.push_back(PackPiece{prm[pi], (int)specs[pi].ld(), c0, rows, cols, dst_ld, tr, dst});
+        return SPNERF_OK;
+    };
+    const int W = d.W, H = d.H;
+    for (int i = 0; i < d.L; ++i) {
+        const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
+        SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wt[i], k.Kp[i], 0));
+        SPN_TRY(piece(x.fcb[i], 0, 1, W, k.bt[i], W, 0));
+        if (i > 0) SPN_TRY(piece(x.fcW[i], 0, W, W, k.WTt[i], W, 1));
+    }
+    if (d.sem) {
+        SPN_TRY(piece(x.fcW[0], d.K0, W, d.sd, k.Wsem0, d.sd, 0));
+        SPN_TRY(piece(x.fcW[d.skip], W + d.K0, W, d.sd, k.Wsem4, d.sd, 0));
+        SPN_TRY(piece(x.emb, 0, d.C + 1, d.sd, k.emb, d.sd, 0));
+        SPN_TRY(piece(x.m1W, 0, H, W, k.WG + (int64_t)W * W, W, 0));
+        SPN_TRY(piece(x.m1b, 0, 1, H, k.bG + W, H, 0));
+        SPN_TRY(piece(x.m1W, 0, H, W, k.WGT + W, d.NG, 1));
+        SPN_TRY(piece(x.m2W, 0, d.C, H, k.Wm2, H, 0));
+        SPN_TRY(piece(x.m2b, 0, 1, d.C, k.bm2, d.C, 0));
+    }
+    SPN_TRY(piece(x.featW, 0, W, W, k.WG, W, 0));
+    SPN_TRY(piece(x.featb, 0, 1, W, k.bG, W, 0));
+    SPN_TRY(piece(x.featW, 0, W, W, k.WGT, d.NG, 1));
+    SPN_TRY(piece(x.s1W, 0, H, W, k.WQ, W, 0));
+    SPN_TRY(piece(x.r1W, 0, H, W, k.WQ + (int64_t)H * W, W, 0));
+    SPN_TRY(piece(x.s1b, 0, 1, H, k.bQ, H, 0));
+    SPN_TRY(piece(x.r1b, 0, 1, H, k.bQ + H, H, 0));
+    SPN_TRY(piece(x.s1W, 0, H, W, k.WQT, d.NQ, 1));
+    SPN_TRY(piece(x.r1W, 0, H, W, k.WQT + H, d.NQ, 1));
+    SPN_TRY(piece(x.s1W, W, H, 3, k.Wsun, 3, 0));
+    if (d.beta) {
+        SPN_TRY(piece(x.b1W, 0, H, W, k.WQ + (int64_t)2 * H * W, W, 0));
+        SPN_TRY(piece(x.b1b, 0, 1, H, k.bQ + 2 * H, H, 0));
+        SPN_TRY(piece(x.b1W, 0, H, W, k.WQT + 2 * H, d.NQ, 1));
+        SPN_TRY(piece(x.b1W, W, H, d.td, k.Wtt, d.td, 0));
+        SPN_TRY(piece(x.b2W, 0, 1, H, k.wb2, H, 0));
+        SPN_TRY(piece(x.b2b, 0, 1, 1, k.bb2, 1, 0));
+    }
+    SPN_TRY(piece(x.s2W, 0, H, H, k.Ws2, H, 0));
+    SPN_TRY(piece(x.s2b, 0, 1, H, k.bs2, H, 0));
+    SPN_TRY(piece(x.s2W, 0, H, H, k.Ws2T, H, 1));
+    SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3, H, 0));
+    SPN_TRY(piece(x.s3b, 0, 1, H, k.bs3, H, 0));
+    SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3T, H, 1));
+    SPN_TRY(piece(x.sigW, 0, 1, W, k.wsig, W, 0));
+    SPN_TRY(piece(x.sigb, 0, 1, 1, k.bsig, 1, 0));
+    SPN_TRY(piece(x.r2W, 0, 3, H, k.Wr2, H, 0));
+    SPN_TRY(piece(x.r2b, 0, 1, 3, k.br2, 3, 0));
+    SPN_TRY(piece(x.s4W, 0, 1, H, k.ws4, H, 0));
+    SPN_TRY(piece(x.s4b, 0, 1, 1, k.bs4, 1, 0));
+    SPN_TRY(piece(x.k1W, 0, H, 3, k.Wk1, 3, 0));
+    SPN_TRY(piece(x.k1b, 0, 1, H, k.bk1, H, 0));
+    SPN_TRY(piece(x.k2W, 0, 3, H, k.Wk2, H, 0));
+    SPN_TRY(piece(x.k2b, 0, 1, 3, k.bk2, 3, 0));
+    return launch_pack(v, packed, s);
+}
+
+namespace {
+struct Ctx {
+    Dims d;
+    Packed k;
+    WS w;
+    const float* P;  // packed
+    float* ws;       // workspace base
+    int S;
+    float* at(int64_t off) const { return ws + off; }
+    const float* pk(int64_t off) const { return P + off; }
+};
+}  // namespace
+
+static int32_t tn_grad(const Ctx& c, const float* A, int lda, int N, const float* B, int ldb, const float* B2, int ldb2,
+                       int K1, int K, hipStream_t s, std::initializer_list<ReduceArgs> outs) {
+    const int P = (int)c.w.P;
+    const int splits = tn_splits(P, N, K);
+    TNArgs t;
+    t.A = A; t.lda = lda;
+    t.B = B; t.ldb = ldb; t.B2 = B2; t.ldb2 = ldb2; t.K1 = K1;
+    t.slab = c.at(c.w.slab); t.ld_slab = K; t.slab_stride = (int64_t)N * K;
+    t.slab_b = c.at(c.w.slab_b);
+    t.P = P; t.N = N; t.K = K;
+    SPN_TRY(gemm_tn(t, splits, s));
+    for (ReduceArgs r : outs) {
+        r.slab = t.slab; r.ld_slab = K; r.slab_stride = t.slab_stride; r.splits = splits; r.N = N;
+        r.slab_b = t.slab_b;
+        SPN_TRY(reduce_slabs(r, s));
+    }
+    return SPNERF_OK;
+}
+
+static ReduceArgs red(int row0, int nrows, int ncols, float* dst, int ld_dst, float* dst_b) {
+    ReduceArgs r;
+    r.row0 = row0; r.nrows = nrows; r.ncols = ncols; r.dst = dst; r.ld_dst = ld_dst; r.dst_b = dst_b;
+    return r;
+}
+
+static int32_t skinny(const Ctx& c, const float* A, int lda, int Ma, const float* B, int ldb, int K, float* dstW,
+                      float* dstb, hipStream_t s) {
+    const int64_t P = c.w.P;
+    const int chunk = 2048;
+    const int chunks = cdiv(P, chunk);
+    float* slab = c.at(c.w.sk_slab);
+    float* slab_b = c.at(c.w.sk_slab_b);
+    hipLaunchKernelGGL(k_tn_skinny, dim3(cdiv(K, 256), chunks), dim3(256), 0, s, A, lda, Ma, B, ldb, K, P, chunk, slab,
+                       slab_b);
+    SPN_HIP(hipGetLastError());
+    ReduceArgs r = red(0, Ma, K, dstW, K, dstb);
+    r.slab = slab; r.ld_slab = K; r.slab_stride = (int64_t)Ma * K; r.splits = chunks; r.N = Ma; r.slab_b = slab_b;
+    return reduce_slabs(r, s);
+}
+
+static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays, int rs, int dir_off,
+                           int64_t n_rays, int S, const float* z, const int64_t* labels, const float* temb, int flags,
+                           float* ws, float* out, hipStream_t s) {
+    Ctx c{d, packed_layout(d), ws_layout(d, n_rays, S, flags), packed, ws, S};
+    const bool save = flags & SPNERF_MLP_SAVE;
+    const int mode = (flags & SPNERF_MLP_SIGMA_ONLY) ? 1 : ((flags & SPNERF_MLP_SUN_ONLY) ? 2 : 0);
+    const int64_t P = n_rays * S;
+    const int W = d.W, H = d.H;
+    if (P == 0) return SPNERF_OK;
+    SPN_ARG(P < (1ll << 31) / std::max(d.NQ, d.NG), "too many points (%lld) for one call", (long long)P);
+    SPN_ARG(!d.sem || labels, "semantic model needs labels");
+    SPN_ARG(!d.beta || mode != 0 || temb, "beta model needs t_emb");
+
+    // per-ray terms
+    {
+        RayFwdArgs a{rays, rs, labels, temb, packed, c.k, d, c.at(c.w.rb0), c.at(c.w.rb4), c.at(c.w.rbQ),
+                     c.at(c.w.skyh), c.at(c.w.sky), d.sem ? 1 : 0, mode != 1, mode == 0};
+        if (d.beta && mode == 0) {
+        } else {
+            a.d.beta = false;
+            a.d.td = 0;
+        }
+        if (d.sem || mode != 1) {
+            hipLaunchKernelGGL(k_ray_fwd, dim3((unsigned)n_rays), dim3(256), 0, s, a);
+            SPN_HIP(hipGetLastError());
+        }
+    }
+    // positional encoding
+    {
+        const int64_t n = P * d.K0p;
+        ProfScope prof("encode", s, 0.0, 4.0 * n);
+        hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rays, rs, dir_off, z, S, P,
+                           d.K0 == 3 ? 0 : d.K0 / 6, d.K0, d.K0p, c.at(c.w.X0));
+        SPN_HIP(hipGetLastError());
+    }
+    // trunk
+    const float* X0 = c.at(c.w.X0);
+    const float* h = X0;
+    int ldh = d.K0p;
+    float* HL = nullptr;
+    for (int i = 0; i < d.L; ++i) {
+        float* dst = save ? c.at(c.w.Hb[i]) : c.at(c.w.Hb[i & 1]);
+        NTArgs g;
+        if (i == d.skip) {
+            g.A = h; g.lda = ldh; g.A2 = X0; g.lda2 = d.K0p; g.K1 = W;
+        } else {
+            g.A = h; g.lda = ldh; g.K1 = c.k.Kp[i];
+        }
+        g.B = c.pk(c.k.Wt[i]); g.ldb = c.k.Kp[i];
+        g.C = dst; g.ldc = W;
+        g.M = (int)P; g.N = W; g.K = c.k.Kp[i];
+        g.bias = c.pk(c.k.bt[i]);
+        if (d.sem && (i == 0 || i == d.skip)) {
+            g.rowbias = c.at(i == 0 ? c.w.rb0 : c.w.rb4); g.ld_rb = W; g.rows_per_ray = S;
+        }
+        g.act = 1; g.w0 = i == 0 ? 30.f : 1.f; g.n_lin = 0;
+        if (save) { g.Dout = c.at(c.w.Db[i]); g.ld_dout = W; }
+        SPN_TRY(gemm_nt(g, s));
+        h = dst;
+        ldh = W;
+        HL = dst;
+    }
+    float* S2buf = save ? c.at(c.w.S2) : c.at(c.w.Hb[((d.L - 1) & 1) ^ 1]);
+    float* S3buf = save ? c.at(c.w.S3) : c.at(c.w.Hb[2]);
+    if (mode != 1) {
+        // G = H_L · [feat ; sem hidden]^T   (feat linear, sem hidden sin)
+        const int NG = mode == 0 ? d.NG : W;
+        NTArgs g;
+        g.A = HL; g.lda = W; g.K1 = W;
+        g.B = c.pk(c.k.WG); g.ldb = W;
+        g.C = c.at(c.w.G); g.ldc = d.NG;
+        g.M = (int)P; g.N = NG; g.K = W;
+        g.bias = c.pk(c.k.bG);
+        g.act = 1; g.w0 = 1.f; g.n_lin = W;
+        if (save) { g.Dout = c.at(c.w.DG); g.ld_dout = d.NG; }
+        SPN_TRY(gemm_nt(g, s));
+        // Q = feat · [sun1 ; rgb1 ; beta1]^T + per-ray (sun_d / t) rows, all sin
+        const int NQ = mode == 0 ? d.NQ : H;
+        NTArgs q;
+        q.A = c.at(c.w.G); q.lda = d.NG; q.K1 = W;
+        q.B = c.pk(c.k.WQ); q.ldb = W;
+        q.C = c.at(c.w.Q); q.ldc = d.NQ;
+        q.M = (int)P; q.N = NQ; q.K = W;
+        q.bias = c.pk(c.k.bQ);
+        q.rowbias = c.at(c.w.rbQ); q.ld_rb = d.NQ; q.rows_per_ray = S;
+        q.act = 1; q.w0 = 1.f;
+        if (save) { q.Dout = c.at(c.w.DQ); q.ld_dout = d.NQ; }
+        SPN_TRY(gemm_nt(q, s));
+        // sun_v_net layers 2 and 3
+        NTArgs s2;
+        s2.A = c.at(c.w.Q); s2.lda = d.NQ; s2.K1 = H;
+        s2.B = c.pk(c.k.Ws2); s2.ldb = H;
+        s2.C = S2buf; s2.ldc = H;
+        s2.M = (int)P; s2.N = H; s2.K = H;
+        s2.bias = c.pk(c.k.bs2); s2.act = 1; s2.w0 = 1.f;
+        if (save) { s2.Dout = c.at(c.w.DS2); s2.ld_dout = H; }
+        SPN_TRY(gemm_nt(s2, s));
+        NTArgs s3 = s2;
+        s3.A = S2buf; s3.lda = H;
+        s3.B = c.pk(c.k.Ws3);
+        s3.C = S3buf;
+        s3.bias = c.pk(c.k.bs3);
+        s3.Dout = save ? c.at(c.w.DS3) : nullptr;
+        SPN_TRY(gemm_nt(s3, s));
+    }
+    {
+        HeadsArgs a{packed, c.k, d, HL, c.at(c.w.G), c.at(c.w.Q), S3buf, c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode};
+        ProfScope prof("heads_fwd", s, 2.0 * P * (W + (mode != 1 ? 4 * H + H * d.C : 0)), 4.0 * P * (W + 3 * H + d.NO));
+        hipLaunchKernelGGL(k_heads_fwd, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, a);
+        SPN_HIP(hipGetLastError());
+    }
+    return SPNERF_OK;
+}
+
+static int32_t mlp_backward(const Dims& d, const float* packed, const float* rays, int rs, int64_t n_rays, int S,
+                            const int64_t* labels, const float* temb, int flags, float* ws, const float* d_out,
+                            float* grad, float* grad_t, hipStream_t s) {
+    SPN_ARG(flags & SPNERF_MLP_SAVE, "backward needs a workspace written with SPNERF_MLP_SAVE");
+    SPN_ARG(!(flags & SPNERF_MLP_SIGMA_ONLY), "backward of a sigma-only pass is not supported");
+    Ctx c{d, packed_layout(d), ws_layout(d, n_rays, S, flags), packed, ws, S};
+    const int mode = (flags & SPNERF_MLP_SUN_ONLY) ? 2 : 0;
+    const int64_t P = n_rays * S;
+    const int W = d.W, H = d.H;
+    PIdx x;
+    auto specs = param_specs(d, &x);
+    const int64_t total = specs.back().off + specs.back().numel();
+    SPN_HIP(hipMemsetAsync(grad, 0, total * sizeof(float), s));
+    if (grad_t && d.beta) SPN_HIP(hipMemsetAsync(grad_t, 0, n_rays * d.td * sizeof(float), s));
+    if (P == 0) return SPNERF_OK;
+    auto gp = [&](int pi) { return grad + specs[pi].off; };
+    auto ld = [&](int pi) { return (int)specs[pi].ld(); };
+
+    float* HL = c.at(c.w.Hb[d.L - 1]);
+    float* Gb = c.at(c.w.G);
+    float* Qb = c.at(c.w.Q);
+    float* dZG = c.at(c.w.dZG);
+    float* dZQ = c.at(c.w.dZQ);
+    float* dS3 = c.at(c.w.dS3);
+    float* dS2 = c.at(c.w.dS2);
+    float* hpre = c.at(c.w.hpre);
+
+    // 1. narrow heads
+    {
+        HeadsBwdArgs a{packed, c.k, d, d_out, c.at(c.w.hsave), c.at(c.w.DQ), c.at(c.w.DG), c.at(c.w.DS3),
+                       hpre, dZQ, dZG, dS3, P, mode};
+        ProfScope prof("heads_bwd", s, 2.0 * P * 4 * H, 4.0 * P * (d.NO + 3 * H + 3 * H));
+        hipLaunchKernelGGL(k_heads_bwd, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, a);
+        SPN_HIP(hipGetLastError());
+    }
+    // 2. narrow-head weights: reductions over points
+    SPN_TRY(skinny(c, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), gp(x.sigb), s));
+    SPN_TRY(skinny(c, hpre + 4, d.HP, 1, c.at(c.w.S3), H, H, gp(x.s4W), gp(x.s4b), s));
+    if (mode == 0) {
+        SPN_TRY(skinny(c, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), gp(x.r2b), s));
+        if (d.beta) SPN_TRY(skinny(c, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), gp(x.b2b), s));
+        if (d.sem) SPN_TRY(skinny(c, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), gp(x.m2b), s));
+    }
+    // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
+    {
+        NTArgs g;
+        g.A = dS3; g.lda = H; g.K1 = H; g.B = c.pk(c.k.Ws3T); g.ldb = H; g.C = dS2; g.ldc = H;
+        g.M = (int)P; g.N = H; g.K = H; g.Dmul = c.at(c.w.DS2); g.ld_dmul = H;
+        SPN_TRY(gemm_nt(g, s));
+        SPN_TRY(tn_grad(c, dS3, H, H, c.at(c.w.S2), H, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}));
+        NTArgs g2 = g;
+        g2.A = dS2; g2.B = c.pk(c.k.Ws2T); g2.C = dZQ; g2.ldc = d.NQ; g2.Dmul = c.at(c.w.DQ); g2.ld_dmul = d.NQ;
+        SPN_TRY(gemm_nt(g2, s));
+        SPN_TRY(tn_grad(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
+    }
+    // 4. feat: dF = dZ_Q · WQ → dZG[:, :W];  dWQ = dZ_Q^T · feat
+    const int NQ = mode == 0 ? d.NQ : H;
+    {
+        NTArgs g;
+        g.A = dZQ; g.lda = d.NQ; g.K1 = NQ; g.B = c.pk(c.k.WQT); g.ldb = d.NQ; g.C = dZG; g.ldc = d.NG;
+        g.M = (int)P; g.N = W; g.K = NQ;
+        SPN_TRY(gemm_nt(g, s));
+        if (mode == 0) {
+            std::vector<ReduceArgs> outs = {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)),
+                                            red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b))};
+            if (d.beta) outs.push_back(red(2 * H, H, W, gp(x.b1W), ld(x.b1W), gp(x.b1b)));
+            const int splits = tn_splits((int)P, NQ, W);
+            TNArgs t;
+            t.A = dZQ; t.lda = d.NQ; t.B = Gb; t.ldb = d.NG; t.K1 = W;
+            t.slab = c.at(c.w.slab); t.ld_slab = W; t.slab_stride = (int64_t)NQ * W; t.slab_b = c.at(c.w.slab_b);
+            t.P = (int)P; t.N = NQ; t.K = W;
+            SPN_TRY(gemm_tn(t, splits, s));
+            for (ReduceArgs r : outs) {
+                r.slab = t.slab; r.ld_slab = W; r.slab_stride = t.slab_stride; r.splits = splits; r.N = NQ; r.slab_b = t.slab_b;
+                SPN_TRY(reduce_slabs(r, s));
+            }
+        } else {
+            SPN_TRY(tn_grad(c, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
+        }
+        // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns
+        hipLaunchKernelGGL(k_ray_rowsum, dim3(cdiv(NQ, 256), (unsigned)n_rays), dim3(256), 0, s, dZQ, d.NQ, 0, NQ, S,
+                           c.at(c.w.RQ), d.NQ);
+        SPN_HIP(hipGetLastError());
+    }
+    // 5. H_L: dH_L = dZ_G · WG + dσ ⊗ w_σ ;  dZ_{L-1} = dH_L ⊙ D_L ;  dWG = dZ_G^T · H_L
+    const int NG = mode == 0 ? d.NG : W;
+    float* dZ = c.at(c.w.dZa);
+    float* dZn = c.at(c.w.dZb);
+    {
+        NTArgs g;
+        g.A = dZG; g.lda = d.NG; g.K1 = NG; g.B = c.pk(c.k.WGT); g.ldb = d.NG; g.C = dZ; g.ldc = W;
+        g.M = (int)P; g.N = W; g.K = NG;
+        g.r1_a = hpre; g.r1_lda = d.HP; g.r1_v = c.pk(c.k.wsig);
+        g.Dmul = c.at(c.w.Db[d.L - 1]); g.ld_dmul = W;
+        SPN_TRY(gemm_nt(g, s));
+        if (mode == 0 && d.sem)
+            SPN_TRY(tn_grad(c, dZG, d.NG, d.NG, HL, W, nullptr, 0, W, W, s,
+                            {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
+        else
+            SPN_TRY(tn_grad(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
+    }
+    // 6. trunk, top to bottom
+    for (int i = d.L - 1; i >= 0; --i) {
+        // dZ holds dL/d(pre-activation of layer i)
+        const float* In = i == 0 ? c.at(c.w.X0) : c.at(c.w.Hb[i - 1]);
+        const int ldin = i == 0 ? d.K0p : W;
+        const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
+        if (i == d.skip)
+            SPN_TRY(tn_grad(c, dZ, W, W, In, W, c.at(c.w.X0), d.K0p, W, W + d.K0p, s,
+                            {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
+        else
+            SPN_TRY(tn_grad(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s,
+                            {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
+        if (d.sem && (i == 0 || i == d.skip)) {
+            hipLaunchKernelGGL(k_ray_rowsum, dim3(cdiv(W, 256), (unsigned)n_rays), dim3(256), 0, s, dZ, W, 0, W, S,
+                               c.at(i == 0 ? c.w.R0 : c.w.R4), W);
+            SPN_HIP(hipGetLastError());
+        }
+        if (i > 0) {
+            NTArgs g;
+            g.A = dZ; g.lda = W; g.K1 = W; g.B = c.pk(c.k.WTt[i]); g.ldb = W; g.C = dZn; g.ldc = W;
+            g.M = (int)P; g.N = W; g.K = W; g.Dmul = c.at(c.w.Db[i - 1]); g.ld_dmul = W;
+            SPN_TRY(gemm_nt(g, s));
+            std::swap(dZ, dZn);
+        }
+    }
+    // 7. per-ray parameters: sun-direction columns, t columns, sky MLP, semantic embedding
+    {
+        const int sky_on = mode == 0;
+        if (sky_on) {
+            hipLaunchKernelGGL(k_ray_rowsum, dim3(1, (unsigned)n_rays), dim3(256), 0, s, d_out, d.NO, 5, 3, S,
+                               c.at(c.w.dsky), 4);
+            SPN_HIP(hipGetLastError());
+        }
+        RayBwdArgs a{packed, c.k, d, c.at(c.w.sky), c.at(c.w.skyh), c.at(c.w.dsky), c.at(c.w.R0), c.at(c.w.R4),
+                     c.at(c.w.RQ), c.at(c.w.skyd), c.at(c.w.skydh), c.at(c.w.gemb), grad_t,
+                     d.sem ? 1 : 0, (d.beta && mode == 0) ? 1 : 0, sky_on};
+        hipLaunchKernelGGL(k_ray_bwd, dim3((unsigned)n_rays), dim3(256), 0, s, a);
+        SPN_HIP(hipGetLastError());
+        const float* sun = rays + 8;
+        auto outer = [&](const float* X, int ldx, int N, const float* Y, int ldy, int J, const int64_t* lab, float* o, int ldo) {
+            const int n = N * (Y ? J : 1);
+            hipLaunchKernelGGL(k_ray_outer, dim3(cdiv(n, 128)), dim3(128), 0, s, n_rays, X, ldx, N, Y, ldy, J, lab, d.C, o, ldo);
+            return hipGetLastError();
+        };
+        SPN_HIP(outer(c.at(c.w.RQ), d.NQ, H, sun, rs, 3, nullptr, gp(x.s1W) + W, ld(x.s1W)));
+        if (sky_on) {
+            SPN_HIP(outer(c.at(c.w.skydh), H, H, sun, rs, 3, nullptr, gp(x.k1W), 3));
+            SPN_HIP(outer(c.at(c.w.skydh), H, H, nullptr, 0, 1, nullptr, gp(x.k1b), 1));
+            SPN_HIP(outer(c.at(c.w.skyd), 4, 3, c.at(c.w.skyh), H, H, nullptr, gp(x.k2W), H));
+            SPN_HIP(outer(c.at(c.w.skyd), 4, 3, nullptr, 0, 1, nullptr, gp(x.k2b), 1));
+        }
+        if (d.beta && mode == 0)
+            SPN_HIP(outer(c.at(c.w.RQ) + 2 * H, d.NQ, H, temb, d.td, d.td, nullptr, gp(x.b1W) + W, ld(x.b1W)));
+        if (d.sem) {
+            SPN_HIP(outer(c.at(c.w.R0), W, W, c.pk(c.k.emb), d.sd, d.sd, labels, gp(x.fcW[0]) + d.K0, ld(x.fcW[0])));
+            SPN_HIP(outer(c.at(c.w.R4), W, W, c.pk(c.k.emb), d.sd, d.sd, labels, gp(x.fcW[d.skip]) + W + d.K0,
+                          ld(x.fcW[d.skip])));
+            hipLaunchKernelGGL(k_class_sum, dim3(cdiv((d.C + 1) * d.sd, 64)), dim3(64), 0, s, n_rays, c.at(c.w.gemb),
+                               d.sd, labels, d.C, gp(x.emb));
+            SPN_HIP(hipGetLastError());
+        }
+    }
+    return SPNERF_OK;
+}
+
+}  // namespace spn
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+using namespace spn;
+
+extern "C" int32_t spnerf_param_count(const spnerf_model_cfg* cfg) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    return (int32_t)param_specs(d, nullptr).size();
+}
+
+extern "C" int32_t spnerf_param_info(const spnerf_model_cfg* cfg, int32_t idx, char* name, int32_t cap, int64_t* rows,
+                                     int64_t* cols) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    auto v = param_specs(d, nullptr);
+    SPN_ARG(idx >= 0 && idx < (int)v.size(), "param index %d out of range", idx);
+    if (name && cap > 0) {
+        snprintf(name, cap, "%s", v[idx].name.c_str());
+    }
+    if (rows) *rows = v[idx].rows;
+    if (cols) *cols = v[idx].cols;
+    return SPNERF_OK;
+}
+
+extern "C" int64_t spnerf_packed_bytes(const spnerf_model_cfg* cfg) {
+    Dims d;
+    if (make_dims(cfg, &d) != SPNERF_OK) return -1;
+    return packed_layout(d).total * (int64_t)sizeof(float);
+}
+
+extern "C" int32_t spnerf_pack_params(const spnerf_model_cfg* cfg, const float* const* params, void* packed, void* stream) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    SPN_ARG(params && packed, "pack: NULL pointer");
+    return pack_params(d, params, (float*)packed, (hipStream_t)stream);
+}
+
+extern "C" int64_t spnerf_mlp_workspace_bytes(const spnerf_model_cfg* cfg, int64_t n_rays, int32_t n_samples, int32_t flags) {
+    Dims d;
+    if (make_dims(cfg, &d) != SPNERF_OK || n_rays < 0 || n_samples <= 0) return -1;
+    return ws_layout(d, n_rays, n_samples, flags).total * (int64_t)sizeof(float);
+}
+
+extern "C" int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed, const float* rays, int32_t ray_stride,
+                                      int32_t dir_offset, int64_t n_rays, int32_t n_samples, const float* z,
+                                      const int64_t* labels, const float* t_emb, int32_t flags, void* workspace, float* out,
+                                      void* stream) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    SPN_ARG(packed && rays && z && workspace && out, "mlp_forward: NULL pointer");
+    SPN_ARG(n_rays >= 0 && n_samples > 0 && ray_stride >= 11, "mlp_forward: bad sizes");
+    SPN_ARG(dir_offset == 3 || dir_offset == 8, "mlp_forward: dir_offset must be 3 (view) or 8 (sun)");
+    return mlp_forward(d, (const float*)packed, rays, ray_stride, dir_offset, n_rays, n_samples, z, labels, t_emb, flags,
+                       (float*)workspace, out, (hipStream_t)stream);
+}
+
+extern "C" int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed, const float* rays,
+                                       int32_t ray_stride, int64_t n_rays, int32_t n_samples, const int64_t* labels,
+                                       const float* t_emb, int32_t flags, void* workspace, const float* d_out,
+                                       float* grad_flat, float* grad_t_emb, void* stream) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    SPN_ARG(packed && rays && workspace && d_out && grad_flat, "mlp_backward: NULL pointer");
+    SPN_ARG(!d.sem || labels, "mlp_backward: semantic model needs labels");
+    SPN_ARG(!d.beta || (flags & SPNERF_MLP_SUN_ONLY) || t_emb, "mlp_backward: beta model needs t_emb");
+    return mlp_backward(d, (const float*)packed, rays, ray_stride, n_rays, n_samples, labels, t_emb, flags,
+                        (float*)workspace, d_out, grad_flat, grad_t_emb, (hipStream_t)stream);
+}

@@ -1,0 +1,69 @@
+// Parameter, packed-weight and workspace layouts of the SP-NeRF MLP (host side).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace spn {
+
+// Derived network dimensions (models/spnerf.py:162-271).
+struct Dims {
+    int W, H, L, skip;
+    int K0, K0p;        // encoded xyz width (60 with PE, 3 without) and its MFMA padding
+    int sd, C, td;      // semantic embedding width, classes, t-embedding width
+    bool sem, beta;
+    int NG;             // H8 consumers  G = [feat (W) | sem hidden (H)]
+    int NQ;             // feat consumers Q = [sun hidden 1 (H) | rgb hidden (H) | beta hidden (H)]
+    int NO;             // outputs per point: 8 + beta + C
+    int sem_col;        // first semantic-logit column of `out`
+    int HP;             // per-point head pre-gradient row: [dσ, drgb3, dsun, dβ, dsem C]
+};
+
+int32_t make_dims(const spnerf_model_cfg* cfg, Dims* d);
+
+struct PSpec {
+    std::string name;
+    int64_t rows, cols;  // torch shape (cols = 0 → 1-D)
+    int64_t off;         // offset (floats) in the flat gradient buffer
+    int64_t numel() const { return cols ? rows * cols : rows; }
+    int64_t ld() const { return cols ? cols : rows; }
+};
+
+// indices into the canonical parameter list
+struct PIdx {
+    int emb = -1;
+    std::vector<int> fcW, fcb;
+    int sigW, sigb, featW, featb, m1W = -1, m1b = -1, m2W = -1, m2b = -1;
+    int r1W, r1b, r2W, r2b, s1W, s1b, s2W, s2b, s3W, s3b, s4W, s4b;
+    int k1W, k1b, k2W, k2b, b1W = -1, b1b = -1, b2W = -1, b2b = -1;
+};
+
+std::vector<PSpec> param_specs(const Dims& d, PIdx* idx);
+
+// Offsets (floats) inside the packed weight buffer.
+struct Packed {
+    std::vector<int64_t> Wt, bt, WTt;   // trunk: forward [W][Kp_i], bias, transposed h-part [W][W]
+    std::vector<int> Kp;                // padded K of each trunk layer
+    int64_t WG, bG, WGT, WQ, bQ, WQT;
+    int64_t Ws2, bs2, Ws2T, Ws3, bs3, Ws3T;
+    int64_t wsig, bsig, Wr2, br2, ws4, bs4, Wm2, bm2, wb2, bb2;
+    int64_t Wk1, bk1, Wk2, bk2, Wsem0, Wsem4, emb, Wsun, Wtt;
+    int64_t total;
+};
+Packed packed_layout(const Dims& d);
+
+// Workspace offsets (floats).  SAVE keeps every activation + derivative for the backward.
+struct WS {
+    int64_t P, B;
+    int64_t X0;
+    std::vector<int64_t> Hb, Db;        // H_1..H_L (save) or 3 ping-pong buffers; D_1..D_L
+    int64_t G, DG, Q, DQ, S2, DS2, S3, DS3, hsave;
+    int64_t rb0, rb4, rbQ, skyh, sky;
+    // backward
+    int64_t dZG, dZQ, dS3, dS2, dZa, dZb, hpre, slab, slab_b, RQ, R0, R4, dsky, skyd, skydh, gemb, sk_slab, sk_slab_b;
+    int64_t total;
+};
+WS ws_layout(const Dims& d, int64_t n_rays, int32_t n_samples, int32_t flags);
+
+}  // namespace spn

@@ -1,0 +1,156 @@
+"""Ray rendering — drop-in for ``modules/rendering.py`` of the reference.
+
+Same functions, signatures, argument meaning, dictionary keys and error behaviour as the
+reference; every step runs on the gfx950 kernels of libspnerf_amd.so:
+
+==============================  ========================================  =====================
+reference (rendering.py)         here                                      kernel
+==============================  ========================================  =====================
+stratified z  :131-144           ``stratified``                            k_stratified
+inference pass 1 :157            σ-only MLP + weights-only composite       mlp + composite
+GenerateGuidedSamples :92-116    ``spnerf_sample_guided`` (+ sort, merge)  k_guided
+  + sort / merge :165-167
+inference pass 2 :169            full MLP + composite                      mlp + composite
+solar correction :171-177        σ+sun MLP + weights-only composite        mlp + composite
+sample_pdf :14-55                ``sample_pdf``                            k_sample_pdf
+sample_3sigma :58-73             ``sample_3sigma``                         k_sample_pdf (window)
+==============================  ========================================  =====================
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .rng import current_random_source
+from .spnerf import inference_rays
+
+
+def stratified(rays: torch.Tensor, n_samples: int, u: torch.Tensor) -> torch.Tensor:
+    """z = lower + (upper - lower)·u over [near, far] (rendering.py:131-144, perturb = 1)."""
+    _lib.require_device(rays, u)
+    rays = rays.contiguous().float()
+    u = u.contiguous().float()
+    z = torch.empty(rays.shape[0], n_samples, device=rays.device)
+    _lib.check(_lib.lib().spnerf_sample_stratified(rays.shape[0], n_samples, _lib.ptr(rays), rays.stride(0), _lib.ptr(u),
+                                                   _lib.ptr(z), _lib.stream_of(rays)), "sample_stratified")
+    return z
+
+
+def sample_pdf(bins, weights, N_importance, det=False, eps=1e-5):
+    """rendering.py:14-55.  (``det=True`` raises in the reference — 1-D ``u`` against a 2-D
+    CDF in searchsorted — here it uses the intended ``linspace(0,1,N)`` for every ray.)"""
+    _lib.require_device(bins, weights)
+    B, nb = weights.shape
+    if det:
+        u = torch.linspace(0, 1, N_importance, device=bins.device).expand(B, N_importance).contiguous()
+    else:
+        u = current_random_source().rand((B, N_importance), bins.device)
+    out = torch.empty(B, N_importance, device=bins.device)
+    _lib.check(_lib.lib().spnerf_sample_pdf(B, nb, _lib.ptr(bins.contiguous().float()), _lib.ptr(weights.contiguous().float()),
+                                            N_importance, _lib.ptr(u.contiguous().float()), float(eps), _lib.ptr(out),
+                                            _lib.stream_of(bins)), "sample_pdf")
+    return out
+
+
+def _bounds(near, far, device):
+    nf = torch.stack([torch.as_tensor(near, dtype=torch.float32, device=device).reshape(()),
+                      torch.as_tensor(far, dtype=torch.float32, device=device).reshape(())])
+    return nf.contiguous()
+
+
+def sample_3sigma(low_3sigma, high_3sigma, N, det, near, far, device=None):
+    """rendering.py:58-73: Gaussian-weighted bins over [low, high] clamped to [near, far]."""
+    _lib.require_device(low_3sigma, high_3sigma)
+    dev = low_3sigma.device
+    B = low_3sigma.shape[0]
+    if det:
+        u = torch.linspace(0, 1, N, device=dev).expand(B, N).contiguous()
+    else:
+        u = current_random_source().rand((B, N), dev)
+    out = torch.empty(B, N, device=dev)
+    _lib.check(_lib.lib().spnerf_sample_3sigma(B, N, _lib.ptr(low_3sigma.contiguous().float()),
+                                               _lib.ptr(high_3sigma.contiguous().float()), _lib.ptr(_bounds(near, far, dev)),
+                                               _lib.ptr(u.contiguous().float()), _lib.ptr(out), _lib.stream_of(low_3sigma)),
+               "sample_3sigma")
+    return out
+
+
+def compute_samples_around_depth(res, N_samples, z_vals, perturb, near, far, device=None):
+    """rendering.py:76-89."""
+    depth, w = res["depth"], res["weights"]
+    std = (((z_vals - depth.unsqueeze(-1)) ** 2) * w).sum(-1).sqrt()
+    return sample_3sigma(depth - 3.0 * std, depth + 3.0 * std, N_samples, perturb == 0.0, near, far, device=device)
+
+
+def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std):
+    """Fused GenerateGuidedSamples + sort + merge.  Returns (z_sorted, z_unsort), both (B, 2n)."""
+    B = z_vals.shape[0]
+    dev = z_vals.device
+    src = current_random_source()
+    u_pred = src.rand((B, n), dev).contiguous().float()                     # rendering.py:35 via :87
+    valid = tdep = tstd = u_gt = None
+    td_stride = 2
+    if mode == "train":
+        assert valid_depth is not None, "valid_depth missing in training batch!"   # rendering.py:99
+        valid = valid_depth.reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
+        tdep = target_depths.to(device=dev, dtype=torch.float32).contiguous()
+        td_stride = tdep.stride(0)
+        tstd = target_std.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
+        u_gt = src.gt_uniform(valid, n, dev).contiguous().float()             # rendering.py:113
+    z_sorted = torch.empty(B, 2 * n, device=dev)
+    z_unsort = torch.empty(B, 2 * n, device=dev)
+    clamp_nf = rays[0, 6:8]                                                   # first ray: rendering.py:95,113
+    _lib.check(_lib.lib().spnerf_sample_guided(B, n, _lib.ptr(z_vals), _lib.ptr(res["depth"].contiguous()),
+                                               _lib.ptr(res["weights"].contiguous()), _lib.ptr(clamp_nf), _lib.ptr(valid),
+                                               _lib.ptr(tdep), td_stride, _lib.ptr(tstd), _lib.ptr(u_pred), _lib.ptr(u_gt),
+                                               _lib.ptr(z_sorted), _lib.ptr(z_unsort), _lib.stream_of(z_vals)),
+               "sample_guided")
+    return z_sorted, z_unsort
+
+
+def GenerateGuidedSamples(res, z_vals, N_samples, perturb, near, far, mode='test', valid_depth=None, target_depths=None,
+                          target_std=None, device=None, margin=0, stdscale=1):
+    """rendering.py:92-116 (``margin`` / ``stdscale`` are unused there too).  The clamp bounds
+    are near[0,0] / far[0,0] — the first ray of the chunk, as in the reference."""
+    B = z_vals.shape[0]
+    rays_like = torch.zeros(B, 11, device=z_vals.device)
+    rays_like[0, 6] = near[0, 0]
+    rays_like[0, 7] = far[0, 0]
+    z_sorted, z_unsort = _guided(res, z_vals.contiguous().float(), N_samples, rays_like, mode, valid_depth, target_depths,
+                                 target_std)
+    return z_unsort[:, N_samples:]   # sorted guided samples (sorting does not change the set)
+
+
+def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth=None, target_depths=None,
+                target_std=None):
+    """rendering.py:119-218 for the coarse SP-NeRF model; returns the same dictionary
+    (keys suffixed ``_coarse``)."""
+    N_samples = args.n_samples
+    if args.model != "sp-nerf":
+        raise ValueError(f'model {args.model} is not valid')
+    _lib.require_device(rays)
+    rays = rays.contiguous().float()
+    B = rays.shape[0]
+    src = current_random_source()
+    z_vals = stratified(rays, N_samples, src.rand((B, N_samples), rays.device))   # rendering.py:143
+    model = models["coarse"]
+    rays_t = None
+    if args.beta:
+        rays_t = models["t"](ts) if ts is not None else None                       # rendering.py:156
+    sem = semantics if model.sem else None
+    if args.guidedsample:
+        with torch.no_grad():   # pass 1 feeds only the detached guided depths (rendering.py:164)
+            res1 = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, mode="sigma")
+        z_vals, z_unsort = _guided(res1, z_vals, N_samples, rays, mode, valid_depth, target_depths, target_std)
+        result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, z_vals_unsort=z_unsort)
+    else:
+        result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t)
+    if args.sc_lambda > 0:                                                           # rendering.py:171-177
+        sc = inference_rays(model, args, rays, z_vals, 8, sem, rays_t, mode="sun")
+        result["weights_sc"] = sc["weights"]
+        result["transparency_sc"] = sc["transparency"]
+        result["sun_sc"] = sc["sun"]
+    out = {f"{k}_coarse": v for k, v in result.items()}
+    if args.n_importance > 0:
+        raise NotImplementedError("hierarchical fine model (n_importance > 0) is the next §8(f) row; not built yet")
+    return out

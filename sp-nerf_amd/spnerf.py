@@ -1,0 +1,357 @@
+"""SP-NeRF model surface — drop-in for ``models/spnerf.py`` of the reference.
+
+``SPNeRF`` keeps the reference's constructor signature, sub-module names and parameter
+shapes (so reference checkpoints load with ``load_state_dict``, and ``torch.manual_seed(s)``
+gives the same initial weights: the RNG-consuming constructors run in the reference's order,
+spnerf.py:162-264), but its forward pass is the HIP library: positional encoding, the
+8-layer SIREN trunk and every head run as gfx950 kernels (csrc/mlp.hip, csrc/gemm_f32.hip),
+with a hand-written backward (``spnerf_mlp_backward``) behind ``torch.autograd.Function``.
+
+``inference`` (spnerf.py:63-159) composites with the wavefront-scan kernels of
+csrc/composite.hip.  Nothing here has a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_SAVE, SPNERF_MLP_SIGMA_ONLY, SPNERF_MLP_SUN_ONLY
+from .rng import current_random_source
+
+
+class Mapping(torch.nn.Module):
+    """Positional-encoding descriptor (spnerf.py:5-37): [sin(2^k x), cos(2^k x)], k < N_freqs.
+    The encoding itself is computed inside the MLP kernels (k_encode); this module only
+    carries the sizes the reference exposes."""
+
+    def __init__(self, mapping_size, in_size, logscale=True):
+        super().__init__()
+        if not logscale:
+            raise NotImplementedError("only log-scale frequency bands (the reference default) are supported")
+        self.N_freqs = mapping_size
+        self.in_channels = in_size
+        self.out_channels = in_size * (2 * mapping_size + 1)
+        self.freq_bands = 2 ** torch.linspace(0, mapping_size - 1, mapping_size)
+
+
+class Siren(torch.nn.Module):
+    """sin(w0 · x) activation marker (spnerf.py:40-46); fused into the GEMM epilogues."""
+
+    def __init__(self, w0=1.0):
+        super().__init__()
+        self.w0 = w0
+
+    def forward(self, x):  # kept for API completeness (elementwise, not on the render path)
+        return torch.sin(self.w0 * x)
+
+
+def sine_init(m):
+    with torch.no_grad():
+        if hasattr(m, "weight"):
+            fan = m.weight.size(-1)
+            m.weight.uniform_(-np.sqrt(6 / fan), np.sqrt(6 / fan))
+
+
+def first_layer_sine_init(m):
+    with torch.no_grad():
+        if hasattr(m, "weight"):
+            fan = m.weight.size(-1)
+            m.weight.uniform_(-1 / fan, 1 / fan)
+
+
+class SPNeRF(torch.nn.Module):
+    """Same constructor and parameters as the reference SPNeRF (spnerf.py:162-271)."""
+
+    def __init__(self, num_sem_classes=3, s_embedding_factor=1, layers=8, feat=256, mapping=False,
+                 mapping_sizes=[10, 4], skips=[4], siren=True, t_embedding_dims=16, beta=False, sem=False):
+        super().__init__()
+        if not siren:
+            raise NotImplementedError("the gfx950 trunk implements the SIREN activations (load_model never "
+                                      "disables them, models/__init__.py:6-13)")
+        if len(skips) > 1:
+            raise NotImplementedError("one skip connection is supported (reference default skips=[4])")
+        self.layers = layers
+        self.skips = list(skips)
+        self.t_embedding_dims = t_embedding_dims
+        self.input_sizes = [3, 0]
+        self.rgb_padding = 0.001
+        self.beta = beta
+        self.sem = sem
+        self.num_sem_classes = num_sem_classes
+        self.s_embedding_factor = s_embedding_factor
+        self.semantic_size = num_sem_classes * s_embedding_factor if sem else 0
+        self.feat = feat
+        self.n_freq = mapping_sizes[0] if mapping else 0
+        in_xyz = 2 * mapping_sizes[0] * 3 if mapping else 3
+        self.mapping = [Mapping(ms, isz) for ms, isz in zip(mapping_sizes, self.input_sizes)] if mapping else \
+            [torch.nn.Identity(), torch.nn.Identity()]
+        H = feat // 2
+        if sem:
+            self.semantic_embedding = torch.nn.Embedding(num_sem_classes + 1, self.semantic_size,
+                                                         padding_idx=num_sem_classes)
+        self.input_size = in_xyz + self.semantic_size
+        mods = []
+        for i in range(layers):
+            fan = self.input_size if i == 0 else (feat + self.input_size if i in self.skips else feat)
+            mods += [torch.nn.Linear(fan, feat), Siren(30.0 if i == 0 else 1.0)]
+        self.fc_net = torch.nn.Sequential(*mods)
+        self.sigma_from_xyz = torch.nn.Sequential(torch.nn.Linear(feat, 1), torch.nn.Softplus())
+        self.feats_from_xyz = torch.nn.Linear(feat, feat)
+        if sem:
+            self.logit_from_label = torch.nn.Sequential(torch.nn.Linear(feat, H), Siren(),
+                                                        torch.nn.Linear(H, num_sem_classes))
+        self.rgb_from_xyzdir = torch.nn.Sequential(torch.nn.Linear(feat, H), Siren(), torch.nn.Linear(H, 3),
+                                                   torch.nn.Sigmoid())
+        self.sun_v_net = torch.nn.Sequential(torch.nn.Linear(feat + 3, H), Siren(), torch.nn.Linear(H, H), Siren(),
+                                             torch.nn.Linear(H, H), Siren(), torch.nn.Linear(H, 1), torch.nn.Sigmoid())
+        self.sky_color = torch.nn.Sequential(torch.nn.Linear(3, H), torch.nn.ReLU(), torch.nn.Linear(H, 3),
+                                             torch.nn.Sigmoid())
+        self.fc_net.apply(sine_init)
+        self.fc_net[0].apply(first_layer_sine_init)
+        self.sun_v_net.apply(sine_init)
+        self.sun_v_net[0].apply(first_layer_sine_init)
+        if beta:
+            self.beta_from_xyz = torch.nn.Sequential(torch.nn.Linear(t_embedding_dims + feat, H), Siren(),
+                                                     torch.nn.Linear(H, 1), torch.nn.Softplus())
+        self.number_of_outputs = 8 + (1 if beta else 0) + (num_sem_classes if sem else 0)
+        self._cfg = None
+        self._order = None
+        self._packed = None
+        self._pack_key = None
+
+    # ---------------------------------------------------------------- library plumbing
+    def cfg(self) -> _lib.ModelCfg:
+        if self._cfg is None:
+            c = _lib.ModelCfg()
+            c.width, c.layers = self.feat, self.layers
+            c.skip = self.skips[0] if self.skips else -1
+            c.n_freq = self.n_freq
+            c.sem_classes = self.num_sem_classes if self.sem else 0
+            c.sem_dim = self.semantic_size
+            c.beta = 1 if self.beta else 0
+            c.t_dim = self.t_embedding_dims if self.beta else 0
+            c.dtype = 0
+            self._cfg = c
+        return self._cfg
+
+    def canonical_parameters(self):
+        """Parameters in the library's canonical order (spnerf_param_info), shape-checked."""
+        if self._order is None:
+            L = _lib.lib()
+            cfg = ctypes.byref(self.cfg())
+            n = L.spnerf_param_count(cfg)
+            if n < 0:
+                _lib.check(n, "param_count")
+            named = dict(self.named_parameters())
+            order = []
+            buf = ctypes.create_string_buffer(128)
+            for i in range(n):
+                r, c = ctypes.c_int64(), ctypes.c_int64()
+                _lib.check(L.spnerf_param_info(cfg, i, buf, 128, ctypes.byref(r), ctypes.byref(c)), "param_info")
+                name = buf.value.decode()
+                shape = (r.value, c.value) if c.value else (r.value,)
+                p = named[name]
+                if tuple(p.shape) != shape:
+                    raise _lib.SpnerfError(f"parameter {name}: module shape {tuple(p.shape)} != library {shape}")
+                order.append(name)
+            self._order = order
+        named = dict(self.named_parameters())
+        return [named[n] for n in self._order]
+
+    def packed_weights(self) -> torch.Tensor:
+        """Kernel-layout copy of the weights, re-packed when any parameter changed (in-place
+        optimizer steps bump ``_version``)."""
+        params = self.canonical_parameters()
+        _lib.require_device(params[0])
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._pack_key != key:
+            if self._packed is None or self._packed.device != params[0].device:
+                nbytes = _lib.lib().spnerf_packed_bytes(ctypes.byref(self.cfg()))
+                self._packed = torch.zeros(nbytes // 4, dtype=torch.float32, device=params[0].device)
+            for p in params:
+                if not p.is_contiguous() or p.dtype != torch.float32:
+                    raise _lib.SpnerfError("parameters must be contiguous float32")
+            arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+            _lib.check(_lib.lib().spnerf_pack_params(ctypes.byref(self.cfg()), arr, _lib.ptr(self._packed),
+                                                     _lib.stream_of(self._packed)), "pack_params")
+            self._pack_key = key
+        return self._packed
+
+    def _apply(self, fn, *args, **kwargs):
+        self._packed, self._pack_key = None, None
+        return super()._apply(fn, *args, **kwargs)
+
+    # ---------------------------------------------------------------- reference forward API
+    def forward(self, input_xyz, input_dir=None, input_sun_dir=None, input_t=None, input_s=None, sigma_only=False):
+        """Per-point network (spnerf.py:273-369) on the HIP kernels: (P,3) → (P, number_of_outputs)
+        with columns [rgb3, σ, sun, sky3, (β), sem] (or σ (P,1) if ``sigma_only``)."""
+        _lib.require_device(input_xyz)
+        P = input_xyz.shape[0]
+        sun = input_sun_dir if input_sun_dir is not None else torch.zeros_like(input_xyz)
+        pts = torch.cat([input_xyz.float(), torch.zeros(P, 5, device=input_xyz.device), sun.float()], 1)
+        z = torch.zeros(P, 1, device=input_xyz.device)
+        labels = None
+        if self.sem:
+            if input_s is None:
+                raise ValueError("semantic SPNeRF needs input_s")
+            labels = input_s.reshape(-1).long()
+        t = input_t.float() if self.beta else None
+        out = run_mlp(self, pts, z, 3, labels, t, sigma_only=sigma_only)
+        return out[:, 3:4] if sigma_only else out
+
+
+# ------------------------------------------------------------------------------------------
+# autograd functions
+# ------------------------------------------------------------------------------------------
+
+class _MLP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, rays, dir_offset, z, labels, temb, flags, *params):
+        cfg = model.cfg()
+        B, S = z.shape
+        dev = rays.device
+        need_grad = any(ctx.needs_input_grad[5:6]) or any(ctx.needs_input_grad[7:])
+        if need_grad:
+            if flags & SPNERF_MLP_SIGMA_ONLY:
+                raise _lib.SpnerfError("sigma-only passes are not differentiable")
+            flags |= SPNERF_MLP_SAVE
+        L = _lib.lib()
+        wsb = L.spnerf_mlp_workspace_bytes(ctypes.byref(cfg), B, S, flags)
+        if wsb < 0:
+            _lib.check(-1, "workspace_bytes")
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
+        out = torch.empty(B * S, model.number_of_outputs, dtype=torch.float32, device=dev)
+        packed = model.packed_weights()
+        _lib.check(L.spnerf_mlp_forward(ctypes.byref(cfg), _lib.ptr(packed), _lib.ptr(rays), rays.stride(0), dir_offset,
+                                        B, S, _lib.ptr(z), _lib.ptr(labels), _lib.ptr(temb), flags, _lib.ptr(ws),
+                                        _lib.ptr(out), _lib.stream_of(rays)), "mlp_forward")
+        if need_grad:
+            ctx.model, ctx.flags, ctx.ws, ctx.packed = model, flags, ws, packed
+            ctx.shape = (B, S)
+            ctx.save_for_backward(rays, labels, temb)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        rays, labels, temb = ctx.saved_tensors
+        model = ctx.model
+        params = model.canonical_parameters()
+        B, S = ctx.shape
+        total = sum(p.numel() for p in params)
+        grad = torch.empty(total, dtype=torch.float32, device=rays.device)
+        gt = torch.empty_like(temb) if (temb is not None and ctx.needs_input_grad[5]) else None
+        _lib.check(_lib.lib().spnerf_mlp_backward(ctypes.byref(model.cfg()), _lib.ptr(ctx.packed), _lib.ptr(rays),
+                                                  rays.stride(0), B, S, _lib.ptr(labels), _lib.ptr(temb), ctx.flags,
+                                                  _lib.ptr(ctx.ws), _lib.ptr(d_out.contiguous()), _lib.ptr(grad),
+                                                  _lib.ptr(gt), _lib.stream_of(rays)), "mlp_backward")
+        grads, off = [], 0
+        for p in params:
+            grads.append(grad[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        ctx.ws = None
+        return (None, None, None, None, None, gt, None, *grads)
+
+
+def run_mlp(model: SPNeRF, rays: torch.Tensor, z: torch.Tensor, dir_offset: int, labels=None, temb=None,
+            sigma_only=False, sun_only=False) -> torch.Tensor:
+    """out (B·S, number_of_outputs) for xyz = rays[:, 0:3] + rays[:, dir:dir+3] · z."""
+    _lib.require_device(rays, z, labels, temb)
+    rays = rays.contiguous().float()
+    z = z.contiguous().float()
+    if labels is not None:
+        labels = labels.reshape(-1).to(torch.int64).contiguous()
+    if temb is not None:
+        temb = temb.contiguous().float()
+    flags = (SPNERF_MLP_SIGMA_ONLY if sigma_only else 0) | (SPNERF_MLP_SUN_ONLY if sun_only else 0)
+    params = model.canonical_parameters()
+    return _MLP.apply(model, rays, dir_offset, z, labels, temb, flags, *params)
+
+
+class _Composite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out, z, noise, noise_std, sem_col, n_sem, weights_only):
+        B, S = z.shape
+        NO = out.shape[1]
+        dev = out.device
+        f = SPNERF_COMP_WEIGHTS_ONLY if weights_only else 0
+        rgb = torch.empty(B, 3, device=dev) if not weights_only else torch.empty(0, device=dev)
+        sem = torch.empty(B, n_sem, device=dev) if (n_sem and not weights_only) else torch.empty(0, device=dev)
+        depth = torch.empty(B, device=dev)
+        w = torch.empty(B, S, device=dev)
+        T = torch.empty(B, S, device=dev)
+        _lib.check(_lib.lib().spnerf_composite_forward(B, S, _lib.ptr(z), _lib.ptr(out), NO, _lib.ptr(noise),
+                                                       float(noise_std), sem_col, n_sem, f, _lib.ptr(rgb), _lib.ptr(depth),
+                                                       _lib.ptr(w), _lib.ptr(T), _lib.ptr(sem), _lib.stream_of(out)),
+                   "composite_forward")
+        ctx.save_for_backward(out, z, noise)
+        ctx.cfg = (float(noise_std), sem_col, n_sem, f)
+        ctx.set_materialize_grads(False)
+        return rgb, depth, w, T, sem
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_w, g_T, g_sem):
+        out, z, noise = ctx.saved_tensors
+        noise_std, sem_col, n_sem, f = ctx.cfg
+        B, S = z.shape
+        c = lambda g: None if g is None else g.contiguous()
+        d_out = torch.empty_like(out)
+        _lib.check(_lib.lib().spnerf_composite_backward(B, S, _lib.ptr(z), _lib.ptr(out), out.shape[1], _lib.ptr(noise),
+                                                        noise_std, sem_col, n_sem, f, _lib.ptr(c(g_rgb)),
+                                                        _lib.ptr(c(g_depth)), _lib.ptr(c(g_w)), _lib.ptr(c(g_T)),
+                                                        _lib.ptr(c(g_sem)), _lib.ptr(d_out), _lib.stream_of(out)),
+                   "composite_backward")
+        return d_out, None, None, None, None, None, None
+
+
+def composite(model: SPNeRF, out: torch.Tensor, z: torch.Tensor, noise_std: float, weights_only=False):
+    B, S = z.shape
+    noise = current_random_source().noise((B, S), z.device, noise_std)       # spnerf.py:122
+    if noise is not None:
+        noise = noise.contiguous().float()
+    sem_col = 8 + (1 if model.beta else 0)
+    n_sem = model.num_sem_classes if model.sem else 0
+    return _Composite.apply(out, z.contiguous(), noise, noise_std, sem_col, n_sem, weights_only)
+
+
+def _result(model, out, z, rgb, depth, w, T, sem, z_unsort=None):
+    B, S = z.shape
+    o = out.view(B, S, model.number_of_outputs)
+    res = {"rgb": rgb, "depth": depth, "weights": w, "transparency": T, "albedo": o[..., :3], "sun": o[..., 4:5],
+           "sky": o[..., 5:8], "z_vals": z}
+    if z_unsort is not None:
+        res["z_vals_unsort"] = z_unsort
+    col = 8
+    if model.beta:
+        res["beta"] = o[..., col:col + 1]
+        col += 1
+    if model.sem:
+        res["sem_logits"] = sem
+    return res
+
+
+def inference_rays(model: SPNeRF, args, rays, z_vals, dir_offset=3, semantics=None, rays_t=None, z_vals_unsort=None,
+                   mode="full"):
+    """inference() over rays given by (origin, direction) + depths, without materialising xyz:
+    mode 'full' (all heads), 'sun' (σ + sun, the solar-correction pass) or 'sigma'."""
+    out = run_mlp(model, rays, z_vals, dir_offset, semantics if model.sem else None, rays_t if model.beta else None,
+                  sigma_only=mode == "sigma", sun_only=mode == "sun")
+    rgb, depth, w, T, sem = composite(model, out, z_vals, args.noise_std, weights_only=mode != "full")
+    return _result(model, out, z_vals, rgb, depth, w, T, sem, z_vals_unsort)
+
+
+def inference(model, args, rays_xyz, z_vals, rays_d=None, sun_d=None, rays_t=None, semantics=None, z_vals_unsort=None):
+    """Drop-in for spnerf.py:63 on explicit sample positions rays_xyz (N_rays, N_samples, 3)."""
+    _lib.require_device(rays_xyz, z_vals)
+    B, S = z_vals.shape
+    pts = rays_xyz.reshape(B * S, 3).float()
+    sd = torch.zeros(B, 3, device=pts.device) if sun_d is None else sun_d.float()
+    rays = torch.cat([pts, torch.zeros(B * S, 5, device=pts.device), sd.repeat_interleave(S, 0)], 1)
+    lab = semantics.reshape(-1).repeat_interleave(S, 0) if (semantics is not None and model.sem) else None
+    t = rays_t.repeat_interleave(S, 0) if (rays_t is not None and model.beta) else None
+    out = run_mlp(model, rays, torch.zeros(B * S, 1, device=pts.device), 3, lab, t)
+    rgb, depth, w, T, sem = composite(model, out, z_vals.contiguous().float(), args.noise_std)
+    return _result(model, out, z_vals, rgb, depth, w, T, sem, z_vals_unsort)

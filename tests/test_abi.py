@@ -1,0 +1,99 @@
+"""C-ABI library: loads without a GPU, exports exactly what include/spnerf_amd.h declares,
+agrees with the oracle on the parameter contract, and reports errors (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import spnerf_amd
+from spnerf_amd import _lib
+from oracle.weights import ModelDims, param_specs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "spnerf_amd.h")).read()
+    return sorted(set(re.findall(r"\b(spnerf_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) == 19
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(_lib.SIGNATURES) == syms, "ctypes signature table out of sync with the header"
+    assert L.spnerf_abi_version() == 1
+
+
+def cfg_of(d: ModelDims):
+    c = _lib.ModelCfg()
+    c.width, c.layers, c.skip = d.width, d.layers, d.skips[0]
+    c.n_freq = d.n_freq if d.mapping else 0
+    c.sem_classes = d.num_sem_classes if d.sem else 0
+    c.sem_dim = d.sem_dim
+    c.beta, c.t_dim = int(d.beta), (d.t_dim if d.beta else 0)
+    return c
+
+
+@pytest.mark.parametrize("dims", [ModelDims(), ModelDims(width=64, sem=True), ModelDims(width=64, sem=True, beta=True),
+                                  ModelDims(width=128, mapping=False), ModelDims(sem=True, num_sem_classes=5)])
+def test_param_contract_matches_reference_order(dims):
+    L = _lib.lib()
+    c = cfg_of(dims)
+    specs = param_specs(dims)
+    assert L.spnerf_param_count(ctypes.byref(c)) == len(specs)
+    buf = ctypes.create_string_buffer(128)
+    for i, (name, shape, _) in enumerate(specs):
+        r, k = ctypes.c_int64(), ctypes.c_int64()
+        assert L.spnerf_param_info(ctypes.byref(c), i, buf, 128, ctypes.byref(r), ctypes.byref(k)) == 0
+        got = (r.value, k.value) if k.value else (r.value,)
+        assert buf.value.decode() == name and got == tuple(shape), (i, name)
+    assert L.spnerf_packed_bytes(ctypes.byref(c)) > 4 * sum(int(__import__("numpy").prod(s)) for _, s, _ in specs)
+
+
+def test_module_parameters_match_reference_state_dict():
+    dims = ModelDims(sem=True, beta=True)
+    m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, beta=True, sem=True, t_embedding_dims=4)
+    assert [(n, tuple(p.shape)) for n, p in m.named_parameters()] == [(n, tuple(s)) for n, s, _ in param_specs(dims)]
+    assert m.number_of_outputs == dims.n_outputs
+    assert [p.shape for p in m.canonical_parameters()] == [p.shape for p in m.parameters()]
+
+
+def test_reference_default_param_count():
+    m = spnerf_amd.SPNeRF(num_sem_classes=3, feat=512, mapping=True, sem=True)
+    assert sum(p.numel() for p in m.parameters()) == 2_696_727
+
+
+def test_errors_are_reported_not_fallen_back():
+    L = _lib.lib()
+    c = _lib.ModelCfg()
+    c.width, c.layers, c.skip, c.n_freq = 100, 8, 4, 10      # width not a multiple of 64
+    assert L.spnerf_param_count(ctypes.byref(c)) < 0
+    assert b"width" in L.spnerf_last_error()
+    assert L.spnerf_mlp_workspace_bytes(ctypes.byref(c), 10, 64, 0) == -1
+    assert L.spnerf_sample_stratified(4, 64, None, 11, None, None, None) == -1
+    assert b"NULL" in L.spnerf_last_error()
+
+
+def test_product_path_refuses_cpu_tensors():
+    import torch
+    import types
+    m = spnerf_amd.SPNeRF(feat=64, mapping=True)
+    args = types.SimpleNamespace(n_samples=8, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                                 sc_lambda=0.0, margin=0, stdscale=1, chunk=5120, noise_std=0.0)
+    with pytest.raises(_lib.SpnerfError, match="MI355X"):
+        spnerf_amd.render_rays({"coarse": m}, args, torch.zeros(4, 11), None)
+    with pytest.raises(ValueError):
+        spnerf_amd.render_rays({"coarse": m}, types.SimpleNamespace(**{**vars(args), "model": "nerf"}), torch.zeros(4, 11), None)
+
+
+def test_workspace_sizes_scale_with_points():
+    L = _lib.lib()
+    c = cfg_of(ModelDims(sem=True))
+    a = L.spnerf_mlp_workspace_bytes(ctypes.byref(c), 1024, 64, _lib.SPNERF_MLP_SAVE)
+    b = L.spnerf_mlp_workspace_bytes(ctypes.byref(c), 2048, 64, _lib.SPNERF_MLP_SAVE)
+    n = L.spnerf_mlp_workspace_bytes(ctypes.byref(c), 1024, 64, 0)
+    assert 0 < n < a < b
