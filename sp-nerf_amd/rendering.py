@@ -82,7 +82,7 @@ def compute_samples_around_depth(res, N_samples, z_vals, perturb, near, far, dev
     return sample_3sigma(depth - 3.0 * std, depth + 3.0 * std, N_samples, perturb == 0.0, near, far, device=device)
 
 
-def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std):
+def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std, clamp_nf=None):
     """Fused GenerateGuidedSamples + sort + merge.  Returns (z_sorted, z_unsort), both (B, 2n)."""
     B = z_vals.shape[0]
     dev = z_vals.device
@@ -99,7 +99,8 @@ def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std):
         u_gt = src.gt_uniform(valid, n, dev).contiguous().float()             # rendering.py:113
     z_sorted = torch.empty(B, 2 * n, device=dev)
     z_unsort = torch.empty(B, 2 * n, device=dev)
-    clamp_nf = rays[0, 6:8]                                                   # first ray: rendering.py:95,113
+    if clamp_nf is None:
+        clamp_nf = rays[0, 6:8]                                               # first ray: rendering.py:95,113
     _lib.check(_lib.lib().spnerf_sample_guided(B, n, _lib.ptr(z_vals), _lib.ptr(res["depth"].contiguous()),
                                                _lib.ptr(res["weights"].contiguous()), _lib.ptr(clamp_nf), _lib.ptr(valid),
                                                _lib.ptr(tdep), td_stride, _lib.ptr(tstd), _lib.ptr(u_pred), _lib.ptr(u_gt),
@@ -122,9 +123,11 @@ def GenerateGuidedSamples(res, z_vals, N_samples, perturb, near, far, mode='test
 
 
 def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth=None, target_depths=None,
-                target_std=None):
+                target_std=None, *, clamp_near_far=None):
     """rendering.py:119-218 for the coarse SP-NeRF model; returns the same dictionary
-    (keys suffixed ``_coarse``)."""
+    (keys suffixed ``_coarse``).  ``clamp_near_far`` (extension, device tensor of 2 floats)
+    overrides the guided-sampling clamp bounds, which otherwise are the first ray's near/far
+    like the reference — data-parallel ranks pass the GLOBAL batch's first ray."""
     N_samples = args.n_samples
     if args.model != "sp-nerf":
         raise ValueError(f'model {args.model} is not valid')
@@ -141,7 +144,8 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
     if args.guidedsample:
         with torch.no_grad():   # pass 1 feeds only the detached guided depths (rendering.py:164)
             res1 = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, mode="sigma")
-        z_vals, z_unsort = _guided(res1, z_vals, N_samples, rays, mode, valid_depth, target_depths, target_std)
+        cnf = None if clamp_near_far is None else clamp_near_far.reshape(2).to(rays.device, torch.float32).contiguous()
+        z_vals, z_unsort = _guided(res1, z_vals, N_samples, rays, mode, valid_depth, target_depths, target_std, cnf)
         result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, z_vals_unsort=z_unsort)
     else:
         result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t)

@@ -214,11 +214,7 @@ class _MLP(torch.autograd.Function):
         cfg = model.cfg()
         B, S = z.shape
         dev = rays.device
-        need_grad = any(ctx.needs_input_grad[5:6]) or any(ctx.needs_input_grad[7:])
-        if need_grad:
-            if flags & SPNERF_MLP_SIGMA_ONLY:
-                raise _lib.SpnerfError("sigma-only passes are not differentiable")
-            flags |= SPNERF_MLP_SAVE
+        need_grad = bool(flags & SPNERF_MLP_SAVE)
         L = _lib.lib()
         wsb = L.spnerf_mlp_workspace_bytes(ctypes.byref(cfg), B, S, flags)
         if wsb < 0:
@@ -268,6 +264,10 @@ def run_mlp(model: SPNeRF, rays: torch.Tensor, z: torch.Tensor, dir_offset: int,
         temb = temb.contiguous().float()
     flags = (SPNERF_MLP_SIGMA_ONLY if sigma_only else 0) | (SPNERF_MLP_SUN_ONLY if sun_only else 0)
     params = model.canonical_parameters()
+    if torch.is_grad_enabled() and (any(p.requires_grad for p in params) or (temb is not None and temb.requires_grad)):
+        if sigma_only:
+            raise _lib.SpnerfError("sigma-only passes are not differentiable (run them under torch.no_grad())")
+        flags |= SPNERF_MLP_SAVE
     return _MLP.apply(model, rays, dir_offset, z, labels, temb, flags, *params)
 
 

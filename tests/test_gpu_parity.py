@@ -119,7 +119,7 @@ def test_composite_unit_matches_reference():
 def test_sort_rows_matches_torch(n):
     g = torch.Generator().manual_seed(n)
     x = torch.rand(123, n, generator=g)
-    x[:, ::7] = x[:, :1]     # ties
+    x[:, ::7] = x[:, :1].clone()     # ties
     out = torch.empty(123, n, device=DEV)
     xd = x.to(DEV)
     from spnerf_amd import _lib
