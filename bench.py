@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""SP-NeRF train-step throughput on MI355X (ray-samples/s), BASELINE.json metric.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3] [--no-cpu-baseline]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = sample a batch of rays from the HBM-resident synthetic scene (shared-seed sampler,
+every rank its slice), render_rays (stratified [+ guided] sampling, MLP, compositing
+[+ solar pass]) on the HIP kernels, the reference losses, backward, ONE RCCL all-reduce of the
+flat gradient bucket (N > 1), Adam.  Per-GPU batch is fixed (weak scaling).
+
+The default workload is BASELINE.json configs[1] (C2: JAX_214 shape at img_downscale=4,
+1024 rays x 64 samples, coarse only, fp32).  ``roofline`` reports the dominant kernel
+(the fp32 MFMA GEMM) from HIP events recorded by the library around each of its launches
+during the timed steps; ``cpu_baseline`` times the repo's PyTorch-CPU oracle (the reference
+algorithm restated, parity-pinned) on the host cores for a bounded sample of the workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import spnerf_amd  # noqa: E402
+from spnerf_amd import _lib, dp  # noqa: E402
+from spnerf_amd.losses import DepthLoss, SemanticLoss, SNerfLoss  # noqa: E402
+from spnerf_amd.scene import synthetic_scene  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    "c2": dict(workload="C2: JAX_214-shape synthetic RPC-like rays, img_downscale=4, 1024 rays x 64 samples, "
+                        "coarse-only, W=512, PE on, fp32", img_downscale=4.0, batch=1024, n_samples=64, sem=False,
+               guided=False, sc_lambda=0.0, depth=False),
+    "c3": dict(workload="C3 flags (README recipe) at fp32: JAX_214-shape synthetic rays, img_downscale=1, 1024 rays x "
+                        "(64 + 64 guided) samples, solar pass, depth + semantic (C=3) heads, W=512",
+               img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True),
+}
+
+
+def make_args(c):
+    return types.SimpleNamespace(n_samples=c["n_samples"], n_importance=0, model="sp-nerf", beta=False,
+                                 guidedsample=c["guided"], sc_lambda=c["sc_lambda"], margin=1e-4, stdscale=1.0,
+                                 chunk=5120, noise_std=0.0)
+
+
+def cpu_baseline(c, seconds: float):
+    """The parity-pinned CPU restatement (oracle/ref_cpu.py) of the same train step on the host
+    cores: 256-ray batches of the same workload, timed for ~``seconds``."""
+    import numpy as np
+    from oracle import ref_cpu
+    from oracle.weights import ModelDims, make_weights
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    dims = ModelDims(width=512, sem=c["sem"])
+    p = ref_cpu.to_params(make_weights(dims, 0), requires_grad=True)
+    opt = torch.optim.Adam(list(p.values()), lr=5e-4)
+    scene = synthetic_scene(c["img_downscale"], seed=1)
+    args = make_args(c)
+    B = 256
+    g = torch.Generator().manual_seed(0)
+    s_final = c["n_samples"] * (2 if c["guided"] else 1)
+
+    def one():
+        idx = torch.randint(0, scene.rays.shape[0], (B,), generator=g)
+        kw = {}
+        if c["guided"]:
+            kw = dict(valid_depth=scene.valid_depth[idx], target_depths=scene.depths[idx], target_std=scene.depth_std[idx])
+        res = ref_cpu.render_rays(p, dims, args, scene.rays[idx], None, scene.sems[idx] if c["sem"] else None, "train", **kw)
+        loss = torch.mean((res["rgb_coarse"] - scene.rgbs[idx]) ** 2)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    one()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        n += 1
+        if time.perf_counter() - t0 >= seconds or n >= 200:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": B * s_final * n / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps of {B} rays x {s_final} samples (oracle/ref_cpu.py, torch CPU, {threads} threads)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    a = ap.parse_args()
+
+    rank, local, world = dp.init_from_env("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    c = CONFIGS[a.config]
+    scene = synthetic_scene(c["img_downscale"], seed=0)
+    R = {k: getattr(scene, k).to(dev) for k in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")}
+    torch.manual_seed(0)
+    model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"]).to(dev)
+    params = list(model.parameters())
+    try:
+        opt = torch.optim.Adam(params, lr=5e-4, fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.Adam(params, lr=5e-4, foreach=True)
+    args = make_args(c)
+    B = c["batch"]
+    sampler = dp.SharedSeedSampler(R["rays"].shape[0], B * world, rank, world, seed=0, device=dev)
+    sloss = SNerfLoss(lambda_sc=c["sc_lambda"])
+    dloss = DepthLoss(lambda_ds=1.0) if c["depth"] else None
+    semloss = SemanticLoss(lambda_ss=1.0) if c["sem"] else None
+    s_final = c["n_samples"] * (2 if c["guided"] else 1)
+
+    def step():
+        gidx, idx = sampler.next()
+        rays = R["rays"][idx]
+        kw = {}
+        if c["guided"]:
+            kw = dict(valid_depth=R["valid_depth"][idx], target_depths=R["depths"][idx], target_std=R["depth_std"][idx],
+                      clamp_near_far=R["rays"][gidx[0], 6:8])
+        sem = R["sems"][idx] if c["sem"] else None
+        res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="train", **kw)
+        loss, _ = sloss(res, R["rgbs"][idx])
+        if dloss is not None:
+            loss = loss + dloss(res, R["depths"][idx, 0], R["depths"][idx, 1], R["valid_depth"][idx], R["depth_std"][idx])[0]
+        if semloss is not None:
+            scale = dp.ce_scale(sem, R["sems"][gidx], world) if world > 1 else 1.0
+            loss = loss + scale * semloss(res, sem)[0]
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        dp.allreduce_grads(params, world)
+        opt.step()
+        args.noise_std *= 0.9          # main.py:155
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _lib.prof_reset()
+    _lib.prof_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    _lib.prof_enable(False)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+
+    kernels = {}
+    for k in ("gemm_nt_f32", "gemm_tn_f32", "encode", "heads_fwd", "heads_bwd", "composite_fwd", "composite_bwd",
+              "sample_guided"):
+        s = _lib.prof_read(k)
+        if s["launches"]:
+            kernels[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / a.steps,
+                          "avg_us": 1e3 * s["ms"] / s["launches"],
+                          "tflops": s["flop"] / (s["ms"] * 1e-3) / 1e12 if s["flop"] else None,
+                          "gbs": s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["bytes"] else None}
+    nt = _lib.prof_read("gemm_nt_f32")
+    achieved = nt["flop"] / (nt["ms"] * 1e-3) / 1e12 if nt["ms"] else 0.0
+    total = world * B * s_final * a.steps
+    out = {
+        "metric": "ray-samples/sec (train step)",
+        "value": total / elapsed,
+        "unit": "ray-samples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * elapsed / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (JAX_214-shape RPC-like rays resident in HBM, seeded-random SPNeRF init)",
+        "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": s_final,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": "gemm_nt_f32 (k_gemm_nt)", "achieved": achieved,
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": None, "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
+        "kernels": kernels,
+        "final_loss": float(loss.item()),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

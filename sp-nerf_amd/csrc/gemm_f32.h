@@ -34,6 +34,15 @@ struct TNArgs {
     int p_per_split = 0;  // set by gemm_tn
 };
 
+// Skinny reduction over points: slab[chunk][m][k] = Σ_p A[p*lda+m]·B[p*ldb+k] (m < Ma ≤ 8,
+// plus m = Ma: Σ_p B[p][k] when `ones`), slab_b[chunk][m] = Σ_p A[p*lda+m].
+struct SkinnyArgs {
+    const float* A = nullptr; int lda = 0; int Ma = 0;
+    const float* B = nullptr; int ldb = 0; int K = 0;
+    int64_t P = 0; int chunk = 0; int ones = 0;
+    float* slab = nullptr; float* slab_b = nullptr;
+};
+
 struct ReduceArgs {
     const float* slab = nullptr; int ld_slab = 0; int64_t slab_stride = 0; int splits = 0; int N = 0;
     const float* slab_b = nullptr;
@@ -41,10 +50,13 @@ struct ReduceArgs {
     float* dst = nullptr; int ld_dst = 0;
     float* dst_b = nullptr;
     int accumulate = 0;
+    int transpose = 0;  // dst[c][r] instead of dst[r][c]
 };
 
 int32_t gemm_nt(const NTArgs& a, hipStream_t s);
 int tn_splits(int P, int N, int K);
+int skinny_chunk(int64_t P);
+int32_t tn_skinny(const SkinnyArgs& a, hipStream_t s);
 int32_t gemm_tn(const TNArgs& a, int splits, hipStream_t s);
 int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s);
 

@@ -216,20 +216,100 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
     if (do_bias && n0 + tid < g.N) g.slab_b[(int64_t)split * g.N + n0 + tid] = bsum;
 }
 
-// dst[r][c] (+)= Σ_s slab[s][row0+r][c] for c < ncols; dst_b[r] = Σ_s slab_b[s][row0+r]
-__global__ void k_reduce_slabs(ReduceArgs g) {
+// dst[r][c] (+)= Σ_s slab[s][row0+r][c] for c < ncols; dst_b[r] = Σ_s slab_b[s][row0+r];
+// with `transpose`, dst[c][r] instead.  256 threads = 64 columns x 4 split phases, the four
+// phase partials combined in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void k_reduce_slabs(ReduceArgs g) {
+    __shared__ float part[4][65];
     const int r = blockIdx.y;
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + tx;
     const int n = g.row0 + r;
+    const bool bias_col = c == g.ncols && g.dst_b;
+    float v = 0.f;
     if (c < g.ncols) {
-        float s = 0.f;
-        for (int k = 0; k < g.splits; ++k) s += g.slab[(int64_t)k * g.slab_stride + (int64_t)n * g.ld_slab + c];
-        float* d = g.dst + (int64_t)r * g.ld_dst + c;
-        *d = g.accumulate ? *d + s : s;
-    } else if (c == g.ncols && g.dst_b) {
-        float s = 0.f;
-        for (int k = 0; k < g.splits; ++k) s += g.slab_b[(int64_t)k * g.N + n];
-        g.dst_b[r] = g.accumulate ? g.dst_b[r] + s : s;
+        const float* src = g.slab + (int64_t)n * g.ld_slab + c;
+        for (int k = ty; k < g.splits; k += 4) v += src[(int64_t)k * g.slab_stride];
+    } else if (bias_col) {
+        for (int k = ty; k < g.splits; k += 4) v += g.slab_b[(int64_t)k * g.N + n];
+    }
+    part[ty][tx] = v;
+    __syncthreads();
+    if (ty == 0 && (c < g.ncols || bias_col)) {
+        const float s = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
+        if (bias_col) {
+            g.dst_b[r] = g.accumulate ? g.dst_b[r] + s : s;
+        } else {
+            float* d = g.transpose ? g.dst + (int64_t)c * g.ld_dst + r : g.dst + (int64_t)r * g.ld_dst + c;
+            *d = g.accumulate ? *d + s : s;
+        }
+    }
+}
+
+// Skinny weight gradient: slab[chunk][m][k] = Σ_{p in chunk} a_m(p) · B[p][k] for m < Ma
+// (a_m(p) = A[p*lda + m], plus a_Ma(p) = 1 when `ones`, i.e. the column sums of B), and
+// slab_b[chunk][m] = Σ_{p in chunk} a_m(p).  Threads own float4 column groups; the rows of a
+// chunk are split over `rph` row phases whose partials are combined through LDS.
+template <int MA>
+__global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g) {
+    __shared__ float red[256 * 4];
+    const int tid = threadIdx.x;
+    const int kq = g.K >> 2;                      // float4 column groups (kq <= 256, checked on host)
+    const int rph = 256 / kq;                     // row phases
+    const int c4 = tid % kq, ph = tid / kq;
+    const bool live = ph < rph;
+    const int64_t p0 = (int64_t)blockIdx.x * g.chunk;
+    const int64_t p1 = min(g.P, p0 + g.chunk);
+    const int Mt = g.Ma + (g.ones ? 1 : 0);
+    f32x4 acc[MA + 1];
+    float asum[MA];
+#pragma unroll
+    for (int m = 0; m <= MA; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < MA; ++m) asum[m] = 0.f;
+    if (live)
+        for (int64_t p = p0 + ph; p < p1; p += rph) {
+            const f32x4 b = *reinterpret_cast<const f32x4*>(g.B + p * g.ldb + 4 * c4);
+            const float* ar = g.A + p * g.lda;
+#pragma unroll
+            for (int m = 0; m < MA; ++m)
+                if (m < g.Ma) {
+                    const float a = ar[m];
+                    acc[m] += a * b;
+                    asum[m] += a;
+                }
+            if (g.ones) acc[MA] += b;
+        }
+    // combine the row phases (every thread reaches every barrier)
+    for (int m = 0; m < Mt; ++m) {
+        f32x4 v = acc[0];
+#pragma unroll
+        for (int q = 0; q <= MA; ++q)
+            if (q == (m == g.Ma ? MA : m)) v = acc[q];
+        __syncthreads();
+        *reinterpret_cast<f32x4*>(red + 4 * tid) = v;
+        __syncthreads();
+        if (ph == 0) {
+            f32x4 sum = v;
+            for (int q = 1; q < rph; ++q) sum += *reinterpret_cast<const f32x4*>(red + 4 * (q * kq + c4));
+            *reinterpret_cast<f32x4*>(g.slab + ((int64_t)blockIdx.x * Mt + m) * g.K + 4 * c4) = sum;
+        }
+    }
+    if (g.slab_b) {
+        for (int m = 0; m < g.Ma; ++m) {
+            float v = 0.f;
+#pragma unroll
+            for (int q = 0; q < MA; ++q)
+                if (q == m) v = asum[q];
+            __syncthreads();
+            red[tid] = v;
+            __syncthreads();
+            if (tid == 0) {
+                float sum = 0.f;
+                for (int q = 0; q < rph; ++q) sum += red[q * kq];
+                g.slab_b[(int64_t)blockIdx.x * g.Ma + m] = sum;
+            }
+        }
     }
 }
 
@@ -247,9 +327,31 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s) {
     return SPNERF_OK;
 }
 
+int skinny_chunk(int64_t P) {
+    int64_t c = (P + 767) / 768;
+    c = (c + 63) / 64 * 64;
+    return (int)(c < 64 ? 64 : c);
+}
+
+int32_t tn_skinny(const SkinnyArgs& a0, hipStream_t s) {
+    SkinnyArgs a = a0;
+    SPN_ARG(a.Ma >= 1 && a.Ma <= 8 && a.K % 4 == 0 && a.K <= 1024 && a.ldb % 4 == 0, "tn_skinny: bad shape Ma=%d K=%d",
+            a.Ma, a.K);
+    a.chunk = skinny_chunk(a.P);
+    const int nb = cdiv(a.P, a.chunk);
+    if (nb == 0) return SPNERF_OK;
+    ProfScope prof("tn_skinny", s, 2.0 * a.P * a.K * (a.Ma + a.ones), 4.0 * a.P * (a.K + a.Ma));
+    if (a.Ma <= 1) hipLaunchKernelGGL(k_tn_skinny<1>, dim3(nb), dim3(256), 0, s, a);
+    else if (a.Ma <= 3) hipLaunchKernelGGL(k_tn_skinny<3>, dim3(nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_tn_skinny<8>, dim3(nb), dim3(256), 0, s, a);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
 int tn_splits(int P, int N, int K) {
     const int tiles = cdiv(N, 128) * cdiv(K, 128);
     int splits = cdiv(1024, tiles);
+    if (splits > 64) splits = 64;
     const int max_splits = cdiv(P, 256);
     if (splits > max_splits) splits = max_splits;
     return splits < 1 ? 1 : splits;
@@ -273,7 +375,7 @@ int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s) {
 int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s) {
     if (a.nrows <= 0) return SPNERF_OK;
     const int cols = a.ncols + 1;
-    hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(cols, 128), a.nrows), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(cols, 64), a.nrows), dim3(256), 0, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

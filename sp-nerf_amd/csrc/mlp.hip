@@ -140,16 +140,21 @@ __global__ __launch_bounds__(256) void k_ray_fwd(RayFwdArgs a) {
     }
 }
 
-__device__ __forceinline__ float dotv(const float* __restrict__ x, const float* __restrict__ w, int n) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    for (int k = 0; k < n; k += 4) {
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// lane-partial dot product of a row with a weight vector, columns 4*lane + 256*i
+__device__ __forceinline__ float pdot(const float* __restrict__ x, const float* __restrict__ w, int n, int lane) {
+    float s = 0.f;
+    for (int k = 4 * lane; k < n; k += 256) {
         const f32x4 a = *reinterpret_cast<const f32x4*>(x + k);
-        s0 += a[0] * w[k];
-        s1 += a[1] * w[k + 1];
-        s2 += a[2] * w[k + 2];
-        s3 += a[3] * w[k + 3];
+        const f32x4 b = *reinterpret_cast<const f32x4*>(w + k);
+        s += (a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3]);
     }
-    return (s0 + s1) + (s2 + s3);
+    return s;
 }
 
 struct HeadsArgs {
@@ -159,45 +164,56 @@ struct HeadsArgs {
     int64_t P; int S; int mode;  // mode: 0 full, 1 sigma only, 2 sigma + sun
 };
 
-// Narrow output heads, one thread per point (spnerf.py:333-367): σ = softplus, albedo =
-// sigmoid·1.002−0.001, sun = sigmoid, β = softplus, semantic logits; sky broadcast per ray.
+// Narrow output heads (spnerf.py:333-367): σ = softplus, albedo = sigmoid·1.002−0.001,
+// sun = sigmoid, β = softplus, semantic logits; sky broadcast per ray.  One wavefront per
+// point: every row read is a coalesced 1-KiB sweep, dot products end in a DPP reduction.
 __global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs a) {
-    const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (p >= a.P) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
     const Dims& d = a.d;
     const float* Pk = a.packed;
-    float* o = a.out + p * d.NO;
-    float* hs = a.hsave + p * 8;
-    const float spre = dotv(a.HL + p * d.W, Pk + a.k.wsig, d.W) + Pk[a.k.bsig];
-    o[3] = softplusf_(spre);
-    hs[0] = spre;
-    if (a.mode == 1) return;
-    const float sun = sigmoidf_(dotv(a.S3 + p * d.H, Pk + a.k.ws4, d.H) + Pk[a.k.bs4]);
-    o[4] = sun;
-    hs[4] = sun;
-    if (a.mode == 2) {
-        o[0] = o[1] = o[2] = o[5] = o[6] = o[7] = 0.f;
-        for (int c = 8; c < d.NO; ++c) o[c] = 0.f;
-        return;
-    }
-    const float* R1 = a.Q + p * d.NQ + d.H;
-    for (int c = 0; c < 3; ++c) {
-        const float s = sigmoidf_(dotv(R1, Pk + a.k.Wr2 + c * d.H, d.H) + Pk[a.k.br2 + c]);
-        hs[1 + c] = s;
-        o[c] = __fsub_rn(__fmul_rn(s, 1.002f), 0.001f);
-    }
-    const float* sk = a.sky + (p / a.S) * 4;
-    o[5] = sk[0];
-    o[6] = sk[1];
-    o[7] = sk[2];
-    if (d.beta) {
-        const float bpre = dotv(a.Q + p * d.NQ + 2 * d.H, Pk + a.k.wb2, d.H) + Pk[a.k.bb2];
-        hs[5] = bpre;
-        o[8] = softplusf_(bpre);
-    }
-    if (d.sem) {
-        const float* M1 = a.G + p * d.NG + d.W;
-        for (int c = 0; c < d.C; ++c) o[d.sem_col + c] = dotv(M1, Pk + a.k.Wm2 + c * d.H, d.H) + Pk[a.k.bm2 + c];
+    for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < a.P; p += nw) {
+        float* o = a.out + p * d.NO;
+        float* hs = a.hsave + p * 8;
+        const float spre = wsum(pdot(a.HL + p * d.W, Pk + a.k.wsig, d.W, lane)) + Pk[a.k.bsig];
+        float sun = 0.f, rgb[3] = {0.f, 0.f, 0.f}, bpre = 0.f;
+        if (a.mode != 1) sun = sigmoidf_(wsum(pdot(a.S3 + p * d.H, Pk + a.k.ws4, d.H, lane)) + Pk[a.k.bs4]);
+        if (a.mode == 0) {
+            const float* R1 = a.Q + p * d.NQ + d.H;
+            for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf_(wsum(pdot(R1, Pk + a.k.Wr2 + c * d.H, d.H, lane)) + Pk[a.k.br2 + c]);
+            if (d.beta) bpre = wsum(pdot(a.Q + p * d.NQ + 2 * d.H, Pk + a.k.wb2, d.H, lane)) + Pk[a.k.bb2];
+            if (d.sem) {
+                const float* M1 = a.G + p * d.NG + d.W;
+                for (int c = 0; c < d.C; ++c) {
+                    const float v = wsum(pdot(M1, Pk + a.k.Wm2 + c * d.H, d.H, lane)) + Pk[a.k.bm2 + c];
+                    if (lane == 0) o[d.sem_col + c] = v;
+                }
+            }
+        }
+        if (lane == 0) {
+            o[3] = softplusf_(spre);
+            hs[0] = spre;
+            if (a.mode == 1) continue;
+            o[4] = sun;
+            hs[4] = sun;
+            if (a.mode == 2) {
+                o[0] = o[1] = o[2] = o[5] = o[6] = o[7] = 0.f;
+                for (int c = 8; c < d.NO; ++c) o[c] = 0.f;
+                continue;
+            }
+            for (int c = 0; c < 3; ++c) {
+                hs[1 + c] = rgb[c];
+                o[c] = __fsub_rn(__fmul_rn(rgb[c], 1.002f), 0.001f);
+            }
+            const float* sk = a.sky + (p / a.S) * 4;
+            o[5] = sk[0];
+            o[6] = sk[1];
+            o[7] = sk[2];
+            if (d.beta) {
+                hs[5] = bpre;
+                o[8] = softplusf_(bpre);
+            }
+        }
     }
 }
 
@@ -208,106 +224,68 @@ struct HeadsBwdArgs {
     int64_t P; int mode;
 };
 
-// Backward of the narrow heads, one thread per point: per-point pre-activation gradients
-// (hpre, reduced over points into the head weights by k_tn_skinny) and the gradients of the
-// wide hidden layers that feed them (torch: Linear → dX = dY·W, then × sin' saved in D*).
+// Backward of the narrow heads, one wavefront per point: per-point pre-activation gradients
+// (hpre, reduced over points into the head weights by the skinny reduction) and the
+// gradients of the hidden layers feeding them (dX = dY·W, × sin' saved in D*), written as
+// coalesced rows.
 __global__ __launch_bounds__(256) void k_heads_bwd(HeadsBwdArgs a) {
-    const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (p >= a.P) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
     const Dims& d = a.d;
     const float* Pk = a.packed;
-    const float* g = a.d_out + p * d.NO;
-    const float* hs = a.hsave + p * 8;
-    float* hp = a.hpre + p * d.HP;
-    for (int c = 0; c < d.HP; ++c) hp[c] = 0.f;
-    hp[0] = softplus_grad(g[3], hs[0]);
-    if (a.mode == 1) return;
-    {
-        const float s = hs[4];
-        const float dys = g[4] * (1.f - s) * s;
-        hp[4] = dys;
-        const float* D = a.DS3 + p * d.H;
-        float* o = a.dS3 + p * d.H;
-        const float* w = Pk + a.k.ws4;
-        for (int k = 0; k < d.H; k += 4) {
-            const f32x4 dv = *reinterpret_cast<const f32x4*>(D + k);
-            f32x4 r;
-            for (int q = 0; q < 4; ++q) r[q] = dys * w[k + q] * dv[q];
-            *reinterpret_cast<f32x4*>(o + k) = r;
+    const int H = d.H;
+    for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < a.P; p += nw) {
+        const float* g = a.d_out + p * d.NO;
+        const float* hs = a.hsave + p * 8;
+        float* hp = a.hpre + p * d.HP;
+        const float dsig = softplus_grad(g[3], hs[0]);
+        float dys = 0.f, dy[3] = {0.f, 0.f, 0.f}, db = 0.f;
+        if (a.mode != 1) {
+            const float s = hs[4];
+            dys = g[4] * (1.f - s) * s;
         }
-    }
-    if (a.mode == 2) return;
-    float dy[3];
-    for (int c = 0; c < 3; ++c) {
-        const float s = hs[1 + c];
-        dy[c] = g[c] * 1.002f * (1.f - s) * s;
-        hp[1 + c] = dy[c];
-    }
-    {
-        const float* D = a.DQ + p * d.NQ + d.H;
-        float* o = a.dZQ + p * d.NQ + d.H;
-        const float* w = Pk + a.k.Wr2;
-        for (int k = 0; k < d.H; k += 4) {
-            const f32x4 dv = *reinterpret_cast<const f32x4*>(D + k);
-            f32x4 r;
-            for (int q = 0; q < 4; ++q)
-                r[q] = (dy[0] * w[k + q] + dy[1] * w[d.H + k + q] + dy[2] * w[2 * d.H + k + q]) * dv[q];
-            *reinterpret_cast<f32x4*>(o + k) = r;
+        if (a.mode == 0) {
+            for (int c = 0; c < 3; ++c) {
+                const float s = hs[1 + c];
+                dy[c] = g[c] * 1.002f * (1.f - s) * s;
+            }
+            if (d.beta) db = softplus_grad(g[8], hs[5]);
         }
-    }
-    if (d.beta) {
-        const float db = softplus_grad(g[8], hs[5]);
-        hp[5] = db;
-        const float* D = a.DQ + p * d.NQ + 2 * d.H;
-        float* o = a.dZQ + p * d.NQ + 2 * d.H;
-        const float* w = Pk + a.k.wb2;
-        for (int k = 0; k < d.H; k += 4) {
-            const f32x4 dv = *reinterpret_cast<const f32x4*>(D + k);
-            f32x4 r;
-            for (int q = 0; q < 4; ++q) r[q] = db * w[k + q] * dv[q];
-            *reinterpret_cast<f32x4*>(o + k) = r;
-        }
-    }
-    if (d.sem) {
-        float gs[32];
-        for (int c = 0; c < d.C; ++c) {
-            gs[c] = g[d.sem_col + c];
-            hp[6 + c] = gs[c];
-        }
-        const float* D = a.DG + p * d.NG + d.W;
-        float* o = a.dZG + p * d.NG + d.W;
-        const float* w = Pk + a.k.Wm2;
-        for (int k = 0; k < d.H; ++k) {
+        for (int c = lane; c < d.HP; c += 64) {
             float v = 0.f;
-            for (int c = 0; c < d.C; ++c) v += gs[c] * w[c * d.H + k];
-            o[k] = v * D[k];
+            if (c == 0) v = dsig;
+            else if (c <= 3) v = dy[c - 1];
+            else if (c == 4) v = dys;
+            else if (c == 5) v = db;
+            else if (a.mode == 0) v = g[d.sem_col + c - 6];
+            hp[c] = v;
         }
-    }
-}
-
-// slab[chunk][m][k] = Σ_{p in chunk} A[p*lda + m] * B[p*ldb + k]   (m < Ma ≤ 8)
-// slab_b[chunk][m]  = Σ_{p in chunk} A[p*lda + m]
-__global__ __launch_bounds__(256) void k_tn_skinny(const float* __restrict__ A, int lda, int Ma,
-                                                   const float* __restrict__ B, int ldb, int K, int64_t P,
-                                                   int chunk, float* __restrict__ slab, float* __restrict__ slab_b) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t p0 = (int64_t)blockIdx.y * chunk;
-    const int64_t p1 = min(P, p0 + chunk);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (k < K) {
-        for (int64_t p = p0; p < p1; ++p) {
-            const float b = B[p * ldb + k];
-            const float* ar = A + p * lda;
-#pragma unroll
-            for (int m = 0; m < 8; ++m)
-                if (m < Ma) acc[m] += ar[m] * b;
+        if (a.mode == 1) continue;
+        for (int k = 4 * lane; k < H; k += 256) {
+            const f32x4 D = *reinterpret_cast<const f32x4*>(a.DS3 + p * H + k);
+            const f32x4 w = *reinterpret_cast<const f32x4*>(Pk + a.k.ws4 + k);
+            *reinterpret_cast<f32x4*>(a.dS3 + p * H + k) = (dys * w) * D;
         }
-        for (int m = 0; m < Ma; ++m) slab[((int64_t)blockIdx.y * Ma + m) * K + k] = acc[m];
-    }
-    if (blockIdx.x == 0 && threadIdx.x < Ma) {
-        float s = 0.f;
-        for (int64_t p = p0; p < p1; ++p) s += A[p * lda + threadIdx.x];
-        slab_b[(int64_t)blockIdx.y * Ma + threadIdx.x] = s;
+        if (a.mode == 2) continue;
+        for (int k = 4 * lane; k < H; k += 256) {
+            const f32x4 D = *reinterpret_cast<const f32x4*>(a.DQ + p * d.NQ + H + k);
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(Pk + a.k.Wr2 + k);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(Pk + a.k.Wr2 + H + k);
+            const f32x4 w2 = *reinterpret_cast<const f32x4*>(Pk + a.k.Wr2 + 2 * H + k);
+            *reinterpret_cast<f32x4*>(a.dZQ + p * d.NQ + H + k) = (dy[0] * w0 + dy[1] * w1 + dy[2] * w2) * D;
+            if (d.beta) {
+                const f32x4 Db = *reinterpret_cast<const f32x4*>(a.DQ + p * d.NQ + 2 * H + k);
+                const f32x4 wb = *reinterpret_cast<const f32x4*>(Pk + a.k.wb2 + k);
+                *reinterpret_cast<f32x4*>(a.dZQ + p * d.NQ + 2 * H + k) = (db * wb) * Db;
+            }
+            if (d.sem) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                for (int c = 0; c < d.C; ++c)
+                    acc += g[d.sem_col + c] * *reinterpret_cast<const f32x4*>(Pk + a.k.Wm2 + c * H + k);
+                const f32x4 Dm = *reinterpret_cast<const f32x4*>(a.DG + p * d.NG + d.W + k);
+                *reinterpret_cast<f32x4*>(a.dZG + p * d.NG + d.W + k) = acc * Dm;
+            }
+        }
     }
 }
 
@@ -326,7 +304,8 @@ __global__ void k_ray_rowsum(const float* __restrict__ in, int ld, int c0, int N
 struct RayBwdArgs {
     const float* packed; Packed k; Dims d;
     const float *sky, *skyh, *dsky, *R0, *R4, *RQ;
-    float *skyd, *skydh, *gemb, *grad_t;
+    const int64_t* labels;
+    float *skyd, *skydh, *gemb, *embr, *grad_t;
     int sem_on, beta_on, sky_on;
 };
 
@@ -352,6 +331,9 @@ __global__ __launch_bounds__(256) void k_ray_bwd(RayBwdArgs a) {
     }
     __shared__ float red[256];
     if (a.sem_on) {
+        int64_t lab = a.labels[ray];
+        if (lab == -100) lab = d.C;
+        for (int j = tid; j < d.sd; j += blockDim.x) a.embr[ray * d.sd + j] = P[a.k.emb + lab * d.sd + j];
         for (int j = 0; j < d.sd; ++j) {
             float acc = 0.f;
             for (int n = tid; n < d.W; n += blockDim.x)
@@ -382,31 +364,6 @@ __global__ __launch_bounds__(256) void k_ray_bwd(RayBwdArgs a) {
             __syncthreads();
         }
     }
-}
-
-// out[n*ldo + j] = Σ_ray X[ray*ldx + n] * Y[row(ray)*ldy + j]   (Y == nullptr → Σ_ray X[ray][n])
-// row(ray) = ray, or the embedding row of the ray's label when `labels` is given.
-__global__ void k_ray_outer(int64_t B, const float* __restrict__ X, int ldx, int N, const float* __restrict__ Y,
-                            int ldy, int J, const int64_t* __restrict__ labels, int pad_row, float* __restrict__ out,
-                            int ldo) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int Jn = Y ? J : 1;
-    if (i >= N * Jn) return;
-    const int n = i / Jn, j = i % Jn;
-    float s = 0.f;
-    for (int64_t r = 0; r < B; ++r) {
-        float y = 1.f;
-        if (Y) {
-            int64_t row = r;
-            if (labels) {
-                row = labels[r];
-                if (row == -100) row = pad_row;
-            }
-            y = Y[row * ldy + j];
-        }
-        s += X[r * ldx + n] * y;
-    }
-    out[(int64_t)n * ldo + j] = s;
 }
 
 // d_emb[c][j] = Σ_{rays with label c} gemb[ray][j]; the padding row (−100 → C) gets none
@@ -546,19 +503,26 @@ static ReduceArgs red(int row0, int nrows, int ncols, float* dst, int ld_dst, fl
     return r;
 }
 
-static int32_t skinny(const Ctx& c, const float* A, int lda, int Ma, const float* B, int ldb, int K, float* dstW,
-                      float* dstb, hipStream_t s) {
-    const int64_t P = c.w.P;
-    const int chunk = 2048;
-    const int chunks = cdiv(P, chunk);
-    float* slab = c.at(c.w.sk_slab);
-    float* slab_b = c.at(c.w.sk_slab_b);
-    hipLaunchKernelGGL(k_tn_skinny, dim3(cdiv(K, 256), chunks), dim3(256), 0, s, A, lda, Ma, B, ldb, K, P, chunk, slab,
-                       slab_b);
-    SPN_HIP(hipGetLastError());
-    ReduceArgs r = red(0, Ma, K, dstW, K, dstb);
-    r.slab = slab; r.ld_slab = K; r.slab_stride = (int64_t)Ma * K; r.splits = chunks; r.N = Ma; r.slab_b = slab_b;
-    return reduce_slabs(r, s);
+// out[m][k] = Σ_r A[r*lda+m] · B[r*ldb+k] over `rows` rows (points or rays), written to dst
+// (row-major, or dst[k][m] with `transpose`); dst_b[m] = Σ_r A[r][m]; dst_ones[k] = Σ_r B[r][k].
+static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int Ma, const float* B, int ldb, int K,
+                      float* dst, int ld_dst, int transpose, float* dst_b, float* dst_ones, hipStream_t s) {
+    SkinnyArgs k;
+    k.A = A; k.lda = lda; k.Ma = Ma; k.B = B; k.ldb = ldb; k.K = K; k.P = rows; k.ones = dst_ones ? 1 : 0;
+    k.slab = c.at(c.w.sk_slab); k.slab_b = c.at(c.w.sk_slab_b);
+    SPN_TRY(tn_skinny(k, s));
+    const int chunks = cdiv(rows, skinny_chunk(rows));
+    const int Mt = Ma + k.ones;
+    ReduceArgs r = red(0, Ma, K, dst, ld_dst, dst_b);
+    r.slab = k.slab; r.ld_slab = K; r.slab_stride = (int64_t)Mt * K; r.splits = chunks; r.N = Mt; r.slab_b = k.slab_b;
+    r.transpose = transpose;
+    if (dst) SPN_TRY(reduce_slabs(r, s));
+    if (dst_ones) {
+        ReduceArgs o = r;
+        o.row0 = Ma; o.nrows = 1; o.dst = dst_ones; o.ld_dst = K; o.dst_b = nullptr; o.transpose = 0;
+        SPN_TRY(reduce_slabs(o, s));
+    }
+    return SPNERF_OK;
 }
 
 static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays, int rs, int dir_off,
@@ -669,7 +633,7 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
     {
         HeadsArgs a{packed, c.k, d, HL, c.at(c.w.G), c.at(c.w.Q), S3buf, c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode};
         ProfScope prof("heads_fwd", s, 2.0 * P * (W + (mode != 1 ? 4 * H + H * d.C : 0)), 4.0 * P * (W + 3 * H + d.NO));
-        hipLaunchKernelGGL(k_heads_fwd, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_heads_fwd, dim3((unsigned)std::min<int64_t>(cdiv(P, 4), 8192)), dim3(256), 0, s, a);
         SPN_HIP(hipGetLastError());
     }
     return SPNERF_OK;
@@ -707,16 +671,16 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
         HeadsBwdArgs a{packed, c.k, d, d_out, c.at(c.w.hsave), c.at(c.w.DQ), c.at(c.w.DG), c.at(c.w.DS3),
                        hpre, dZQ, dZG, dS3, P, mode};
         ProfScope prof("heads_bwd", s, 2.0 * P * 4 * H, 4.0 * P * (d.NO + 3 * H + 3 * H));
-        hipLaunchKernelGGL(k_heads_bwd, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_heads_bwd, dim3((unsigned)std::min<int64_t>(cdiv(P, 4), 8192)), dim3(256), 0, s, a);
         SPN_HIP(hipGetLastError());
     }
     // 2. narrow-head weights: reductions over points
-    SPN_TRY(skinny(c, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), gp(x.sigb), s));
-    SPN_TRY(skinny(c, hpre + 4, d.HP, 1, c.at(c.w.S3), H, H, gp(x.s4W), gp(x.s4b), s));
+    SPN_TRY(skinny(c, P, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), W, 0, gp(x.sigb), nullptr, s));
+    SPN_TRY(skinny(c, P, hpre + 4, d.HP, 1, c.at(c.w.S3), H, H, gp(x.s4W), H, 0, gp(x.s4b), nullptr, s));
     if (mode == 0) {
-        SPN_TRY(skinny(c, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), gp(x.r2b), s));
-        if (d.beta) SPN_TRY(skinny(c, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), gp(x.b2b), s));
-        if (d.sem) SPN_TRY(skinny(c, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), gp(x.m2b), s));
+        SPN_TRY(skinny(c, P, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), H, 0, gp(x.r2b), nullptr, s));
+        if (d.beta) SPN_TRY(skinny(c, P, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), H, 0, gp(x.b2b), nullptr, s));
+        if (d.sem) SPN_TRY(skinny(c, P, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), H, 0, gp(x.m2b), nullptr, s));
     }
     // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
     {
@@ -810,29 +774,26 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
             SPN_HIP(hipGetLastError());
         }
         RayBwdArgs a{packed, c.k, d, c.at(c.w.sky), c.at(c.w.skyh), c.at(c.w.dsky), c.at(c.w.R0), c.at(c.w.R4),
-                     c.at(c.w.RQ), c.at(c.w.skyd), c.at(c.w.skydh), c.at(c.w.gemb), grad_t,
+                     c.at(c.w.RQ), labels, c.at(c.w.skyd), c.at(c.w.skydh), c.at(c.w.gemb), c.at(c.w.embr), grad_t,
                      d.sem ? 1 : 0, (d.beta && mode == 0) ? 1 : 0, sky_on};
         hipLaunchKernelGGL(k_ray_bwd, dim3((unsigned)n_rays), dim3(256), 0, s, a);
         SPN_HIP(hipGetLastError());
         const float* sun = rays + 8;
-        auto outer = [&](const float* X, int ldx, int N, const float* Y, int ldy, int J, const int64_t* lab, float* o, int ldo) {
-            const int n = N * (Y ? J : 1);
-            hipLaunchKernelGGL(k_ray_outer, dim3(cdiv(n, 128)), dim3(128), 0, s, n_rays, X, ldx, N, Y, ldy, J, lab, d.C, o, ldo);
-            return hipGetLastError();
-        };
-        SPN_HIP(outer(c.at(c.w.RQ), d.NQ, H, sun, rs, 3, nullptr, gp(x.s1W) + W, ld(x.s1W)));
+        const int64_t B = n_rays;
+        // sun_v_net.0 sun-direction columns: dW[n][W+j] = Σ_ray RQ[ray][n] sun[ray][j]
+        SPN_TRY(skinny(c, B, sun, rs, 3, c.at(c.w.RQ), d.NQ, H, gp(x.s1W) + W, ld(x.s1W), 1, nullptr, nullptr, s));
         if (sky_on) {
-            SPN_HIP(outer(c.at(c.w.skydh), H, H, sun, rs, 3, nullptr, gp(x.k1W), 3));
-            SPN_HIP(outer(c.at(c.w.skydh), H, H, nullptr, 0, 1, nullptr, gp(x.k1b), 1));
-            SPN_HIP(outer(c.at(c.w.skyd), 4, 3, c.at(c.w.skyh), H, H, nullptr, gp(x.k2W), H));
-            SPN_HIP(outer(c.at(c.w.skyd), 4, 3, nullptr, 0, 1, nullptr, gp(x.k2b), 1));
+            SPN_TRY(skinny(c, B, sun, rs, 3, c.at(c.w.skydh), H, H, gp(x.k1W), 3, 1, nullptr, gp(x.k1b), s));
+            SPN_TRY(skinny(c, B, c.at(c.w.skyd), 4, 3, c.at(c.w.skyh), H, H, gp(x.k2W), H, 0, gp(x.k2b), nullptr, s));
         }
         if (d.beta && mode == 0)
-            SPN_HIP(outer(c.at(c.w.RQ) + 2 * H, d.NQ, H, temb, d.td, d.td, nullptr, gp(x.b1W) + W, ld(x.b1W)));
+            SPN_TRY(skinny(c, B, temb, d.td, d.td, c.at(c.w.RQ) + 2 * H, d.NQ, H, gp(x.b1W) + W, ld(x.b1W), 1, nullptr,
+                           nullptr, s));
         if (d.sem) {
-            SPN_HIP(outer(c.at(c.w.R0), W, W, c.pk(c.k.emb), d.sd, d.sd, labels, gp(x.fcW[0]) + d.K0, ld(x.fcW[0])));
-            SPN_HIP(outer(c.at(c.w.R4), W, W, c.pk(c.k.emb), d.sd, d.sd, labels, gp(x.fcW[d.skip]) + W + d.K0,
-                          ld(x.fcW[d.skip])));
+            SPN_TRY(skinny(c, B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R0), W, W, gp(x.fcW[0]) + d.K0, ld(x.fcW[0]), 1,
+                           nullptr, nullptr, s));
+            SPN_TRY(skinny(c, B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R4), W, W, gp(x.fcW[d.skip]) + W + d.K0,
+                           ld(x.fcW[d.skip]), 1, nullptr, nullptr, s));
             hipLaunchKernelGGL(k_class_sum, dim3(cdiv((d.C + 1) * d.sd, 64)), dim3(64), 0, s, n_rays, c.at(c.w.gemb),
                                d.sd, labels, d.C, gp(x.emb));
             SPN_HIP(hipGetLastError());

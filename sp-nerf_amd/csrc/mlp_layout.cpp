@@ -1,6 +1,8 @@
 // Parameter / packed-weight / workspace layouts (host only).
 #include "mlp_layout.h"
 
+#include <algorithm>
+
 #include "gemm_f32.h"
 
 namespace spn {
@@ -211,9 +213,10 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         w.skyd = take(B * 4);
         w.skydh = take(B * H);
         w.gemb = take(B * (d.sd ? d.sd : 1));
-        const int64_t chunks = (P + 2047) / 2048;
-        w.sk_slab = take(chunks * 8 * W);
-        w.sk_slab_b = take(chunks * 8);
+        w.embr = take(B * (d.sd ? d.sd : 1));
+        const int64_t chunks = std::max((P + skinny_chunk(P) - 1) / skinny_chunk(P), (B + skinny_chunk(B) - 1) / skinny_chunk(B));
+        w.sk_slab = take(chunks * 9 * W);
+        w.sk_slab_b = take(chunks * 9);
     }
     w.total = off;
     return w;
