@@ -53,11 +53,15 @@ struct ReduceArgs {
     int transpose = 0;  // dst[c][r] instead of dst[r][c]
 };
 
-int32_t gemm_nt(const NTArgs& a, hipStream_t s);
+// variant: -1 = library default (g_nt_variant); 0 = K-step 32, 1 LDS stage; 1 = 64/1;
+// 2 = 32 with double-buffered LDS; 3 = 64 double-buffered
+extern int g_nt_variant;
+int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant = -1);
 int tn_splits(int P, int N, int K);
 int skinny_chunk(int64_t P);
 int32_t tn_skinny(const SkinnyArgs& a, hipStream_t s);
-int32_t gemm_tn(const TNArgs& a, int splits, hipStream_t s);
+extern int g_tn_variant;  // 0 = one LDS stage, 1 = double-buffered
+int32_t gemm_tn(const TNArgs& a, int splits, hipStream_t s, int variant = -1);
 int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s);
 
 }  // namespace spn

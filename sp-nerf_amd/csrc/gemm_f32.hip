@@ -21,30 +21,44 @@ constexpr int BM = 128, BN = 128, BK = 32, LDK = BK + 4;
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
+// NT main loop variants: KS = K-step depth (32 or 64), ST = LDS stages (1: register prefetch,
+// two barriers per K-step; 2: double-buffered LDS, one barrier per K-step).
+template <int KS, int ST>
 __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
-    __shared__ __attribute__((aligned(16))) float sA[BM * LDK];
-    __shared__ __attribute__((aligned(16))) float sB[BN * LDK];
+    constexpr int LK = KS + 4;                    // padded LDS row (floats): conflict-free b128 reads
+    constexpr int NLD = KS / 8;                   // float4 loads per thread per operand per K-step
+    __shared__ __attribute__((aligned(16))) float smem[ST * 2 * BM * LK];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nN = (g.N + BN - 1) / BN;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int bm = (t / nN) * BM, bn = (t % nN) * BN;
-    const int lr = tid >> 3, lk = (tid & 7) * 4;
+    const int lr = tid / (KS / 4), lk = (tid % (KS / 4)) * 4;
+    constexpr int RSTEP = 256 / (KS / 4);         // rows covered by one pass of the block
 
-    f32x4 ra[4], rb[4];
+    f32x4 ra[NLD], rb[NLD];
     auto gload = [&](int k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = bm + lr + 32 * i;
+        for (int i = 0; i < NLD; ++i) {
+            const int row = bm + lr + RSTEP * i;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if (row < g.M) {
                 if (k0 < g.K1) v = ld4(g.A + (int64_t)row * g.lda + k0 + lk);
                 else v = ld4(g.A2 + (int64_t)row * g.lda2 + (k0 - g.K1) + lk);
             }
             ra[i] = v;
-            const int col = bn + lr + 32 * i;
+            const int col = bn + lr + RSTEP * i;
             f32x4 w = {0.f, 0.f, 0.f, 0.f};
             if (col < g.N) w = ld4(g.B + (int64_t)col * g.ldb + k0 + lk);
             rb[i] = w;
+        }
+    };
+    auto sstore = [&](int stg) {
+        float* sA = smem + stg * 2 * BM * LK;
+        float* sB = sA + BM * LK;
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            *reinterpret_cast<f32x4*>(sA + (lr + RSTEP * i) * LK + lk) = ra[i];
+            *reinterpret_cast<f32x4*>(sB + (lr + RSTEP * i) * LK + lk) = rb[i];
         }
     };
 
@@ -57,23 +71,14 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int wr = wid >> 1, wc = wid & 1, r32 = lane & 31, h = lane >> 5;
-    const float* pa0 = sA + (wr * 64 + r32) * LDK + 4 * h;
-    const float* pa1 = pa0 + 32 * LDK;
-    const float* pb0 = sB + (wc * 64 + r32) * LDK + 4 * h;
-    const float* pb1 = pb0 + 32 * LDK;
-
-    gload(0);
-    for (int k0 = 0; k0 < g.K; k0 += BK) {
-        __syncthreads();
+    auto compute = [&](int stg) {
+        const float* sA = smem + stg * 2 * BM * LK;
+        const float* pa0 = sA + (wr * 64 + r32) * LK + 4 * h;
+        const float* pa1 = pa0 + 32 * LK;
+        const float* pb0 = sA + BM * LK + (wc * 64 + r32) * LK + 4 * h;
+        const float* pb1 = pb0 + 32 * LK;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            *reinterpret_cast<f32x4*>(sA + (lr + 32 * i) * LDK + lk) = ra[i];
-            *reinterpret_cast<f32x4*>(sB + (lr + 32 * i) * LDK + lk) = rb[i];
-        }
-        __syncthreads();
-        if (k0 + BK < g.K) gload(k0 + BK);
-#pragma unroll
-        for (int kg = 0; kg < BK / 8; ++kg) {
+        for (int kg = 0; kg < KS / 8; ++kg) {
             const f32x4 a0 = ld4(pa0 + kg * 8), a1 = ld4(pa1 + kg * 8);
             const f32x4 b0 = ld4(pb0 + kg * 8), b1 = ld4(pb1 + kg * 8);
 #pragma unroll
@@ -84,12 +89,70 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
                 acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
             }
         }
+    };
+
+    const int nk = g.K / KS;
+    gload(0);
+    if (ST == 1) {
+        for (int kt = 0; kt < nk; ++kt) {
+            __syncthreads();
+            sstore(0);
+            __syncthreads();
+            if (kt + 1 < nk) gload((kt + 1) * KS);
+            compute(0);
+        }
+    } else {
+        sstore(0);
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) gload((kt + 1) * KS);
+            compute(kt & 1);
+            if (kt + 1 < nk) sstore((kt + 1) & 1);
+            __syncthreads();
+        }
     }
 
-    // epilogue: each wave stages one 32x32 accumulator tile at a time in LDS (acc reg r sits at
-    // row (r&3)+8(r>>2)+4h, column lane&31) and walks it back row-major, so every global access
-    // of the epilogue (rowbias, Dmul, Dout, C) is a 128-B row segment and sincos is not unrolled.
-    float* stage = sA + wid * 1024;
+    const int row0 = bm + wr * 64 + 4 * h;  // + i*32 + (r&3) + 8(r>>2)
+    if (g.act == 0 || bn + BN <= g.n_lin) {
+        // Linear epilogue (backward dX, feature layer): applied in the accumulator layout —
+        // for a fixed register r the 32 lanes of a half-wave touch 32 consecutive columns of one
+        // row, so every Dmul / rowbias / C access is a 128-B segment and, fully unrolled, all
+        // loads of the tile are in flight together.
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = bn + wc * 64 + j * 32 + r32;
+            if (col >= g.N) continue;
+            const float bias = g.bias ? g.bias[col] : 0.f;
+            const float r1v = g.r1_a ? g.r1_v[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                float dm[16], rbv[16], r1[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = row0 + i * 32 + (r & 3) + 8 * (r >> 2);
+                    const bool ok = row < g.M;
+                    dm[r] = (g.Dmul && ok) ? g.Dmul[(int64_t)row * g.ld_dmul + col] : 1.f;
+                    rbv[r] = (g.rowbias && ok) ? g.rowbias[(int64_t)(row / g.rows_per_ray) * g.ld_rb + col] : 0.f;
+                    r1[r] = (g.r1_a && ok) ? g.r1_a[(int64_t)row * g.r1_lda] : 0.f;
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = row0 + i * 32 + (r & 3) + 8 * (r >> 2);
+                    if (row >= g.M) continue;
+                    float v = acc[i][j][r] + bias;
+                    v += rbv[r];
+                    if (g.r1_a) v += r1[r] * r1v;
+                    if (g.Dout) g.Dout[(int64_t)row * g.ld_dout + col] = 1.f;
+                    g.C[(int64_t)row * g.ldc + col] = g.Dmul ? v * dm[r] : v;
+                }
+            }
+        }
+        return;
+    }
+    // Sine epilogue: each wave stages one 32x32 accumulator tile at a time in LDS and walks it
+    // back row-major, so global accesses are 128-B row segments and sincos is not unrolled 64x.
+    float* stage = smem + wid * 1024;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -103,7 +166,7 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
             const float bias = g.bias ? g.bias[col] : 0.f;
             const bool sine = g.act == 1 && col >= g.n_lin;
             const float r1v = g.r1_a ? g.r1_v[col] : 0.f;
-#pragma unroll 2
+#pragma unroll 4
             for (int e = 0; e < 16; ++e) {
                 const int rr = 2 * e + h;
                 const int row = bm + wr * 64 + i * 32 + rr;
@@ -127,10 +190,10 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
     }
 }
 
+template <int ST>
 __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
     constexpr int LDN = 128;
-    __shared__ __attribute__((aligned(16))) float sA[BK * LDN];
-    __shared__ __attribute__((aligned(16))) float sB[BK * LDN];
+    __shared__ __attribute__((aligned(16))) float smem[ST * 2 * BK * LDN];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nK = (g.K + 127) / 128;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -158,6 +221,15 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
             rb[i] = w;
         }
     };
+    auto sstore = [&](int stg) {
+        float* sA = smem + stg * 2 * BK * LDN;
+        float* sB = sA + BK * LDN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            *reinterpret_cast<f32x4*>(sA + (lr + 8 * i) * LDN + lc) = ra[i];
+            *reinterpret_cast<f32x4*>(sB + (lr + 8 * i) * LDN + lc) = rb[i];
+        }
+    };
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -170,17 +242,9 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
     const bool do_bias = g.slab_b != nullptr && k0 == 0 && tid < 128;
     float bsum = 0.f;
     const int wr = wid >> 1, wc = wid & 1, r32 = lane & 31, h = lane >> 5;
-
-    if (p_beg < p_end) gload(p_beg);
-    for (int p0 = p_beg; p0 < p_end; p0 += BK) {
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            *reinterpret_cast<f32x4*>(sA + (lr + 8 * i) * LDN + lc) = ra[i];
-            *reinterpret_cast<f32x4*>(sB + (lr + 8 * i) * LDN + lc) = rb[i];
-        }
-        __syncthreads();
-        if (p0 + BK < p_end) gload(p0 + BK);
+    auto compute = [&](int stg) {
+        const float* sA = smem + stg * 2 * BK * LDN;
+        const float* sB = sA + BK * LDN;
         if (do_bias) {
 #pragma unroll 8
             for (int q = 0; q < BK; ++q) bsum += sA[q * LDN + tid];
@@ -197,6 +261,29 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
                 acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
                 acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
             }
+        }
+    };
+
+    if (p_beg < p_end) gload(p_beg);
+    if (ST == 1) {
+        for (int p0 = p_beg; p0 < p_end; p0 += BK) {
+            __syncthreads();
+            sstore(0);
+            __syncthreads();
+            if (p0 + BK < p_end) gload(p0 + BK);
+            compute(0);
+        }
+    } else if (p_beg < p_end) {
+        sstore(0);
+        __syncthreads();
+        int stg = 0;
+        for (int p0 = p_beg; p0 < p_end; p0 += BK) {
+            const bool more = p0 + BK < p_end;
+            if (more) gload(p0 + BK);
+            compute(stg);
+            if (more) sstore(stg ^ 1);
+            __syncthreads();
+            stg ^= 1;
         }
     }
 
@@ -313,7 +400,9 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g) {
     }
 }
 
-int32_t gemm_nt(const NTArgs& a, hipStream_t s) {
+int g_nt_variant = 2;
+
+int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
     SPN_ARG(a.K % BK == 0 && a.K1 % BK == 0 && a.K1 <= a.K, "gemm_nt: K=%d/K1=%d must be multiples of %d", a.K, a.K1, BK);
     SPN_ARG(a.K1 == a.K || a.A2 != nullptr, "gemm_nt: second A segment missing");
@@ -322,7 +411,11 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s) {
     if (a.M == 0) return SPNERF_OK;
     const int nb = cdiv(a.M, BM) * cdiv(a.N, BN);
     ProfScope prof("gemm_nt_f32", s, 2.0 * a.M * a.N * a.K, 4.0 * ((double)a.M * a.K + (double)a.N * a.K + 2.0 * a.M * a.N));
-    hipLaunchKernelGGL(k_gemm_nt, dim3(nb), dim3(256), 0, s, a);
+    const int v = variant >= 0 ? variant : g_nt_variant;
+    if (v == 1 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 1>), dim3(nb), dim3(256), 0, s, a);
+    else if (v == 2) hipLaunchKernelGGL((k_gemm_nt<32, 2>), dim3(nb), dim3(256), 0, s, a);
+    else if (v == 3 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 2>), dim3(nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_gemm_nt<32, 1>), dim3(nb), dim3(256), 0, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
@@ -357,7 +450,9 @@ int tn_splits(int P, int N, int K) {
     return splits < 1 ? 1 : splits;
 }
 
-int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s) {
+int g_tn_variant = 1;
+
+int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s, int variant) {
     TNArgs a = a0;
     SPN_ARG(a.N > 0 && a.K > 0 && a.P >= 0, "gemm_tn: bad shape");
     SPN_ARG(a.N % 4 == 0 && a.K % 4 == 0 && a.K1 % 4 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm_tn: dims must be /4");
@@ -367,7 +462,9 @@ int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s) {
     a.p_per_split = pps < BK ? BK : pps;
     const int nb = cdiv(a.N, 128) * cdiv(a.K, 128);
     ProfScope prof("gemm_tn_f32", s, 2.0 * a.P * a.N * a.K, 4.0 * ((double)a.P * (a.N + a.K) + (double)splits * a.N * a.K));
-    hipLaunchKernelGGL(k_gemm_tn, dim3(nb, splits), dim3(256), 0, s, a);
+    const int v = variant >= 0 ? variant : g_tn_variant;
+    if (v == 1) hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nb, splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nb, splits), dim3(256), 0, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

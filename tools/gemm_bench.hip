@@ -1,0 +1,97 @@
+// Standalone timing of the fp32 MFMA GEMM kernels (tools only; not part of the library ABI).
+//   make -C tools gemm_bench && ./tools/gemm_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../sp-nerf_amd/csrc/gemm_f32.h"
+
+using namespace spn;
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t e = (x);                                                \
+        if (e != hipSuccess) {                                             \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); \
+            exit(1);                                                       \
+        }                                                                  \
+    } while (0)
+
+static float* rnd(size_t n, float scale, unsigned seed) {
+    std::vector<float> h(n);
+    srand(seed);
+    for (auto& v : h) v = scale * (2.f * rand() / RAND_MAX - 1.f);
+    float* d;
+    CK(hipMalloc(&d, n * 4));
+    CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+    return d;
+}
+
+template <typename F>
+static double time_it(F f, int iters = 20) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) f();
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < iters; ++i) f();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return 1e3 * ms / iters;  // us
+}
+
+int main(int argc, char** argv) {
+    const int M = argc > 1 ? atoi(argv[1]) : 65536, N = 512, K = 512;
+    float* A = rnd((size_t)M * K, 1.f, 1);
+    float* B = rnd((size_t)N * K, 0.1f, 2);
+    float* bias = rnd(N, 0.1f, 3);
+    float *C, *D, *slab, *slab_b;
+    CK(hipMalloc(&C, (size_t)M * N * 4));
+    CK(hipMalloc(&D, (size_t)M * N * 4));
+    CK(hipMalloc(&slab, (size_t)64 * N * K * 4));
+    CK(hipMalloc(&slab_b, (size_t)64 * N * 4));
+    const double flop = 2.0 * M * N * K;
+    auto report = [&](const char* name, double us) { printf("%-34s %9.1f us  %6.1f TF/s\n", name, us, flop / us * 1e-6); };
+
+    NTArgs g;
+    g.A = A; g.lda = K; g.K1 = K; g.B = B; g.ldb = K; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K;
+    for (int v = 0; v < 4; ++v) {
+        char nm[64];
+        snprintf(nm, 64, "nt plain variant %d", v);
+        report(nm, time_it([&] { gemm_nt(g, 0, v); }));
+    }
+    for (int v = 0; v < 4; ++v) {
+        NTArgs f = g;
+        f.bias = bias; f.act = 1; f.w0 = 1.f; f.Dout = D; f.ld_dout = N;
+        char nm[64];
+        snprintf(nm, 64, "nt fwd variant %d", v);
+        report(nm, time_it([&] { gemm_nt(f, 0, v); }));
+    }
+    NTArgs f = g;
+    f.bias = bias; f.act = 1; f.w0 = 1.f; f.Dout = D; f.ld_dout = N;
+    report("nt fwd: bias+sincos+Dout", time_it([&] { gemm_nt(f, 0); }));
+    NTArgs f2 = f;
+    f2.Dout = nullptr;
+    report("nt fwd: bias+sin, no Dout", time_it([&] { gemm_nt(f2, 0); }));
+    NTArgs b = g;
+    b.Dmul = D; b.ld_dmul = N;
+    report("nt bwd: Dmul", time_it([&] { gemm_nt(b, 0); }));
+    TNArgs t;
+    t.A = C; t.lda = N; t.B = A; t.ldb = K; t.K1 = K; t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K;
+    t.slab_b = slab_b; t.P = M; t.N = N; t.K = K;
+    const int sp = tn_splits(M, N, K);
+    report("tn (dW) 1 stage", time_it([&] { gemm_tn(t, sp, 0, 0); }));
+    report("tn (dW) 2 stages", time_it([&] { gemm_tn(t, sp, 0, 1); }));
+    for (int v = 0; v < 4; ++v) {
+        NTArgs bb = b;
+        char nm[64];
+        snprintf(nm, 64, "nt bwd Dmul variant %d", v);
+        report(nm, time_it([&] { gemm_nt(bb, 0, v); }));
+    }
+    printf("tn splits=%d\n", sp);
+    return 0;
+}
