@@ -242,6 +242,24 @@ def unit_composite(ref_spnerf):
     print("unit_composite written")
 
 
+def init_weights(ref_spnerf):
+    """SPNeRF(...) built after torch.manual_seed(7): the reference's own initialisation, for the
+    seeded-init equivalence test of the drop-in module (stored as per-parameter sums and
+    projections, not the weights)."""
+    out = {}
+    for tag, kw in (("w64_sem_beta", dict(num_sem_classes=3, feat=64, mapping=True, sem=True, beta=True,
+                                          t_embedding_dims=4)),
+                    ("w512", dict(feat=512, mapping=True))):
+        torch.manual_seed(7)
+        m = ref_spnerf.SPNeRF(**kw)
+        Q = param_projections([(n, tuple(p.shape)) for n, p in m.named_parameters()])
+        for n, p in m.named_parameters():
+            out[f"{tag}|{n}|sum"] = np.array(p.detach().double().sum().item())
+            out[f"{tag}|{n}|proj"] = np.array((p.detach().double() * torch.tensor(Q[n]).double()).sum().item())
+    np.savez_compressed(os.path.join(HERE, "init_seed7.npz"), **out)
+    print("init_seed7 written")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -268,6 +286,7 @@ def main():
              make_args(n_samples=32), 40, "test", full_grads=True, seed=6)
     unit_sampling(ref_rendering)
     unit_composite(ref_spnerf)
+    init_weights(ref_spnerf)
 
 
 if __name__ == "__main__":

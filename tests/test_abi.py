@@ -97,3 +97,23 @@ def test_workspace_sizes_scale_with_points():
     b = L.spnerf_mlp_workspace_bytes(ctypes.byref(c), 2048, 64, _lib.SPNERF_MLP_SAVE)
     n = L.spnerf_mlp_workspace_bytes(ctypes.byref(c), 1024, 64, 0)
     assert 0 < n < a < b
+
+
+def test_seeded_init_matches_reference():
+    """torch.manual_seed(7); SPNeRF(...) gives the reference's initial weights (fixture made by
+    running the reference's constructor, tests/golden/gen_golden.py::init_weights)."""
+    import numpy as np
+    import torch
+    import golden_util as gu
+    with np.load(f"{gu.GOLDEN}/init_seed7.npz") as z:
+        ref = {k: float(z[k]) for k in z.files}
+    for tag, kw in (("w64_sem_beta", dict(num_sem_classes=3, feat=64, mapping=True, sem=True, beta=True,
+                                          t_embedding_dims=4)),
+                    ("w512", dict(feat=512, mapping=True))):
+        torch.manual_seed(7)
+        m = spnerf_amd.SPNeRF(**kw)
+        Q = gu.param_projections([(n, tuple(p.shape)) for n, p in m.named_parameters()])
+        for n, p in m.named_parameters():
+            assert abs(p.detach().double().sum().item() - ref[f"{tag}|{n}|sum"]) <= 1e-9 * max(1.0, abs(ref[f"{tag}|{n}|sum"])), n
+            proj = (p.detach().double() * torch.tensor(Q[n]).double()).sum().item()
+            assert abs(proj - ref[f"{tag}|{n}|proj"]) <= 1e-9 * max(1.0, abs(ref[f"{tag}|{n}|proj"])), n

@@ -1,0 +1,116 @@
+"""Data-parallel path on CPU (gloo, world_size 2): shared-seed sampling, one flat gradient
+all-reduce, loss decomposition.  The per-rank compute is the oracle (CPU); the DP logic under
+test is sp-nerf_amd/dp.py, the same code bench.py runs over RCCL."""
+import os
+import socket
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ref_cpu
+from oracle.weights import ModelDims, make_weights
+from spnerf_amd import dp
+
+DIMS = ModelDims(width=64)
+ARGS = types.SimpleNamespace(n_samples=16, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                             sc_lambda=0.05, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)
+N_RAYS, GB = 96, 32
+
+
+def _scene():
+    rng = np.random.default_rng(0)
+    rays = np.zeros((N_RAYS, 11), np.float32)
+    rays[:, 0:3] = rng.uniform(-0.5, 0.5, (N_RAYS, 3))
+    d = rng.normal(size=(N_RAYS, 3)) + np.array([0, 0, -3.0])
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 7] = 0.2
+    rays[:, 9] = 1.0
+    rgbs = rng.uniform(0, 1, (N_RAYS, 3)).astype(np.float32)
+    u = rng.uniform(size=(N_RAYS, ARGS.n_samples)).astype(np.float32)
+    return torch.tensor(rays), torch.tensor(rgbs), torch.tensor(u)
+
+
+def _step_grads(idx, world):
+    """oracle render + the reference colour/solar losses on rays idx → flat gradient."""
+    rays, rgbs, u = _scene()
+    p = ref_cpu.to_params(make_weights(DIMS, 0), requires_grad=True)
+    queue = [("rand", u[idx]), ("randn", torch.zeros(len(idx), ARGS.n_samples)),
+             ("randn", torch.zeros(len(idx), ARGS.n_samples))]
+    draw = lambda kind, shape: queue.pop(0)[1]
+    res = ref_cpu.render_rays(p, DIMS, ARGS, rays[idx], draw=draw)
+    sun_sc = res["sun_sc_coarse"].squeeze()
+    loss = torch.mean((res["rgb_coarse"] - rgbs[idx]) ** 2)
+    loss = loss + 0.05 / 3 * torch.mean(torch.sum((res["transparency_sc_coarse"].detach() - sun_sc) ** 2, -1))
+    loss.backward()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    r, _, w = dp.init_from_env("gloo")
+    sampler = dp.SharedSeedSampler(N_RAYS, GB, r, w, seed=3)
+    gidx, idx = sampler.next()
+    p = _step_grads(idx, w)
+    params = list(p.values())
+    dp.allreduce_grads(params, w)
+    flat = torch.cat([t.grad.reshape(-1) for t in params])
+    gathered = [torch.empty_like(gidx) for _ in range(w)]
+    dist.all_gather(gathered, gidx)
+    out[rank] = (flat.numpy(), gidx.numpy(), torch.stack(gathered).numpy())
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_dp_two_ranks_gradient_equals_single_process():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    g0, gidx0, all0 = out[0]
+    g1, gidx1, _ = out[1]
+    # every rank drew the same global batch (no collective needed to agree on it)
+    assert np.array_equal(gidx0, gidx1)
+    assert np.array_equal(all0[0], all0[1])
+    # after the all-reduce both ranks hold the same gradient ...
+    np.testing.assert_allclose(g0, g1, rtol=0, atol=0)
+    # ... equal to the single-process gradient of the concatenated batch (mean losses decompose)
+    p = _step_grads(torch.tensor(gidx0), 1)
+    ref = torch.cat([t.grad.reshape(-1) for t in p.values()]).numpy()
+    np.testing.assert_allclose(g0, ref, rtol=2e-4, atol=1e-7 * np.abs(ref).max())
+
+
+def test_shared_seed_sampler_partitions_each_global_batch():
+    s = [dp.SharedSeedSampler(100, 20, r, 4, seed=1) for r in range(4)]
+    for _ in range(12):   # crosses epoch boundaries
+        parts = [x.next() for x in s]
+        g = parts[0][0]
+        assert all(torch.equal(p[0], g) for p in parts)
+        assert torch.equal(torch.cat([p[1] for p in parts]), g)
+        assert len(set(g.tolist())) == 20
+
+
+def test_cross_entropy_rescale_recovers_global_mean():
+    torch.manual_seed(0)
+    logits = torch.randn(40, 3)
+    labels = torch.randint(0, 3, (40,))
+    labels[::5] = -100
+    ce = torch.nn.CrossEntropyLoss(ignore_index=-100)
+    glob = ce(logits, labels)
+    parts = []
+    for r in range(4):
+        sl = slice(10 * r, 10 * r + 10)
+        parts.append(dp.ce_scale(labels[sl], labels, 4) * ce(logits[sl], labels[sl]))
+    np.testing.assert_allclose(float(sum(parts) / 4), float(glob), rtol=1e-6)
