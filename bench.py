@@ -40,10 +40,10 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 
 HBM_PEAK_GBS = 8000.0
 
 CONFIGS = {
-    "c2": dict(workload="C2: JAX_214-shape synthetic RPC-like rays, img_downscale=4, 1024 rays x 64 samples, "
-                        "coarse-only, W=512, PE on, fp32", img_downscale=4.0, batch=1024, n_samples=64, sem=False,
+    "c2": dict(workload="C2: JAX_214-shape scene (3 JAX_269 RPC cameras, GPU-generated rays), img_downscale=4, "
+                        "1024 rays x 64 samples, coarse-only, W=512, PE on, fp32", img_downscale=4.0, batch=1024, n_samples=64, sem=False,
                guided=False, sc_lambda=0.0, depth=False),
-    "c3": dict(workload="C3 flags (README recipe) at fp32: JAX_214-shape synthetic rays, img_downscale=1, 1024 rays x "
+    "c3": dict(workload="C3 flags (README recipe) at fp32: JAX_214-shape scene (3 JAX_269 RPC cameras), img_downscale=1, 1024 rays x "
                         "(64 + 64 guided) samples, solar pass, depth + semantic (C=3) heads, W=512",
                img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True),
 }
@@ -67,7 +67,7 @@ def cpu_baseline(c, seconds: float):
     dims = ModelDims(width=512, sem=c["sem"])
     p = ref_cpu.to_params(make_weights(dims, 0), requires_grad=True)
     opt = torch.optim.Adam(list(p.values()), lr=5e-4)
-    scene = synthetic_scene(c["img_downscale"], seed=1)
+    scene = synthetic_scene(c["img_downscale"], seed=1, device="cuda").to("cpu")
     args = make_args(c)
     B = 256
     g = torch.Generator().manual_seed(0)
@@ -110,8 +110,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     c = CONFIGS[a.config]
-    scene = synthetic_scene(c["img_downscale"], seed=0)
-    R = {k: getattr(scene, k).to(dev) for k in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")}
+    scene = synthetic_scene(c["img_downscale"], seed=0, device=dev)
+    R = {k: getattr(scene, k) for k in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")}
     torch.manual_seed(0)
     model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"]).to(dev)
     params = list(model.parameters())
@@ -194,7 +194,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (JAX_214-shape RPC-like rays resident in HBM, seeded-random SPNeRF init)",
+        "data": "synthetic targets on real JAX_269 RPC camera rays (JAX_214 proxy, resident in HBM), seeded-random SPNeRF init",
         "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": s_final,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": "gemm_nt_f32 (k_gemm_nt)", "achieved": achieved,

@@ -119,6 +119,18 @@ int32_t spnerf_sample_3sigma(int64_t n_rays, int32_t n, const float* low, const 
 /* row-wise ascending sort of (n_rays, n) floats, n <= 256 (torch.sort(-1) values) */
 int32_t spnerf_sort_rows(int64_t n_rays, int32_t n, const float* in, float* out, void* stream);
 
+/* ---- RPC camera rays: get_rays + normalize_rays + get_sun_dirs (datasets/satellite_scene.py:21-68,
+ *      :415-425, :449-473; modules/utils.py:59-100).  rpc = 90 host doubles: row/col/lat/lon/alt
+ *      offsets, then row/col/lat/lon/alt scales, then row_num, row_den, col_num, col_den (20 each,
+ *      RPC00B order); rescaled for `downscale` like utils.rescale_rpc(rpc, 1/downscale).  Pixels:
+ *      the rectangle [row0, row0+n_rows) x [col0, col0+n_cols) in row-major order, or the device
+ *      list `pixels` of (col, row) int32 pairs.  center (3 host floats) == NULL skips the fp32
+ *      normalisation; sun = 3 host floats (needed when ray_stride >= 11). */
+int32_t spnerf_rpc_rays(const double* rpc, double downscale, double min_alt, double max_alt, int32_t row0,
+                        int32_t col0, int32_t n_rows, int32_t n_cols, const int32_t* pixels, int64_t n_pixels,
+                        const float* center, float range, const float* sun, float* rays, int32_t ray_stride,
+                        void* stream);
+
 /* ---- in-library kernel timing (HIP events on the launch stream) ------------------------- */
 int32_t spnerf_prof_enable(int32_t on);
 int32_t spnerf_prof_reset(void);

@@ -53,6 +53,9 @@ SIGNATURES = {
     "spnerf_sample_pdf": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_void_p, c_void_p]),
     "spnerf_sample_3sigma": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "spnerf_sort_rows": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
+    "spnerf_rpc_rays": (c_int32, [POINTER(c_double), c_double, c_double, c_double, c_int32, c_int32, c_int32, c_int32,
+                                  c_void_p, c_int64, POINTER(c_float), c_float, POINTER(c_float), c_void_p, c_int32,
+                                  c_void_p]),
     "spnerf_prof_enable": (c_int32, [c_int32]),
     "spnerf_prof_reset": (c_int32, []),
     "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),

@@ -1,34 +1,32 @@
-"""Synthetic satellite scene of the JAX_214 shape (benchmark / smoke data).
+"""Benchmark scene of the JAX_214 shape.
 
-JAX_214 imagery is not shipped with the reference (only DFC2019_269 is), so the benchmark
-uses synthetic rays with the layout of ``SatelliteSceneDataset`` (datasets/satellite_scene.py
-:167-221): per view, one ray per pixel in row-major order, ``[o(3), d(3), near, far, sun(3)]``
-in the normalised ECEF frame (``scene.loc`` range 141.21875), near = 0 and far = altitude span
-/ cos(off-nadir).  Each view is an off-nadir pushbroom-like affine camera over the unit AOI
-(3 train views, README's ``JAX_214_3_imgs``; 813×793 px like JAX_269_006 at ds=1).  Targets:
-a smooth synthetic albedo field; depth priors (valid ~68 %, as JAX_269's 2D-point coverage
-438,256 / 644,709) and semantic labels {0,1,2,-100} for the config-3 flags.
+JAX_214 imagery is not shipped with the reference (only DFC2019_269 is), so, as SURVEY §8d
+prescribes, the JAX_269 RPC cameras stand in for it: three views (README's
+``JAX_214_3_imgs``: JAX_269_006 / 007 / 011), rays generated on the GPU by the RPC ray
+generator (satellite.image_rays: get_rays + normalize_rays + get_sun_dirs of
+datasets/satellite_scene.py) at the requested ``img_downscale``, in the dataset's order
+(images concatenated, pixels row-major; satellite_scene.py:186-221).  The JSONs carry
+sun_elevation = sun_azimuth = 0, hence sun_d = (0, 1, 0).
+
+Targets are synthetic (no GeoTIFF I/O on the GPU box): a smooth albedo field of the ray's
+ground point; depth priors valid on ~68 % of the rays (JAX_269's 2D-point coverage
+438,256 / 644,709) with GT depth far·U(0.3, 0.7) and std (1-corr)·0.05+1e-4; semantic labels
+{0, 1, 2, -100} with fixed frequencies.
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 
-import numpy as np
 import torch
 
-RANGE = 141.21875          # max(X,Y,Z)_scale of JAX_269 scene.loc
-ALT_SPAN_M = 28.0          # max_alt - min_alt of the JAX JSONs (-2 .. -30 m)
-# local frame at Jacksonville (lat 30.3, lon -81.7) in ECEF
-_LAT, _LON = math.radians(30.3), math.radians(-81.7)
-UP = np.array([math.cos(_LAT) * math.cos(_LON), math.cos(_LAT) * math.sin(_LON), math.sin(_LAT)])
-EAST = np.array([-math.sin(_LON), math.cos(_LON), 0.0])
-NORTH = np.cross(UP, EAST)
+from .satellite import image_rays, load_cameras
+
+VIEWS = ("JAX_269_006_RGB", "JAX_269_007_RGB", "JAX_269_011_RGB")
 
 
 @dataclass
 class Scene:
-    rays: torch.Tensor        # (N, 11) float32
+    rays: torch.Tensor        # (N, 11) float32 [o(3), d(3), near, far, sun(3)]
     rgbs: torch.Tensor        # (N, 3)
     depths: torch.Tensor      # (N, 2) [depth, correlation]
     valid_depth: torch.Tensor  # (N,) int64
@@ -36,46 +34,31 @@ class Scene:
     sems: torch.Tensor        # (N,) int64 in {0, 1, 2, -100}
     view_sizes: list
 
-
-def sun_direction(elev_deg: float, azim_deg: float) -> np.ndarray:
-    """get_sun_dirs (satellite_scene.py:449-473) for one image, in the local frame."""
-    el, az = math.radians(elev_deg), math.radians(azim_deg)
-    return np.array([math.sin(az) * math.cos(el), math.cos(az) * math.cos(el), math.sin(el)])
+    def to(self, device):
+        return Scene(*(getattr(self, f).to(device) for f in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")),
+                     self.view_sizes)
 
 
-def synthetic_scene(img_downscale: float = 4.0, n_views: int = 3, height: int = 813, width: int = 793,
-                    seed: int = 0) -> Scene:
-    rng = np.random.default_rng(seed)
-    h, w = int(height // img_downscale), int(width // img_downscale)
-    views = [(8.0, 30.0), (17.0, 160.0), (26.0, 280.0)][:n_views]
-    rays, rgbs, sizes = [], [], []
-    for vi, (theta_deg, phi_deg) in enumerate(views):
-        th, ph = math.radians(theta_deg), math.radians(phi_deg)
-        d = -math.cos(th) * UP + math.sin(th) * (math.cos(ph) * EAST + math.sin(ph) * NORTH)
-        d = d / np.linalg.norm(d)
-        r, c = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")          # row-major pixels
-        ge = (c.reshape(-1) + 0.5) / w * 1.6 - 0.8
-        gn = 0.8 - (r.reshape(-1) + 0.5) / h * 1.6
-        far = (ALT_SPAN_M / RANGE) / math.cos(th)
-        top = -2.0 / RANGE
-        o = ge[:, None] * EAST + gn[:, None] * NORTH + top * UP - d * 0.0
-        sun = sun_direction(60.0, 140.0)
-        sun_ecef = sun[0] * EAST + sun[1] * NORTH + sun[2] * UP
-        v = np.zeros((h * w, 11), np.float64)
-        v[:, 0:3], v[:, 3:6], v[:, 7], v[:, 8:11] = o, d, far, sun_ecef
-        rays.append(v.astype(np.float32))
-        # smooth albedo field of the ground point hit at mid depth
-        gx, gy = ge + 0.5 * far * d @ EAST, gn + 0.5 * far * d @ NORTH
-        col = np.stack([0.45 + 0.3 * np.sin(7 * gx + 1.3 * vi), 0.5 + 0.25 * np.cos(5 * gy), 0.4 + 0.2 * np.sin(3 * (gx + gy))], 1)
-        rgbs.append(np.clip(col, 0, 1).astype(np.float32))
-        sizes.append((h, w))
-    rays = np.concatenate(rays)
-    rgbs = np.concatenate(rgbs)
+def synthetic_scene(img_downscale: float = 4.0, views=VIEWS, seed: int = 0, device="cuda") -> Scene:
+    cams = load_cameras()
+    rays, sizes = [], []
+    for v in views:
+        meta = cams["images"][v]
+        rays.append(image_rays(meta, img_downscale, cams["scene_loc"], device=device))
+        sizes.append((int(meta["height"] // img_downscale), int(meta["width"] // img_downscale)))
+    rays = torch.cat(rays)
     n = rays.shape[0]
-    valid = (rng.uniform(size=n) < 438256 / 644709).astype(np.int64)
-    gt = (rays[:, 7] * rng.uniform(0.3, 0.7, size=n)).astype(np.float32)
-    corr = rng.uniform(0.2, 1.0, size=n).astype(np.float32)
-    std = ((1.0 - corr) * 0.05 + 1e-4).astype(np.float32)
-    sems = rng.choice([0, 1, 2, -100], size=n, p=[0.45, 0.3, 0.15, 0.1]).astype(np.int64)
-    return Scene(torch.tensor(rays), torch.tensor(rgbs), torch.tensor(np.stack([gt, corr], 1)), torch.tensor(valid),
-                 torch.tensor(std), torch.tensor(sems), sizes)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    mid = rays[:, 0:3] + 0.5 * rays[:, 7:8] * rays[:, 3:6]
+    gx, gy = mid[:, 0] + mid[:, 2], mid[:, 1]
+    rgbs = torch.stack([0.45 + 0.3 * torch.sin(9 * gx), 0.5 + 0.25 * torch.cos(7 * gy), 0.4 + 0.2 * torch.sin(5 * (gx + gy))],
+                       1).clamp(0, 1)
+    valid = (torch.rand(n, generator=g) < 438256 / 644709).long()
+    gt = rays[:, 7].cpu() * (0.3 + 0.4 * torch.rand(n, generator=g))
+    corr = 0.2 + 0.8 * torch.rand(n, generator=g)
+    std = (1.0 - corr) * 0.05 + 1e-4
+    sems = torch.multinomial(torch.tensor([0.45, 0.3, 0.15, 0.1]), n, replacement=True, generator=g)
+    sems = torch.where(sems == 3, torch.full_like(sems, -100), sems)
+    dev = rays.device
+    return Scene(rays, rgbs.float(), torch.stack([gt, corr], 1).float().to(dev), valid.to(dev), std.float().to(dev),
+                 sems.to(dev), sizes)

@@ -260,6 +260,64 @@ def init_weights(ref_spnerf):
     print("init_seed7 written")
 
 
+def rpc_rays(ref: str):
+    """Rays of JAX_269 views through the reference's own datasets/satellite_scene.py get_rays
+    (:21-68, with modules/utils.py geodetic_to_ecef :80-100), normalize_rays (:415-425) and
+    get_sun_dirs (:449-473).  Its I/O-only imports (rasterio, rpcm, torchvision, cv2, …) are
+    replaced by MagicMock modules; the rpcm localization it calls is the numpy restatement
+    oracle/rpc_ref.RPC (rpcm itself is unavailable offline and unpinned — SURVEY §8c)."""
+    import json
+    import types
+    from unittest import mock
+    from oracle.rpc_ref import RPC
+    stubs = ["rasterio", "rpcm", "torchvision", "torchvision.transforms", "cv2", "pyproj", "utm", "osgeo", "gdal",
+             "plyflatten", "kornia", "kornia.losses", "srtm4", "numba", "lpips", "PIL", "PIL.Image"]
+    saved = {k: sys.modules.get(k) for k in stubs}
+    for k in stubs:
+        sys.modules[k] = mock.MagicMock()
+    try:
+        import datasets.satellite_scene as ss
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    jdir = os.path.join(ref, "Dataset", "DFC2019_269", "JSON")
+    loc = json.load(open(os.path.join(jdir, "scene.loc")))
+    center = torch.tensor([float(loc["X_offset"]), float(loc["Y_offset"]), float(loc["Z_offset"])])
+    rng = torch.max(torch.tensor([float(loc["X_scale"]), float(loc["Y_scale"]), float(loc["Z_scale"])]))
+    holder = types.SimpleNamespace(center=center, range=rng)
+    out = {"center": center.numpy(), "range": np.array(rng.item(), np.float32)}
+    for tag, img, ds, crop in (("006_crop", "JAX_269_006_RGB.json", 1.0, (400, 400, 16, 16)),
+                               ("007_ds8", "JAX_269_007_RGB.json", 8.0, None)):
+        d = json.load(open(os.path.join(jdir, img)))
+        h, w = int(d["height"] // ds), int(d["width"] // ds)
+        rpc = RPC(d["rpc"], ds)
+        cols, rows = np.meshgrid(np.arange(w), np.arange(h))
+        cols, rows = cols.flatten(), rows.flatten()
+        if crop:
+            r0, c0, ch, cw = crop
+            sel = (rows >= r0) & (rows < r0 + ch) & (cols >= c0) & (cols < c0 + cw)
+            cols, rows = cols[sel], rows[sel]
+        rays = ss.get_rays(cols, rows, rpc, float(d["min_alt"]), float(d["max_alt"]))
+        rays = ss.SatelliteSceneDataset.normalize_rays(holder, rays)
+        sun = ss.SatelliteSceneDataset.get_sun_dirs(holder, float(d["sun_elevation"]), float(d["sun_azimuth"]),
+                                                    rays.shape[0])
+        out[f"{tag}|rays"] = torch.hstack([rays, sun]).numpy()
+        out[f"{tag}|meta"] = np.array([h, w, ds, float(d["min_alt"]), float(d["max_alt"]),
+                                       *(crop if crop else (0, 0, h, w))], np.float64)
+        out[f"{tag}|rpc"] = np.array([d["rpc"][k] for k in ("row_offset", "col_offset", "lat_offset", "lon_offset",
+                                      "alt_offset", "row_scale", "col_scale", "lat_scale", "lon_scale", "alt_scale")]
+                                     + list(d["rpc"]["row_num"]) + list(d["rpc"]["row_den"])
+                                     + list(d["rpc"]["col_num"]) + list(d["rpc"]["col_den"]), np.float64)
+        out[f"{tag}|sun_deg"] = np.array([float(d["sun_elevation"]), float(d["sun_azimuth"])])
+    # a non-trivial sun direction through the reference formula as well
+    out["sun_60_140"] = ss.SatelliteSceneDataset.get_sun_dirs(holder, 60.0, 140.0, 2).numpy()
+    np.savez_compressed(os.path.join(HERE, "rpc_rays.npz"), **out)
+    print("rpc_rays written", {k: v.shape for k, v in out.items() if k.endswith("rays")})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -287,6 +345,7 @@ def main():
     unit_sampling(ref_rendering)
     unit_composite(ref_spnerf)
     init_weights(ref_spnerf)
+    rpc_rays(a.ref)
 
 
 if __name__ == "__main__":
