@@ -11,6 +11,7 @@ inference pass 1 :157            σ-only MLP + weights-only composite       mlp 
 GenerateGuidedSamples :92-116    ``spnerf_sample_guided`` (+ sort, merge)  k_guided
   + sort / merge :165-167
 inference pass 2 :169            full MLP + composite                      mlp + composite
+fine pass :186-216               sample_pdf + sort + fine MLP/composite    k_sample_pdf, k_sort_rows
 solar correction :171-177        σ+sun MLP + weights-only composite        mlp + composite
 sample_pdf :14-55                ``sample_pdf``                            k_sample_pdf
 sample_3sigma :58-73             ``sample_3sigma``                         k_sample_pdf (window)
@@ -156,5 +157,40 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
         result["sun_sc"] = sc["sun"]
     out = {f"{k}_coarse": v for k, v in result.items()}
     if args.n_importance > 0:
-        raise NotImplementedError("hierarchical fine model (n_importance > 0) is the next §8(f) row; not built yet")
+        out = _fine(models, args, rays, ts, z_vals, out, semantics, rays_t)
     return out
+
+
+def sort_rows(x: torch.Tensor) -> torch.Tensor:
+    """torch.sort(x, -1)[0] for rows of ≤ 256 values (k_sort_rows)."""
+    _lib.require_device(x)
+    x = x.contiguous().float()
+    out = torch.empty_like(x)
+    _lib.check(_lib.lib().spnerf_sort_rows(x.shape[0], x.shape[1], _lib.ptr(x), _lib.ptr(out), _lib.stream_of(x)),
+               "sort_rows")
+    return out
+
+
+def _fine(models, args, rays, ts, z_vals, result_, semantics, rays_t_coarse):
+    """Hierarchical fine pass, rendering.py:186-216, reproduced as the reference returns it:
+    with the solar pass on, ``result_`` is replaced by the fine solar inference's dictionary
+    (:207), so the coarse keys are dropped and un-suffixed fine-solar keys appear."""
+    n_imp = args.n_importance
+    with torch.no_grad():
+        mid = 0.5 * (z_vals[:, :-1] + z_vals[:, 1:])                               # :188
+        z_ = sample_pdf(mid, result_["weights_coarse"][:, 1:-1], n_imp, det=False)  # :189 (perturb = 1)
+        z_vals = sort_rows(torch.cat([z_vals, z_], -1))                             # :190
+    model = models["fine"]
+    rays_t = None
+    if args.beta:
+        rays_t = models['t'](ts) if ts else None                                    # :201, as written there
+    sem = semantics if model.sem else None
+    result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t)
+    if args.sc_lambda > 0:
+        result_ = inference_rays(model, args, rays, z_vals, 8, sem, rays_t)        # :207 overwrites result_
+        result["weights_sc"] = result_["weights"]
+        result["transparency_sc"] = result_["transparency"]
+        result["sun_sc"] = result_["sun"]
+    for k in list(result.keys()):
+        result_[f"{k}_fine"] = result[k]
+    return result_

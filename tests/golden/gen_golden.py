@@ -122,6 +122,8 @@ def run_case(ref_spnerf, ref_rendering, name: str, dims: ModelDims, args, n_rays
     torch.manual_seed(torch_seed)
     model = build_model(ref_spnerf, dims, seed)
     models = {"coarse": model}
+    if args.n_importance > 0:   # second network, weights from seed + 100
+        models["fine"] = build_model(ref_spnerf, dims, seed + 100)
     rays = torch.tensor(synthetic_rays(n_rays, seed=100 + seed))
     rng = np.random.default_rng(7 + seed)
     sem = ts = None
@@ -152,11 +154,13 @@ def run_case(ref_spnerf, ref_rendering, name: str, dims: ModelDims, args, n_rays
         extra.update(valid_depth=valid, target_depths=np.stack([gt, corr], 1), target_std=std)
     with Recorder() as rec:
         res = ref_rendering.render_rays(models, args, rays, ts, semantics=sem, mode=mode, **kw)
-    outs = {k: v for k, v in res.items()}
+    outs = {k: v for k, v in res.items() if torch.is_tensor(v)}
     shapes = {k: tuple(v.shape) for k, v in outs.items() if v.requires_grad}
     R = projection_weights(shapes)
     loss = sum((outs[k] * torch.tensor(R[k])).sum() for k in sorted(R))
     params = list(model.named_parameters())
+    if "fine" in models:
+        params += [("fine." + n, p) for n, p in models["fine"].named_parameters()]
     if dims.beta:
         params += [("t.weight", models["t"].weight)]
     loss.backward()
@@ -168,8 +172,8 @@ def run_case(ref_spnerf, ref_rendering, name: str, dims: ModelDims, args, n_rays
     for k, v in outs.items():
         data["out_" + k] = v.detach().numpy()
     if full_grads:
-        for n, p in params:
-            data["grad_" + n] = p.grad.numpy()
+        for n, p in params:   # a parameter the outputs do not depend on has no .grad → zeros
+            data["grad_" + n] = p.grad.numpy() if p.grad is not None else np.zeros(tuple(p.shape), np.float32)
     else:
         Q = param_projections([(n, tuple(p.shape)) for n, p in params])
         for n, p in params:
@@ -339,6 +343,13 @@ def main():
     # beta head + time embedding, noise on
     run_case(ref_spnerf, ref_rendering, "beta_w64", ModelDims(width=64, sem=True, beta=True),
              make_args(beta=True, sc_lambda=0.05, noise_std=0.5), 32, "train", full_grads=True, seed=5)
+    # hierarchical fine model (rendering.py:186-216): plain, and with the solar pass (which in the
+    # reference replaces the coarse dictionary by the fine solar inference's, :207)
+    run_case(ref_spnerf, ref_rendering, "fine_w64", ModelDims(width=64, sem=True), make_args(n_importance=32),
+             32, "test", full_grads=True, seed=7)
+    run_case(ref_spnerf, ref_rendering, "fine_sc_guided_w64", ModelDims(width=64),
+             make_args(n_importance=48, sc_lambda=0.1, guidedsample=True), 24, "train", full_grads=True, seed=8,
+             with_depth=True)
     # no positional encoding (mapping off), n_samples=32
     run_case(ref_spnerf, ref_rendering, "nomap_w64", ModelDims(width=64, mapping=False),
              make_args(n_samples=32), 40, "test", full_grads=True, seed=6)

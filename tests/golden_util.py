@@ -9,7 +9,8 @@ import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
-CASES = ["c1_w512", "c1_w64", "c3_w64", "c3_w512", "c3_test_w64", "beta_w64", "nomap_w64"]
+CASES = ["c1_w512", "c1_w64", "c3_w64", "c3_w512", "c3_test_w64", "beta_w64", "nomap_w64", "fine_w64",
+         "fine_sc_guided_w64"]
 
 
 def load(name: str) -> dict:

@@ -14,6 +14,7 @@ def run_oracle(name):
     meta = data["meta"]
     dims, args = gu.dims_of(meta), gu.args_of(meta)
     p = ref_cpu.to_params(make_weights(dims, meta["seed"]), requires_grad=True)
+    pf = ref_cpu.to_params(make_weights(dims, meta["seed"] + 100), requires_grad=True) if args.n_importance else None
     replay = gu.Replay(gu.draws_of(data), torch.tensor)
     rays = torch.tensor(data["rays"])
     sem = torch.tensor(data["in_semantics"]) if "in_semantics" in data else None
@@ -24,8 +25,10 @@ def run_oracle(name):
         kw = dict(valid_depth=torch.tensor(data["in_valid_depth"]), target_depths=torch.tensor(data["in_target_depths"]),
                   target_std=torch.tensor(data["in_target_std"]))
     res = ref_cpu.render_rays(p, dims, args, rays, ts, sem, meta["mode"], t_embed=(lambda t: emb_t[t]) if emb_t is not None else None,
-                              draw=replay, **kw)
+                              draw=replay, fine_params=pf, **kw)
     assert replay.used == len(replay.draws)
+    if pf is not None:
+        p = dict(p, **{"fine." + k: v for k, v in pf.items()})
     return data, p, emb_t, res
 
 
@@ -51,7 +54,8 @@ def test_oracle_grads_match_reference(name):
         params["t.weight"] = emb_t
     if any(k.startswith("grad_") for k in data):
         for n, t in params.items():
-            gu.assert_close("grad " + n, t.grad.numpy(), data["grad_" + n], rtol=1e-4, atol_frac=1e-5)
+            g = t.grad.numpy() if t.grad is not None else np.zeros(tuple(t.shape), np.float32)
+            gu.assert_close("grad " + n, g, data["grad_" + n], rtol=1e-4, atol_frac=1e-5)
     else:
         Q = gu.param_projections([(n, tuple(t.shape)) for n, t in params.items()])
         for n, t in params.items():
