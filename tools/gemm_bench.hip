@@ -2,6 +2,8 @@
 //   make -C tools gemm_bench && ./tools/gemm_bench
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -45,7 +47,7 @@ static double time_it(F f, int iters = 20) {
 }
 
 int main(int argc, char** argv) {
-    const int M = argc > 1 ? atoi(argv[1]) : 65536, N = 512, K = 512;
+    const int M = argc > 1 ? atoi(argv[1]) : 65536, N = 512, K = argc > 2 ? atoi(argv[2]) : 512;
     float* A = rnd((size_t)M * K, 1.f, 1);
     float* B = rnd((size_t)N * K, 0.1f, 2);
     float* bias = rnd(N, 0.1f, 3);
@@ -59,6 +61,28 @@ int main(int argc, char** argv) {
 
     NTArgs g;
     g.A = A; g.lda = K; g.K1 = K; g.B = B; g.ldb = K; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K;
+    // correctness cross-check of every variant against variant 0 (fwd epilogue incl. Dout)
+    {
+        std::vector<float> ref((size_t)M * N), got((size_t)M * N), refD((size_t)M * N), gotD((size_t)M * N);
+        NTArgs f = g;
+        f.bias = bias; f.act = 1; f.w0 = 1.f; f.Dout = D; f.ld_dout = N;
+        gemm_nt(f, 0, 0);
+        CK(hipMemcpy(ref.data(), C, ref.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(refD.data(), D, ref.size() * 4, hipMemcpyDeviceToHost));
+        for (int v = 1; v < 4; ++v) {
+            CK(hipMemset(C, 0, ref.size() * 4));
+            CK(hipMemset(D, 0, ref.size() * 4));
+            gemm_nt(f, 0, v);
+            CK(hipMemcpy(got.data(), C, ref.size() * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(gotD.data(), D, ref.size() * 4, hipMemcpyDeviceToHost));
+            double md = 0, mdd = 0;
+            for (size_t i = 0; i < ref.size(); ++i) {
+                md = std::max(md, (double)std::fabs(ref[i] - got[i]));
+                mdd = std::max(mdd, (double)std::fabs(refD[i] - gotD[i]));
+            }
+            printf("variant %d max|diff| vs variant 0: C %.3g D %.3g\n", v, md, mdd);
+        }
+    }
     for (int v = 0; v < 4; ++v) {
         char nm[64];
         snprintf(nm, 64, "nt plain variant %d", v);
