@@ -37,15 +37,24 @@ from spnerf_amd.losses import DepthLoss, SemanticLoss, SNerfLoss  # noqa: E402
 from spnerf_amd.scene import synthetic_scene  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec
+BF16_MFMA_PEAK_TFLOPS = 2516.6    # dense bf16 = 16 x the f32 MFMA rate (MI355X_MICROARCH.md "Peak BF16", ~2.5 PF)
 HBM_PEAK_GBS = 8000.0
+GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt (fp32 MFMA)", FP32_MFMA_PEAK_TFLOPS),
+                "gemm_tn_f32": ("k_gemm_tn (fp32 MFMA, weight gradients)", FP32_MFMA_PEAK_TFLOPS),
+                "gemm_nt_bf16": ("k_gemm_nt_bf16 (bf16 MFMA)", BF16_MFMA_PEAK_TFLOPS),
+                "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA, weight gradients)", BF16_MFMA_PEAK_TFLOPS)}
 
 CONFIGS = {
     "c2": dict(workload="C2: JAX_214-shape scene (3 JAX_269 RPC cameras, GPU-generated rays), img_downscale=4, "
                         "1024 rays x 64 samples, coarse-only, W=512, PE on, fp32", img_downscale=4.0, batch=1024, n_samples=64, sem=False,
-               guided=False, sc_lambda=0.0, depth=False),
-    "c3": dict(workload="C3 flags (README recipe) at fp32: JAX_214-shape scene (3 JAX_269 RPC cameras), img_downscale=1, 1024 rays x "
-                        "(64 + 64 guided) samples, solar pass, depth + semantic (C=3) heads, W=512",
-               img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True),
+               guided=False, sc_lambda=0.0, depth=False, precision="fp32"),
+    "c3": dict(workload="C3: JAX_214-shape scene (3 JAX_269 RPC cameras), img_downscale=1, 1024 rays x (64 + 64 guided) "
+                        "samples, solar pass, depth + semantic (C=3) heads, W=512, bf16 MLP (fp32 accumulate / params)",
+               img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True,
+               precision="bf16"),
+    "c3_fp32": dict(workload="C3 flags at fp32 (parity arithmetic): as c3 with the fp32 MLP",
+                    img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True,
+                    precision="fp32"),
 }
 
 
@@ -96,6 +105,22 @@ def cpu_baseline(c, seconds: float):
             "sample": f"{n} train steps of {B} rays x {s_final} samples (oracle/ref_cpu.py, torch CPU, {threads} threads)"}
 
 
+def gemm_totals(steps):
+    """All MFMA GEMM launches of the timed steps: counted FLOP / summed kernel time, against the
+    peak of each launch's dtype (time-weighted) — the MLP's MFMA utilisation."""
+    flop = ms = peak_ms = 0.0
+    for k, (_, peak) in GEMM_CLASSES.items():
+        r = _lib.prof_read(k)
+        flop += r["flop"]
+        ms += r["ms"]
+        peak_ms += peak * r["ms"]
+    if ms == 0:
+        return None
+    tf = flop / (ms * 1e-3) / 1e12
+    peak = peak_ms / ms
+    return {"tflops": tf, "peak": peak, "frac": tf / peak, "ms_per_step": ms / steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -113,7 +138,8 @@ def main():
     scene = synthetic_scene(c["img_downscale"], seed=0, device=dev)
     R = {k: getattr(scene, k) for k in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")}
     torch.manual_seed(0)
-    model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"]).to(dev)
+    model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"],
+                              precision=c["precision"]).to(dev)
     params = list(model.parameters())
     try:
         opt = torch.optim.Adam(params, lr=5e-4, fused=True)
@@ -171,15 +197,18 @@ def main():
     elapsed = float(elapsed.item())
 
     kernels = {}
-    for k in ("gemm_nt_f32", "gemm_tn_f32", "encode", "heads_fwd", "heads_bwd", "composite_fwd", "composite_bwd",
-              "sample_guided"):
+    for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "tn_skinny", "encode", "heads_fwd",
+              "heads_bwd", "composite_fwd", "composite_bwd", "sample_guided"):
         s = _lib.prof_read(k)
         if s["launches"]:
             kernels[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / a.steps,
                           "avg_us": 1e3 * s["ms"] / s["launches"],
                           "tflops": s["flop"] / (s["ms"] * 1e-3) / 1e12 if s["flop"] else None,
                           "gbs": s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["bytes"] else None}
-    nt = _lib.prof_read("gemm_nt_f32")
+    # dominant kernel = the GEMM class with the most time in the timed steps
+    dom = max(GEMM_CLASSES, key=lambda k: _lib.prof_read(k)["ms"])
+    nt = _lib.prof_read(dom)
+    dom_name, peak = GEMM_CLASSES[dom]
     achieved = nt["flop"] / (nt["ms"] * 1e-3) / 1e12 if nt["ms"] else 0.0
     total = world * B * s_final * a.steps
     out = {
@@ -193,13 +222,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": c["precision"],
         "data": "synthetic targets on real JAX_269 RPC camera rays (JAX_214 proxy, resident in HBM), seeded-random SPNeRF init",
         "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": s_final,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_nt_f32 (k_gemm_nt)", "achieved": achieved,
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+        "roofline": {"bound": "mfma", "kernel": f"{dom} ({dom_name})", "achieved": achieved,
+                     "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": None, "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
+        "mlp_gemms": gemm_totals(a.steps),
         "kernels": kernels,
         "final_loss": float(loss.item()),
     }

@@ -25,5 +25,6 @@ def load_model(args):
     if args.model == "sp-nerf":
         return SPNeRF(num_sem_classes=args.num_sem_classes, s_embedding_factor=args.s_embedding_factor,
                       layers=args.fc_layers, feat=args.fc_units, mapping=args.mapping,
-                      t_embedding_dims=args.t_embbeding_tau, beta=args.beta, sem=args.sem)
+                      t_embedding_dims=args.t_embbeding_tau, beta=args.beta, sem=args.sem,
+                      precision=getattr(args, "mlp_precision", "fp32"))
     raise ValueError(f'model {args.model} is not valid')

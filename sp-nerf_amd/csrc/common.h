@@ -48,7 +48,27 @@ struct ProfScope {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+typedef __bf16 bf16;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// 4 consecutive activations as fp32 (the MLP keeps activations in fp32 or bf16, cfg.dtype)
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 ld4(const bf16* p) {
+    const u32x2 v = *reinterpret_cast<const u32x2*>(p);
+    return f32x4{__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u), __uint_as_float(v[1] << 16),
+                 __uint_as_float(v[1] & 0xffff0000u)};
+}
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void st4(bf16* p, f32x4 v) {
+    const __bf16 a = (__bf16)v[0], b = (__bf16)v[1], c = (__bf16)v[2], d = (__bf16)v[3];
+    *reinterpret_cast<u32x2*>(p) =
+        u32x2{(uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16),
+              (uint32_t)__builtin_bit_cast(uint16_t, c) | ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16)};
+}
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16* p) { return (float)*p; }
 
 // Bijective XCD-aware remap of a 1-D grid: blocks b and b+8 share an XCD (round-robin
 // dispatch), so hand each XCD a contiguous run of tiles (cdna_hip_programming.md T1).

@@ -1,0 +1,43 @@
+// Launch descriptors of the bf16 MFMA GEMMs (gemm_bf16.hip), the cfg.dtype = 1 path.
+#pragma once
+#include "common.h"
+
+namespace spn {
+
+typedef __bf16 bf16;
+
+// C[M,N] = epi(A[M,K] · B[N,K]^T), bf16 operands, fp32 accumulation, bf16 C.  A may be split
+// along K (columns [K1,K) from A2: the skip-layer input [h | x0]).  Epilogue (as NTArgs):
+// + bias[col] + rowbias[row/rows_per_ray][col] + r1_a[row]*r1_v[col]; act==1 and col>=n_lin:
+// y = sin(w0*v), D = w0*cos(w0*v) (else y = v, D = 1); y *= Dmul.
+struct NT16Args {
+    const bf16* A = nullptr; int lda = 0;
+    const bf16* A2 = nullptr; int lda2 = 0; int K1 = 0;
+    const bf16* B = nullptr; int ldb = 0;
+    bf16* C = nullptr; int ldc = 0;
+    int M = 0, N = 0, K = 0;
+    const float* bias = nullptr;
+    const float* rowbias = nullptr; int ld_rb = 0; int rows_per_ray = 1;
+    const float* r1_a = nullptr; int r1_lda = 0; const float* r1_v = nullptr;
+    int act = 0; float w0 = 1.f; int n_lin = 0;
+    bf16* Dout = nullptr; int ld_dout = 0;
+    const bf16* Dmul = nullptr; int ld_dmul = 0;
+};
+
+// slab[s][n][k] = Σ_{p in split s} A[p][n] · B[p][k] (B split along k at K1),
+// slab_b[s][n] = Σ_{p in split s} A[p][n]; reduced by reduce_slabs (gemm_f32.h).
+struct TN16Args {
+    const bf16* A = nullptr; int lda = 0;
+    const bf16* B = nullptr; int ldb = 0;
+    const bf16* B2 = nullptr; int ldb2 = 0; int K1 = 0;
+    float* slab = nullptr; int ld_slab = 0; int64_t slab_stride = 0;
+    float* slab_b = nullptr;
+    int P = 0, N = 0, K = 0;
+    int p_per_split = 0;  // set by gemm_tn_bf16
+};
+
+int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s);
+int tn_splits_bf16(int P, int N, int K);
+int32_t gemm_tn_bf16(const TN16Args& a, int splits, hipStream_t s);
+
+}  // namespace spn

@@ -20,6 +20,8 @@ struct NTArgs {
     int act = 0; float w0 = 1.f; int n_lin = 0;
     float* Dout = nullptr; int ld_dout = 0;
     const float* Dmul = nullptr; int ld_dmul = 0;
+    // bf16 outputs instead of C / Dout (sine epilogue only: layer 0 of the bf16 MLP), same ld
+    bf16* C16 = nullptr; bf16* D16 = nullptr;
 };
 
 // slab[s][n][k] = Σ_{p in split s} A[p][n] · B[p][k]  (B split along K at K1 like NTArgs.A);
@@ -39,6 +41,7 @@ struct TNArgs {
 struct SkinnyArgs {
     const float* A = nullptr; int lda = 0; int Ma = 0;
     const float* B = nullptr; int ldb = 0; int K = 0;
+    const bf16* B16 = nullptr;  // bf16 B rows instead of B (same ldb)
     int64_t P = 0; int chunk = 0; int ones = 0;
     float* slab = nullptr; float* slab_b = nullptr;
 };

@@ -17,9 +17,7 @@
 
 namespace spn {
 
-constexpr int BM = 128, BN = 128, BK = 32, LDK = BK + 4;
-
-__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+constexpr int BM = 128, BN = 128, BK = 32;
 
 // NT main loop variants: KS = K-step depth (32 or 64), ST = LDS stages (1: register prefetch,
 // two barriers per K-step; 2: double-buffered LDS, one barrier per K-step).
@@ -182,9 +180,14 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
                     y = sn;
                     dv = g.w0 * cs;
                 }
-                if (g.Dout) g.Dout[(int64_t)row * g.ld_dout + col] = dv;
                 if (g.Dmul) y *= g.Dmul[(int64_t)row * g.ld_dmul + col];
-                g.C[(int64_t)row * g.ldc + col] = y;
+                if (g.C16) {
+                    if (g.D16) g.D16[(int64_t)row * g.ld_dout + col] = (bf16)dv;
+                    g.C16[(int64_t)row * g.ldc + col] = (bf16)y;
+                } else {
+                    if (g.Dout) g.Dout[(int64_t)row * g.ld_dout + col] = dv;
+                    g.C[(int64_t)row * g.ldc + col] = y;
+                }
             }
         }
     }
@@ -337,8 +340,8 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(ReduceArgs g) {
 // (a_m(p) = A[p*lda + m], plus a_Ma(p) = 1 when `ones`, i.e. the column sums of B), and
 // slab_b[chunk][m] = Σ_{p in chunk} a_m(p).  Threads own float4 column groups; the rows of a
 // chunk are split over `rph` row phases whose partials are combined through LDS.
-template <int MA>
-__global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g) {
+template <int MA, typename TB>
+__global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __restrict__ Bm) {
     __shared__ float red[256 * 4];
     const int tid = threadIdx.x;
     const int kq = g.K >> 2;                      // float4 column groups (kq <= 256, checked on host)
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g) {
     for (int m = 0; m < MA; ++m) asum[m] = 0.f;
     if (live)
         for (int64_t p = p0 + ph; p < p1; p += rph) {
-            const f32x4 b = *reinterpret_cast<const f32x4*>(g.B + p * g.ldb + 4 * c4);
+            const f32x4 b = ld4(Bm + p * g.ldb + 4 * c4);
             const float* ar = g.A + p * g.lda;
 #pragma unroll
             for (int m = 0; m < MA; ++m)
@@ -408,6 +411,7 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     SPN_ARG(a.K1 == a.K || a.A2 != nullptr, "gemm_nt: second A segment missing");
     SPN_ARG(a.lda % 4 == 0 && a.ldb % 4 == 0 && (a.K1 == a.K || a.lda2 % 4 == 0), "gemm_nt: leading dims must be /4");
     SPN_ARG(a.rowbias == nullptr || a.rows_per_ray > 0, "gemm_nt: rows_per_ray");
+    SPN_ARG(a.C16 == nullptr || (a.act == 1 && a.n_lin == 0 && a.Dmul == nullptr), "gemm_nt: bf16 output needs the sine epilogue");
     if (a.M == 0) return SPNERF_OK;
     const int nb = cdiv(a.M, BM) * cdiv(a.N, BN);
     ProfScope prof("gemm_nt_f32", s, 2.0 * a.M * a.N * a.K, 4.0 * ((double)a.M * a.K + (double)a.N * a.K + 2.0 * a.M * a.N));
@@ -434,9 +438,15 @@ int32_t tn_skinny(const SkinnyArgs& a0, hipStream_t s) {
     const int nb = cdiv(a.P, a.chunk);
     if (nb == 0) return SPNERF_OK;
     ProfScope prof("tn_skinny", s, 2.0 * a.P * a.K * (a.Ma + a.ones), 4.0 * a.P * (a.K + a.Ma));
-    if (a.Ma <= 1) hipLaunchKernelGGL(k_tn_skinny<1>, dim3(nb), dim3(256), 0, s, a);
-    else if (a.Ma <= 3) hipLaunchKernelGGL(k_tn_skinny<3>, dim3(nb), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_tn_skinny<8>, dim3(nb), dim3(256), 0, s, a);
+    if (a.B16) {
+        if (a.Ma <= 1) hipLaunchKernelGGL((k_tn_skinny<1, bf16>), dim3(nb), dim3(256), 0, s, a, a.B16);
+        else if (a.Ma <= 3) hipLaunchKernelGGL((k_tn_skinny<3, bf16>), dim3(nb), dim3(256), 0, s, a, a.B16);
+        else hipLaunchKernelGGL((k_tn_skinny<8, bf16>), dim3(nb), dim3(256), 0, s, a, a.B16);
+    } else {
+        if (a.Ma <= 1) hipLaunchKernelGGL((k_tn_skinny<1, float>), dim3(nb), dim3(256), 0, s, a, a.B);
+        else if (a.Ma <= 3) hipLaunchKernelGGL((k_tn_skinny<3, float>), dim3(nb), dim3(256), 0, s, a, a.B);
+        else hipLaunchKernelGGL((k_tn_skinny<8, float>), dim3(nb), dim3(256), 0, s, a, a.B);
+    }
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

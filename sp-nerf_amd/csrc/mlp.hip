@@ -12,9 +12,11 @@
 //    Q = feat·[sun hidden 1; rgb hidden; beta hidden]^T;
 //  * N ≤ C-wide output heads (σ, rgb, sun, β, semantic logits) are per-point dot products.
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
+#include "gemm_bf16.h"
 #include "gemm_f32.h"
 #include "mlp_layout.h"
 
@@ -26,7 +28,7 @@ namespace spn {
 
 struct PackPiece {
     const float* src;
-    int src_ld, src_c0, rows, cols, dst_ld, transpose;
+    int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;  // bf: bf16 destination, dst in bf16 units
     int64_t dst;
 };
 constexpr int kMaxPieces = 24;
@@ -41,8 +43,9 @@ __global__ void k_pack(PackArgs a) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int r = (int)(i / pc.cols), c = (int)(i % pc.cols);
         const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
-        if (pc.transpose) a.packed[pc.dst + (int64_t)c * pc.dst_ld + r] = v;
-        else a.packed[pc.dst + (int64_t)r * pc.dst_ld + c] = v;
+        const int64_t o = pc.dst + (pc.transpose ? (int64_t)c * pc.dst_ld + r : (int64_t)r * pc.dst_ld + c);
+        if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)v;
+        else a.packed[o] = v;
     }
 }
 
@@ -50,7 +53,7 @@ __global__ void k_pack(PackArgs a) {
 // output element per thread.  o + dir*z is evaluated as two rounded ops like the reference
 // (no FMA contraction: sin(2^9 x) amplifies a 1-ulp difference in x by 512).
 __global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, const float* __restrict__ z, int S,
-                         int64_t P, int n_freq, int K0, int K0p, float* __restrict__ X0) {
+                         int64_t P, int n_freq, int K0, int K0p, float* __restrict__ X0, bf16* __restrict__ X0b) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= P * K0p) return;
     const int64_t p = i / K0p;
@@ -69,12 +72,13 @@ __global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, co
         }
     }
     X0[i] = v;
+    if (X0b) X0b[i] = (bf16)v;
 }
 
 struct RayFwdArgs {
     const float* rays; int rs;
     const int64_t* labels; const float* temb;
-    const float* packed; Packed k; Dims d;
+    const float* packed; PackedOffs k; Dims d;
     float *rb0, *rb4, *rbQ, *skyh, *sky;
     int sem_on, need_q, need_sky;
 };
@@ -147,19 +151,22 @@ __device__ __forceinline__ float wsum(float v) {
 }
 
 // lane-partial dot product of a row with a weight vector, columns 4*lane + 256*i
-__device__ __forceinline__ float pdot(const float* __restrict__ x, const float* __restrict__ w, int n, int lane) {
+template <typename T>
+__device__ __forceinline__ float pdot(const T* __restrict__ x, const float* __restrict__ w, int n, int lane) {
     float s = 0.f;
     for (int k = 4 * lane; k < n; k += 256) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(x + k);
+        const f32x4 a = ld4(x + k);
         const f32x4 b = *reinterpret_cast<const f32x4*>(w + k);
         s += (a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3]);
     }
     return s;
 }
 
+template <typename T>
 struct HeadsArgs {
-    const float* packed; Packed k; Dims d;
-    const float *HL, *G, *Q, *S3, *sky;
+    const float* packed; Dims d;
+    const T *HL, *G, *Q, *S3;
+    const float* sky;
     float* out; float* hsave;
     int64_t P; int S; int mode;  // mode: 0 full, 1 sigma only, 2 sigma + sun
 };
@@ -167,7 +174,8 @@ struct HeadsArgs {
 // Narrow output heads (spnerf.py:333-367): σ = softplus, albedo = sigmoid·1.002−0.001,
 // sun = sigmoid, β = softplus, semantic logits; sky broadcast per ray.  One wavefront per
 // point: every row read is a coalesced 1-KiB sweep, dot products end in a DPP reduction.
-__global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs a) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs<T> a, PackedOffs k) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4;
     const Dims& d = a.d;
@@ -175,17 +183,17 @@ __global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs a) {
     for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < a.P; p += nw) {
         float* o = a.out + p * d.NO;
         float* hs = a.hsave + p * 8;
-        const float spre = wsum(pdot(a.HL + p * d.W, Pk + a.k.wsig, d.W, lane)) + Pk[a.k.bsig];
+        const float spre = wsum(pdot(a.HL + p * d.W, Pk + k.wsig, d.W, lane)) + Pk[k.bsig];
         float sun = 0.f, rgb[3] = {0.f, 0.f, 0.f}, bpre = 0.f;
-        if (a.mode != 1) sun = sigmoidf_(wsum(pdot(a.S3 + p * d.H, Pk + a.k.ws4, d.H, lane)) + Pk[a.k.bs4]);
+        if (a.mode != 1) sun = sigmoidf_(wsum(pdot(a.S3 + p * d.H, Pk + k.ws4, d.H, lane)) + Pk[k.bs4]);
         if (a.mode == 0) {
-            const float* R1 = a.Q + p * d.NQ + d.H;
-            for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf_(wsum(pdot(R1, Pk + a.k.Wr2 + c * d.H, d.H, lane)) + Pk[a.k.br2 + c]);
-            if (d.beta) bpre = wsum(pdot(a.Q + p * d.NQ + 2 * d.H, Pk + a.k.wb2, d.H, lane)) + Pk[a.k.bb2];
+            const T* R1 = a.Q + p * d.NQ + d.H;
+            for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf_(wsum(pdot(R1, Pk + k.Wr2 + c * d.H, d.H, lane)) + Pk[k.br2 + c]);
+            if (d.beta) bpre = wsum(pdot(a.Q + p * d.NQ + 2 * d.H, Pk + k.wb2, d.H, lane)) + Pk[k.bb2];
             if (d.sem) {
-                const float* M1 = a.G + p * d.NG + d.W;
+                const T* M1 = a.G + p * d.NG + d.W;
                 for (int c = 0; c < d.C; ++c) {
-                    const float v = wsum(pdot(M1, Pk + a.k.Wm2 + c * d.H, d.H, lane)) + Pk[a.k.bm2 + c];
+                    const float v = wsum(pdot(M1, Pk + k.Wm2 + c * d.H, d.H, lane)) + Pk[k.bm2 + c];
                     if (lane == 0) o[d.sem_col + c] = v;
                 }
             }
@@ -217,10 +225,13 @@ __global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs a) {
     }
 }
 
+template <typename T>
 struct HeadsBwdArgs {
-    const float* packed; Packed k; Dims d;
-    const float *d_out, *hsave, *DQ, *DG, *DS3;
-    float *hpre, *dZQ, *dZG, *dS3;
+    const float* packed; Dims d;
+    const float *d_out, *hsave;
+    const T *DQ, *DG, *DS3;
+    float* hpre;
+    T *dZQ, *dZG, *dS3;
     int64_t P; int mode;
 };
 
@@ -228,7 +239,8 @@ struct HeadsBwdArgs {
 // (hpre, reduced over points into the head weights by the skinny reduction) and the
 // gradients of the hidden layers feeding them (dX = dY·W, × sin' saved in D*), written as
 // coalesced rows.
-__global__ __launch_bounds__(256) void k_heads_bwd(HeadsBwdArgs a) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_heads_bwd(HeadsBwdArgs<T> a, PackedOffs k) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * 4;
     const Dims& d = a.d;
@@ -261,48 +273,49 @@ __global__ __launch_bounds__(256) void k_heads_bwd(HeadsBwdArgs a) {
             hp[c] = v;
         }
         if (a.mode == 1) continue;
-        for (int k = 4 * lane; k < H; k += 256) {
-            const f32x4 D = *reinterpret_cast<const f32x4*>(a.DS3 + p * H + k);
-            const f32x4 w = *reinterpret_cast<const f32x4*>(Pk + a.k.ws4 + k);
-            *reinterpret_cast<f32x4*>(a.dS3 + p * H + k) = (dys * w) * D;
+        for (int c = 4 * lane; c < H; c += 256) {
+            const f32x4 D = ld4(a.DS3 + p * H + c);
+            const f32x4 w = *reinterpret_cast<const f32x4*>(Pk + k.ws4 + c);
+            st4(a.dS3 + p * H + c, (dys * w) * D);
         }
         if (a.mode == 2) continue;
-        for (int k = 4 * lane; k < H; k += 256) {
-            const f32x4 D = *reinterpret_cast<const f32x4*>(a.DQ + p * d.NQ + H + k);
-            const f32x4 w0 = *reinterpret_cast<const f32x4*>(Pk + a.k.Wr2 + k);
-            const f32x4 w1 = *reinterpret_cast<const f32x4*>(Pk + a.k.Wr2 + H + k);
-            const f32x4 w2 = *reinterpret_cast<const f32x4*>(Pk + a.k.Wr2 + 2 * H + k);
-            *reinterpret_cast<f32x4*>(a.dZQ + p * d.NQ + H + k) = (dy[0] * w0 + dy[1] * w1 + dy[2] * w2) * D;
+        for (int c = 4 * lane; c < H; c += 256) {
+            const f32x4 D = ld4(a.DQ + p * d.NQ + H + c);
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(Pk + k.Wr2 + c);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(Pk + k.Wr2 + H + c);
+            const f32x4 w2 = *reinterpret_cast<const f32x4*>(Pk + k.Wr2 + 2 * H + c);
+            st4(a.dZQ + p * d.NQ + H + c, (dy[0] * w0 + dy[1] * w1 + dy[2] * w2) * D);
             if (d.beta) {
-                const f32x4 Db = *reinterpret_cast<const f32x4*>(a.DQ + p * d.NQ + 2 * H + k);
-                const f32x4 wb = *reinterpret_cast<const f32x4*>(Pk + a.k.wb2 + k);
-                *reinterpret_cast<f32x4*>(a.dZQ + p * d.NQ + 2 * H + k) = (db * wb) * Db;
+                const f32x4 Db = ld4(a.DQ + p * d.NQ + 2 * H + c);
+                const f32x4 wb = *reinterpret_cast<const f32x4*>(Pk + k.wb2 + c);
+                st4(a.dZQ + p * d.NQ + 2 * H + c, (db * wb) * Db);
             }
             if (d.sem) {
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-                for (int c = 0; c < d.C; ++c)
-                    acc += g[d.sem_col + c] * *reinterpret_cast<const f32x4*>(Pk + a.k.Wm2 + c * H + k);
-                const f32x4 Dm = *reinterpret_cast<const f32x4*>(a.DG + p * d.NG + d.W + k);
-                *reinterpret_cast<f32x4*>(a.dZG + p * d.NG + d.W + k) = acc * Dm;
+                for (int j = 0; j < d.C; ++j)
+                    acc += g[d.sem_col + j] * *reinterpret_cast<const f32x4*>(Pk + k.Wm2 + j * H + c);
+                const f32x4 Dm = ld4(a.DG + p * d.NG + d.W + c);
+                st4(a.dZG + p * d.NG + d.W + c, acc * Dm);
             }
         }
     }
 }
 
 // out[ray][n] = Σ_{s<S} in[(ray*S + s)*ld + c0 + n]
-__global__ void k_ray_rowsum(const float* __restrict__ in, int ld, int c0, int N, int S, float* __restrict__ out,
+template <typename T>
+__global__ void k_ray_rowsum(const T* __restrict__ in, int ld, int c0, int N, int S, float* __restrict__ out,
                              int ldo) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t ray = blockIdx.y;
     if (n >= N) return;
-    const float* p = in + ray * S * (int64_t)ld + c0 + n;
+    const T* p = in + ray * S * (int64_t)ld + c0 + n;
     float s = 0.f;
-    for (int i = 0; i < S; ++i) s += p[(int64_t)i * ld];
+    for (int i = 0; i < S; ++i) s += ld1(p + (int64_t)i * ld);
     out[ray * ldo + n] = s;
 }
 
 struct RayBwdArgs {
-    const float* packed; Packed k; Dims d;
+    const float* packed; PackedOffs k; Dims d;
     const float *sky, *skyh, *dsky, *R0, *R4, *RQ;
     const int64_t* labels;
     float *skyd, *skydh, *gemb, *embr, *grad_t;
@@ -406,9 +419,9 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
     auto specs = param_specs(d, &x);
     const Packed k = packed_layout(d);
     std::vector<PackPiece> v;
-    auto piece = [&](int pi, int c0, int rows, int cols, int64_t dst, int dst_ld, int tr) {
+    auto piece = [&](int pi, int c0, int rows, int cols, int64_t dst, int dst_ld, int tr, int bf = 0) {
         SPN_ARG(prm[pi] != nullptr, "parameter %s is NULL", specs[pi].name.c_str());
-        v.push_back(PackPiece{prm[pi], (int)specs[pi].ld(), c0, rows, cols, dst_ld, tr, dst});
+        v.push_back(PackPiece{prm[pi], (int)specs[pi].ld(), c0, rows, cols, dst_ld, tr, bf, dst});
         return SPNERF_OK;
     };
     const int W = d.W, H = d.H;
@@ -462,6 +475,31 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
     SPN_TRY(piece(x.k1b, 0, 1, H, k.bk1, H, 0));
     SPN_TRY(piece(x.k2W, 0, 3, H, k.Wk2, H, 0));
     SPN_TRY(piece(x.k2b, 0, 1, 3, k.bk2, 3, 0));
+    if (d.bf) {  // bf16 GEMM operands (same shapes as their fp32 counterparts above)
+        for (int i = 1; i < d.L; ++i) {
+            const int kreal = i == d.skip ? W + d.K0 : W;
+            SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wt16[i], k.Kp[i], 0, 1));
+            SPN_TRY(piece(x.fcW[i], 0, W, W, k.WTt16[i], W, 1, 1));
+        }
+        if (d.sem) {
+            SPN_TRY(piece(x.m1W, 0, H, W, k.WG16 + (int64_t)W * W, W, 0, 1));
+            SPN_TRY(piece(x.m1W, 0, H, W, k.WGT16 + W, d.NG, 1, 1));
+        }
+        SPN_TRY(piece(x.featW, 0, W, W, k.WG16, W, 0, 1));
+        SPN_TRY(piece(x.featW, 0, W, W, k.WGT16, d.NG, 1, 1));
+        SPN_TRY(piece(x.s1W, 0, H, W, k.WQ16, W, 0, 1));
+        SPN_TRY(piece(x.r1W, 0, H, W, k.WQ16 + (int64_t)H * W, W, 0, 1));
+        SPN_TRY(piece(x.s1W, 0, H, W, k.WQT16, d.NQ, 1, 1));
+        SPN_TRY(piece(x.r1W, 0, H, W, k.WQT16 + H, d.NQ, 1, 1));
+        if (d.beta) {
+            SPN_TRY(piece(x.b1W, 0, H, W, k.WQ16 + (int64_t)2 * H * W, W, 0, 1));
+            SPN_TRY(piece(x.b1W, 0, H, W, k.WQT16 + 2 * H, d.NQ, 1, 1));
+        }
+        SPN_TRY(piece(x.s2W, 0, H, H, k.Ws2_16, H, 0, 1));
+        SPN_TRY(piece(x.s2W, 0, H, H, k.Ws2T16, H, 1, 1));
+        SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3_16, H, 0, 1));
+        SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3T16, H, 1, 1));
+    }
     return launch_pack(v, packed, s);
 }
 
@@ -475,20 +513,49 @@ struct Ctx {
     int S;
     float* at(int64_t off) const { return ws + off; }
     const float* pk(int64_t off) const { return P + off; }
+    bf16* hb(int64_t off) const { return reinterpret_cast<bf16*>(ws + off); }          // bf16 workspace buffer
+    const bf16* pk16(int64_t off) const { return reinterpret_cast<const bf16*>(P) + off; }  // bf16 packed weights
 };
 }  // namespace
 
-static int32_t tn_grad(const Ctx& c, const float* A, int lda, int N, const float* B, int ldb, const float* B2, int ldb2,
-                       int K1, int K, hipStream_t s, std::initializer_list<ReduceArgs> outs) {
+// dtype dispatch for the GEMM sequence: fp32 (NTArgs / TNArgs) or bf16 (NT16Args / TN16Args,
+// same field names); T is the activation element type.
+template <typename T>
+struct Gemms;
+template <>
+struct Gemms<float> {
+    using NT = NTArgs;
+    using TN = TNArgs;
+    static float* buf(const Ctx& c, int64_t off) { return c.at(off); }
+    static const float* w(const Ctx& c, int64_t off32, int64_t) { return c.pk(off32); }
+    static int32_t nt(const NT& a, hipStream_t s) { return gemm_nt(a, s); }
+    static int splits(int P, int N, int K) { return tn_splits(P, N, K); }
+    static int32_t tn(const TN& a, int sp, hipStream_t s) { return gemm_tn(a, sp, s); }
+};
+template <>
+struct Gemms<bf16> {
+    using NT = NT16Args;
+    using TN = TN16Args;
+    static bf16* buf(const Ctx& c, int64_t off) { return c.hb(off); }
+    static const bf16* w(const Ctx& c, int64_t, int64_t off16) { return c.pk16(off16); }
+    static int32_t nt(const NT& a, hipStream_t s) { return gemm_nt_bf16(a, s); }
+    static int splits(int P, int N, int K) { return tn_splits_bf16(P, N, K); }
+    static int32_t tn(const TN& a, int sp, hipStream_t s) { return gemm_tn_bf16(a, sp, s); }
+};
+
+template <typename T>
+static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int ldb, const T* B2, int ldb2, int K1,
+                       int K, hipStream_t s, std::initializer_list<ReduceArgs> outs) {
+    using G = Gemms<T>;
     const int P = (int)c.w.P;
-    const int splits = tn_splits(P, N, K);
-    TNArgs t;
+    const int splits = G::splits(P, N, K);
+    typename G::TN t;
     t.A = A; t.lda = lda;
     t.B = B; t.ldb = ldb; t.B2 = B2; t.ldb2 = ldb2; t.K1 = K1;
     t.slab = c.at(c.w.slab); t.ld_slab = K; t.slab_stride = (int64_t)N * K;
     t.slab_b = c.at(c.w.slab_b);
     t.P = P; t.N = N; t.K = K;
-    SPN_TRY(gemm_tn(t, splits, s));
+    SPN_TRY(G::tn(t, splits, s));
     for (ReduceArgs r : outs) {
         r.slab = t.slab; r.ld_slab = K; r.slab_stride = t.slab_stride; r.splits = splits; r.N = N;
         r.slab_b = t.slab_b;
@@ -505,10 +572,13 @@ static ReduceArgs red(int row0, int nrows, int ncols, float* dst, int ld_dst, fl
 
 // out[m][k] = Σ_r A[r*lda+m] · B[r*ldb+k] over `rows` rows (points or rays), written to dst
 // (row-major, or dst[k][m] with `transpose`); dst_b[m] = Σ_r A[r][m]; dst_ones[k] = Σ_r B[r][k].
-static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int Ma, const float* B, int ldb, int K,
+template <typename TB>
+static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int Ma, const TB* B, int ldb, int K,
                       float* dst, int ld_dst, int transpose, float* dst_b, float* dst_ones, hipStream_t s) {
     SkinnyArgs k;
-    k.A = A; k.lda = lda; k.Ma = Ma; k.B = B; k.ldb = ldb; k.K = K; k.P = rows; k.ones = dst_ones ? 1 : 0;
+    k.A = A; k.lda = lda; k.Ma = Ma; k.ldb = ldb; k.K = K; k.P = rows; k.ones = dst_ones ? 1 : 0;
+    if constexpr (std::is_same<TB, bf16>::value) k.B16 = B;
+    else k.B = B;
     k.slab = c.at(c.w.sk_slab); k.slab_b = c.at(c.w.sk_slab_b);
     SPN_TRY(tn_skinny(k, s));
     const int chunks = cdiv(rows, skinny_chunk(rows));
@@ -523,6 +593,94 @@ static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int M
         SPN_TRY(reduce_slabs(o, s));
     }
     return SPNERF_OK;
+}
+
+// Trunk + G/Q/sun_v GEMMs of the forward (spnerf.py:323-355).  In the bf16 MLP, layer 0 stays
+// an fp32 GEMM (sin(30·x) amplifies operand rounding 30x) that writes bf16 H_1 / D_1.
+template <typename T>
+static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
+    using G = Gemms<T>;
+    using NT = typename G::NT;
+    const Dims& d = c.d;
+    const int64_t P = c.w.P;
+    const int W = d.W, H = d.H, S = c.S;
+    constexpr bool BF = std::is_same<T, bf16>::value;
+    const T* X0 = BF ? G::buf(c, c.w.X0b) : G::buf(c, c.w.X0);
+    const T* h = nullptr;
+    T* HL = nullptr;
+    for (int i = 0; i < d.L; ++i) {
+        T* dst = save ? G::buf(c, c.w.Hb[i]) : G::buf(c, c.w.Hb[i & 1]);
+        T* dd = save ? G::buf(c, c.w.Db[i]) : nullptr;
+        const float* rb = (d.sem && (i == 0 || i == d.skip)) ? c.at(i == 0 ? c.w.rb0 : c.w.rb4) : nullptr;
+        if (i == 0) {
+            NTArgs g;
+            g.A = c.at(c.w.X0); g.lda = d.K0p; g.K1 = d.K0p;
+            g.B = c.pk(c.k.Wt[0]); g.ldb = d.K0p;
+            g.ldc = W;
+            g.M = (int)P; g.N = W; g.K = d.K0p;
+            g.bias = c.pk(c.k.bt[0]);
+            if (rb) { g.rowbias = rb; g.ld_rb = W; g.rows_per_ray = S; }
+            g.act = 1; g.w0 = 30.f; g.n_lin = 0;
+            g.ld_dout = W;
+            if constexpr (BF) { g.C16 = dst; g.D16 = dd; }
+            else { g.C = dst; g.Dout = dd; }
+            SPN_TRY(gemm_nt(g, s));
+        } else {
+            NT g;
+            g.A = h; g.lda = W; g.K1 = W;
+            if (i == d.skip) { g.A2 = X0; g.lda2 = d.K0p; }
+            g.B = G::w(c, c.k.Wt[i], BF ? c.k.Wt16[i] : -1); g.ldb = c.k.Kp[i];
+            g.C = dst; g.ldc = W;
+            g.M = (int)P; g.N = W; g.K = c.k.Kp[i];
+            g.bias = c.pk(c.k.bt[i]);
+            if (rb) { g.rowbias = rb; g.ld_rb = W; g.rows_per_ray = S; }
+            g.act = 1; g.w0 = 1.f; g.n_lin = 0;
+            if (save) { g.Dout = dd; g.ld_dout = W; }
+            SPN_TRY(G::nt(g, s));
+        }
+        h = dst;
+        HL = dst;
+    }
+    if (mode == 1) return SPNERF_OK;
+    T* S2buf = save ? G::buf(c, c.w.S2) : G::buf(c, c.w.Hb[((d.L - 1) & 1) ^ 1]);
+    T* S3buf = save ? G::buf(c, c.w.S3) : G::buf(c, c.w.Hb[2]);
+    // G = H_L · [feat ; sem hidden]^T   (feat linear, sem hidden sin)
+    NT g;
+    g.A = HL; g.lda = W; g.K1 = W;
+    g.B = G::w(c, c.k.WG, c.k.WG16); g.ldb = W;
+    g.C = G::buf(c, c.w.G); g.ldc = d.NG;
+    g.M = (int)P; g.N = mode == 0 ? d.NG : W; g.K = W;
+    g.bias = c.pk(c.k.bG);
+    g.act = 1; g.w0 = 1.f; g.n_lin = W;
+    if (save) { g.Dout = G::buf(c, c.w.DG); g.ld_dout = d.NG; }
+    SPN_TRY(G::nt(g, s));
+    // Q = feat · [sun1 ; rgb1 ; beta1]^T + per-ray (sun_d / t) rows, all sin
+    NT q;
+    q.A = G::buf(c, c.w.G); q.lda = d.NG; q.K1 = W;
+    q.B = G::w(c, c.k.WQ, c.k.WQ16); q.ldb = W;
+    q.C = G::buf(c, c.w.Q); q.ldc = d.NQ;
+    q.M = (int)P; q.N = mode == 0 ? d.NQ : H; q.K = W;
+    q.bias = c.pk(c.k.bQ);
+    q.rowbias = c.at(c.w.rbQ); q.ld_rb = d.NQ; q.rows_per_ray = S;
+    q.act = 1; q.w0 = 1.f;
+    if (save) { q.Dout = G::buf(c, c.w.DQ); q.ld_dout = d.NQ; }
+    SPN_TRY(G::nt(q, s));
+    // sun_v_net layers 2 and 3
+    NT s2;
+    s2.A = G::buf(c, c.w.Q); s2.lda = d.NQ; s2.K1 = H;
+    s2.B = G::w(c, c.k.Ws2, c.k.Ws2_16); s2.ldb = H;
+    s2.C = S2buf; s2.ldc = H;
+    s2.M = (int)P; s2.N = H; s2.K = H;
+    s2.bias = c.pk(c.k.bs2); s2.act = 1; s2.w0 = 1.f;
+    if (save) { s2.Dout = G::buf(c, c.w.DS2); s2.ld_dout = H; }
+    SPN_TRY(G::nt(s2, s));
+    NT s3 = s2;
+    s3.A = S2buf; s3.lda = H;
+    s3.B = G::w(c, c.k.Ws3, c.k.Ws3_16);
+    s3.C = S3buf;
+    s3.bias = c.pk(c.k.bs3);
+    s3.Dout = save ? G::buf(c, c.w.DS3) : nullptr;
+    return G::nt(s3, s);
 }
 
 static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays, int rs, int dir_off,
@@ -552,89 +710,157 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
             SPN_HIP(hipGetLastError());
         }
     }
-    // positional encoding
+    // positional encoding (fp32 for layer 0, plus a bf16 copy for the skip layer / dW_0)
     {
         const int64_t n = P * d.K0p;
-        ProfScope prof("encode", s, 0.0, 4.0 * n);
+        ProfScope prof("encode", s, 0.0, (d.bf ? 6.0 : 4.0) * n);
         hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rays, rs, dir_off, z, S, P,
-                           d.K0 == 3 ? 0 : d.K0 / 6, d.K0, d.K0p, c.at(c.w.X0));
+                           d.K0 == 3 ? 0 : d.K0 / 6, d.K0, d.K0p, c.at(c.w.X0), d.bf ? c.hb(c.w.X0b) : nullptr);
         SPN_HIP(hipGetLastError());
     }
-    // trunk
-    const float* X0 = c.at(c.w.X0);
-    const float* h = X0;
-    int ldh = d.K0p;
-    float* HL = nullptr;
-    for (int i = 0; i < d.L; ++i) {
-        float* dst = save ? c.at(c.w.Hb[i]) : c.at(c.w.Hb[i & 1]);
-        NTArgs g;
-        if (i == d.skip) {
-            g.A = h; g.lda = ldh; g.A2 = X0; g.lda2 = d.K0p; g.K1 = W;
-        } else {
-            g.A = h; g.lda = ldh; g.K1 = c.k.Kp[i];
-        }
-        g.B = c.pk(c.k.Wt[i]); g.ldb = c.k.Kp[i];
-        g.C = dst; g.ldc = W;
-        g.M = (int)P; g.N = W; g.K = c.k.Kp[i];
-        g.bias = c.pk(c.k.bt[i]);
-        if (d.sem && (i == 0 || i == d.skip)) {
-            g.rowbias = c.at(i == 0 ? c.w.rb0 : c.w.rb4); g.ld_rb = W; g.rows_per_ray = S;
-        }
-        g.act = 1; g.w0 = i == 0 ? 30.f : 1.f; g.n_lin = 0;
-        if (save) { g.Dout = c.at(c.w.Db[i]); g.ld_dout = W; }
-        SPN_TRY(gemm_nt(g, s));
-        h = dst;
-        ldh = W;
-        HL = dst;
-    }
-    float* S2buf = save ? c.at(c.w.S2) : c.at(c.w.Hb[((d.L - 1) & 1) ^ 1]);
-    float* S3buf = save ? c.at(c.w.S3) : c.at(c.w.Hb[2]);
-    if (mode != 1) {
-        // G = H_L · [feat ; sem hidden]^T   (feat linear, sem hidden sin)
-        const int NG = mode == 0 ? d.NG : W;
-        NTArgs g;
-        g.A = HL; g.lda = W; g.K1 = W;
-        g.B = c.pk(c.k.WG); g.ldb = W;
-        g.C = c.at(c.w.G); g.ldc = d.NG;
-        g.M = (int)P; g.N = NG; g.K = W;
-        g.bias = c.pk(c.k.bG);
-        g.act = 1; g.w0 = 1.f; g.n_lin = W;
-        if (save) { g.Dout = c.at(c.w.DG); g.ld_dout = d.NG; }
-        SPN_TRY(gemm_nt(g, s));
-        // Q = feat · [sun1 ; rgb1 ; beta1]^T + per-ray (sun_d / t) rows, all sin
-        const int NQ = mode == 0 ? d.NQ : H;
-        NTArgs q;
-        q.A = c.at(c.w.G); q.lda = d.NG; q.K1 = W;
-        q.B = c.pk(c.k.WQ); q.ldb = W;
-        q.C = c.at(c.w.Q); q.ldc = d.NQ;
-        q.M = (int)P; q.N = NQ; q.K = W;
-        q.bias = c.pk(c.k.bQ);
-        q.rowbias = c.at(c.w.rbQ); q.ld_rb = d.NQ; q.rows_per_ray = S;
-        q.act = 1; q.w0 = 1.f;
-        if (save) { q.Dout = c.at(c.w.DQ); q.ld_dout = d.NQ; }
-        SPN_TRY(gemm_nt(q, s));
-        // sun_v_net layers 2 and 3
-        NTArgs s2;
-        s2.A = c.at(c.w.Q); s2.lda = d.NQ; s2.K1 = H;
-        s2.B = c.pk(c.k.Ws2); s2.ldb = H;
-        s2.C = S2buf; s2.ldc = H;
-        s2.M = (int)P; s2.N = H; s2.K = H;
-        s2.bias = c.pk(c.k.bs2); s2.act = 1; s2.w0 = 1.f;
-        if (save) { s2.Dout = c.at(c.w.DS2); s2.ld_dout = H; }
-        SPN_TRY(gemm_nt(s2, s));
-        NTArgs s3 = s2;
-        s3.A = S2buf; s3.lda = H;
-        s3.B = c.pk(c.k.Ws3);
-        s3.C = S3buf;
-        s3.bias = c.pk(c.k.bs3);
-        s3.Dout = save ? c.at(c.w.DS3) : nullptr;
-        SPN_TRY(gemm_nt(s3, s));
-    }
+    if (d.bf) SPN_TRY(forward_gemms<bf16>(c, save, mode, s));
+    else SPN_TRY(forward_gemms<float>(c, save, mode, s));
     {
-        HeadsArgs a{packed, c.k, d, HL, c.at(c.w.G), c.at(c.w.Q), S3buf, c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode};
-        ProfScope prof("heads_fwd", s, 2.0 * P * (W + (mode != 1 ? 4 * H + H * d.C : 0)), 4.0 * P * (W + 3 * H + d.NO));
-        hipLaunchKernelGGL(k_heads_fwd, dim3((unsigned)std::min<int64_t>(cdiv(P, 4), 8192)), dim3(256), 0, s, a);
+        const int64_t L = d.L - 1;
+        const int64_t hl = save ? c.w.Hb[L] : c.w.Hb[L & 1];
+        const int64_t s3 = save ? c.w.S3 : c.w.Hb[2];
+        const int grid = (int)std::min<int64_t>(cdiv(P, 4), 8192);
+        ProfScope prof("heads_fwd", s, 2.0 * P * (W + (mode != 1 ? 4 * H + H * d.C : 0)),
+                       (d.bf ? 2.0 : 4.0) * P * (W + 3 * H) + 4.0 * P * d.NO);
+        if (d.bf) {
+            HeadsArgs<bf16> a{packed, d, c.hb(hl), c.hb(c.w.G), c.hb(c.w.Q), c.hb(s3), c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode};
+            hipLaunchKernelGGL(k_heads_fwd<bf16>, dim3(grid), dim3(256), 0, s, a, (PackedOffs)c.k);
+        } else {
+            HeadsArgs<float> a{packed, d, c.at(hl), c.at(c.w.G), c.at(c.w.Q), c.at(s3), c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode};
+            hipLaunchKernelGGL(k_heads_fwd<float>, dim3(grid), dim3(256), 0, s, a, (PackedOffs)c.k);
+        }
         SPN_HIP(hipGetLastError());
+    }
+    return SPNERF_OK;
+}
+
+// Backward of the per-point network (steps 1-6): narrow heads, head / sun_v / feat / trunk
+// weight gradients (split-P TN GEMMs + fixed-order slab reduction), dX GEMMs with the saved
+// sin' as Dmul, and the per-ray sums R0 / R4 / RQ feeding the per-ray parameters.
+template <typename T>
+static int32_t backward_points(const Ctx& c, int mode, const float* packed, const float* d_out, int64_t n_rays,
+                               float* grad, hipStream_t s) {
+    using G = Gemms<T>;
+    using NT = typename G::NT;
+    constexpr bool BF = std::is_same<T, bf16>::value;
+    const Dims& d = c.d;
+    const int64_t P = c.w.P;
+    const int W = d.W, H = d.H, S = c.S;
+    PIdx x;
+    auto specs = param_specs(d, &x);
+    auto gp = [&](int pi) { return grad + specs[pi].off; };
+    auto ld = [&](int pi) { return (int)specs[pi].ld(); };
+    auto buf = [&](int64_t off) { return G::buf(c, off); };
+
+    T* HL = buf(c.w.Hb[d.L - 1]);
+    T* Gb = buf(c.w.G);
+    T* Qb = buf(c.w.Q);
+    T* dZG = buf(c.w.dZG);
+    T* dZQ = buf(c.w.dZQ);
+    T* dS3 = buf(c.w.dS3);
+    T* dS2 = buf(c.w.dS2);
+    float* hpre = c.at(c.w.hpre);
+
+    // 1. narrow heads
+    {
+        HeadsBwdArgs<T> a{packed, d, d_out, c.at(c.w.hsave), buf(c.w.DQ), buf(c.w.DG), buf(c.w.DS3), hpre, dZQ, dZG, dS3,
+                          P, mode};
+        const double eb = BF ? 2.0 : 4.0;
+        ProfScope prof("heads_bwd", s, 2.0 * P * 4 * H, 4.0 * P * (d.NO + d.HP) + eb * P * 6 * H);
+        hipLaunchKernelGGL(k_heads_bwd<T>, dim3((unsigned)std::min<int64_t>(cdiv(P, 4), 8192)), dim3(256), 0, s, a,
+                           (PackedOffs)c.k);
+        SPN_HIP(hipGetLastError());
+    }
+    // 2. narrow-head weights: reductions over points
+    SPN_TRY(skinny(c, P, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), W, 0, gp(x.sigb), nullptr, s));
+    SPN_TRY(skinny(c, P, hpre + 4, d.HP, 1, buf(c.w.S3), H, H, gp(x.s4W), H, 0, gp(x.s4b), nullptr, s));
+    if (mode == 0) {
+        SPN_TRY(skinny(c, P, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), H, 0, gp(x.r2b), nullptr, s));
+        if (d.beta) SPN_TRY(skinny(c, P, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), H, 0, gp(x.b2b), nullptr, s));
+        if (d.sem) SPN_TRY(skinny(c, P, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), H, 0, gp(x.m2b), nullptr, s));
+    }
+    // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
+    {
+        NT g;
+        g.A = dS3; g.lda = H; g.K1 = H; g.B = G::w(c, c.k.Ws3T, c.k.Ws3T16); g.ldb = H; g.C = dS2; g.ldc = H;
+        g.M = (int)P; g.N = H; g.K = H; g.Dmul = buf(c.w.DS2); g.ld_dmul = H;
+        SPN_TRY(G::nt(g, s));
+        SPN_TRY(tn_grad<T>(c, dS3, H, H, buf(c.w.S2), H, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}));
+        NT g2 = g;
+        g2.A = dS2; g2.B = G::w(c, c.k.Ws2T, c.k.Ws2T16); g2.C = dZQ; g2.ldc = d.NQ; g2.Dmul = buf(c.w.DQ); g2.ld_dmul = d.NQ;
+        SPN_TRY(G::nt(g2, s));
+        SPN_TRY(tn_grad<T>(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
+    }
+    // 4. feat: dF = dZ_Q · WQ → dZG[:, :W];  dWQ = dZ_Q^T · feat
+    const int NQ = mode == 0 ? d.NQ : H;
+    {
+        NT g;
+        g.A = dZQ; g.lda = d.NQ; g.K1 = NQ; g.B = G::w(c, c.k.WQT, c.k.WQT16); g.ldb = d.NQ; g.C = dZG; g.ldc = d.NG;
+        g.M = (int)P; g.N = W; g.K = NQ;
+        SPN_TRY(G::nt(g, s));
+        if (mode == 0) {
+            if (d.beta)
+                SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, NQ, Gb, d.NG, nullptr, 0, W, W, s,
+                                   {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b)),
+                                    red(2 * H, H, W, gp(x.b1W), ld(x.b1W), gp(x.b1b))}));
+            else
+                SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, NQ, Gb, d.NG, nullptr, 0, W, W, s,
+                                   {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b))}));
+        } else {
+            SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
+        }
+        // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns
+        hipLaunchKernelGGL(k_ray_rowsum<T>, dim3(cdiv(NQ, 256), (unsigned)n_rays), dim3(256), 0, s, dZQ, d.NQ, 0, NQ, S,
+                           c.at(c.w.RQ), d.NQ);
+        SPN_HIP(hipGetLastError());
+    }
+    // 5. H_L: dH_L = dZ_G · WG + dσ ⊗ w_σ ;  dZ_{L-1} = dH_L ⊙ D_L ;  dWG = dZ_G^T · H_L
+    const int NG = mode == 0 ? d.NG : W;
+    T* dZ = buf(c.w.dZa);
+    T* dZn = buf(c.w.dZb);
+    {
+        NT g;
+        g.A = dZG; g.lda = d.NG; g.K1 = NG; g.B = G::w(c, c.k.WGT, c.k.WGT16); g.ldb = d.NG; g.C = dZ; g.ldc = W;
+        g.M = (int)P; g.N = W; g.K = NG;
+        g.r1_a = hpre; g.r1_lda = d.HP; g.r1_v = c.pk(c.k.wsig);
+        g.Dmul = buf(c.w.Db[d.L - 1]); g.ld_dmul = W;
+        SPN_TRY(G::nt(g, s));
+        if (mode == 0 && d.sem)
+            SPN_TRY(tn_grad<T>(c, dZG, d.NG, d.NG, HL, W, nullptr, 0, W, W, s,
+                               {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
+        else
+            SPN_TRY(tn_grad<T>(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
+    }
+    // 6. trunk, top to bottom
+    const T* X0 = BF ? buf(c.w.X0b) : buf(c.w.X0);
+    for (int i = d.L - 1; i >= 0; --i) {
+        // dZ holds dL/d(pre-activation of layer i)
+        const T* In = i == 0 ? X0 : buf(c.w.Hb[i - 1]);
+        const int ldin = i == 0 ? d.K0p : W;
+        const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
+        if (i == d.skip)
+            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, W, X0, d.K0p, W, W + d.K0p, s,
+                               {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
+        else
+            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s,
+                               {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
+        if (d.sem && (i == 0 || i == d.skip)) {
+            hipLaunchKernelGGL(k_ray_rowsum<T>, dim3(cdiv(W, 256), (unsigned)n_rays), dim3(256), 0, s, dZ, W, 0, W, S,
+                               c.at(i == 0 ? c.w.R0 : c.w.R4), W);
+            SPN_HIP(hipGetLastError());
+        }
+        if (i > 0) {
+            NT g;
+            g.A = dZ; g.lda = W; g.K1 = W; g.B = G::w(c, c.k.WTt[i], BF ? c.k.WTt16[i] : -1); g.ldb = W; g.C = dZn; g.ldc = W;
+            g.M = (int)P; g.N = W; g.K = W; g.Dmul = buf(c.w.Db[i - 1]); g.ld_dmul = W;
+            SPN_TRY(G::nt(g, s));
+            std::swap(dZ, dZn);
+        }
     }
     return SPNERF_OK;
 }
@@ -656,120 +882,13 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
     if (P == 0) return SPNERF_OK;
     auto gp = [&](int pi) { return grad + specs[pi].off; };
     auto ld = [&](int pi) { return (int)specs[pi].ld(); };
-
-    float* HL = c.at(c.w.Hb[d.L - 1]);
-    float* Gb = c.at(c.w.G);
-    float* Qb = c.at(c.w.Q);
-    float* dZG = c.at(c.w.dZG);
-    float* dZQ = c.at(c.w.dZQ);
-    float* dS3 = c.at(c.w.dS3);
-    float* dS2 = c.at(c.w.dS2);
-    float* hpre = c.at(c.w.hpre);
-
-    // 1. narrow heads
-    {
-        HeadsBwdArgs a{packed, c.k, d, d_out, c.at(c.w.hsave), c.at(c.w.DQ), c.at(c.w.DG), c.at(c.w.DS3),
-                       hpre, dZQ, dZG, dS3, P, mode};
-        ProfScope prof("heads_bwd", s, 2.0 * P * 4 * H, 4.0 * P * (d.NO + 3 * H + 3 * H));
-        hipLaunchKernelGGL(k_heads_bwd, dim3((unsigned)std::min<int64_t>(cdiv(P, 4), 8192)), dim3(256), 0, s, a);
-        SPN_HIP(hipGetLastError());
-    }
-    // 2. narrow-head weights: reductions over points
-    SPN_TRY(skinny(c, P, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), W, 0, gp(x.sigb), nullptr, s));
-    SPN_TRY(skinny(c, P, hpre + 4, d.HP, 1, c.at(c.w.S3), H, H, gp(x.s4W), H, 0, gp(x.s4b), nullptr, s));
-    if (mode == 0) {
-        SPN_TRY(skinny(c, P, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), H, 0, gp(x.r2b), nullptr, s));
-        if (d.beta) SPN_TRY(skinny(c, P, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), H, 0, gp(x.b2b), nullptr, s));
-        if (d.sem) SPN_TRY(skinny(c, P, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), H, 0, gp(x.m2b), nullptr, s));
-    }
-    // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
-    {
-        NTArgs g;
-        g.A = dS3; g.lda = H; g.K1 = H; g.B = c.pk(c.k.Ws3T); g.ldb = H; g.C = dS2; g.ldc = H;
-        g.M = (int)P; g.N = H; g.K = H; g.Dmul = c.at(c.w.DS2); g.ld_dmul = H;
-        SPN_TRY(gemm_nt(g, s));
-        SPN_TRY(tn_grad(c, dS3, H, H, c.at(c.w.S2), H, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}));
-        NTArgs g2 = g;
-        g2.A = dS2; g2.B = c.pk(c.k.Ws2T); g2.C = dZQ; g2.ldc = d.NQ; g2.Dmul = c.at(c.w.DQ); g2.ld_dmul = d.NQ;
-        SPN_TRY(gemm_nt(g2, s));
-        SPN_TRY(tn_grad(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
-    }
-    // 4. feat: dF = dZ_Q · WQ → dZG[:, :W];  dWQ = dZ_Q^T · feat
-    const int NQ = mode == 0 ? d.NQ : H;
-    {
-        NTArgs g;
-        g.A = dZQ; g.lda = d.NQ; g.K1 = NQ; g.B = c.pk(c.k.WQT); g.ldb = d.NQ; g.C = dZG; g.ldc = d.NG;
-        g.M = (int)P; g.N = W; g.K = NQ;
-        SPN_TRY(gemm_nt(g, s));
-        if (mode == 0) {
-            std::vector<ReduceArgs> outs = {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)),
-                                            red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b))};
-            if (d.beta) outs.push_back(red(2 * H, H, W, gp(x.b1W), ld(x.b1W), gp(x.b1b)));
-            const int splits = tn_splits((int)P, NQ, W);
-            TNArgs t;
-            t.A = dZQ; t.lda = d.NQ; t.B = Gb; t.ldb = d.NG; t.K1 = W;
-            t.slab = c.at(c.w.slab); t.ld_slab = W; t.slab_stride = (int64_t)NQ * W; t.slab_b = c.at(c.w.slab_b);
-            t.P = (int)P; t.N = NQ; t.K = W;
-            SPN_TRY(gemm_tn(t, splits, s));
-            for (ReduceArgs r : outs) {
-                r.slab = t.slab; r.ld_slab = W; r.slab_stride = t.slab_stride; r.splits = splits; r.N = NQ; r.slab_b = t.slab_b;
-                SPN_TRY(reduce_slabs(r, s));
-            }
-        } else {
-            SPN_TRY(tn_grad(c, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
-        }
-        // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns
-        hipLaunchKernelGGL(k_ray_rowsum, dim3(cdiv(NQ, 256), (unsigned)n_rays), dim3(256), 0, s, dZQ, d.NQ, 0, NQ, S,
-                           c.at(c.w.RQ), d.NQ);
-        SPN_HIP(hipGetLastError());
-    }
-    // 5. H_L: dH_L = dZ_G · WG + dσ ⊗ w_σ ;  dZ_{L-1} = dH_L ⊙ D_L ;  dWG = dZ_G^T · H_L
-    const int NG = mode == 0 ? d.NG : W;
-    float* dZ = c.at(c.w.dZa);
-    float* dZn = c.at(c.w.dZb);
-    {
-        NTArgs g;
-        g.A = dZG; g.lda = d.NG; g.K1 = NG; g.B = c.pk(c.k.WGT); g.ldb = d.NG; g.C = dZ; g.ldc = W;
-        g.M = (int)P; g.N = W; g.K = NG;
-        g.r1_a = hpre; g.r1_lda = d.HP; g.r1_v = c.pk(c.k.wsig);
-        g.Dmul = c.at(c.w.Db[d.L - 1]); g.ld_dmul = W;
-        SPN_TRY(gemm_nt(g, s));
-        if (mode == 0 && d.sem)
-            SPN_TRY(tn_grad(c, dZG, d.NG, d.NG, HL, W, nullptr, 0, W, W, s,
-                            {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
-        else
-            SPN_TRY(tn_grad(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
-    }
-    // 6. trunk, top to bottom
-    for (int i = d.L - 1; i >= 0; --i) {
-        // dZ holds dL/d(pre-activation of layer i)
-        const float* In = i == 0 ? c.at(c.w.X0) : c.at(c.w.Hb[i - 1]);
-        const int ldin = i == 0 ? d.K0p : W;
-        const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
-        if (i == d.skip)
-            SPN_TRY(tn_grad(c, dZ, W, W, In, W, c.at(c.w.X0), d.K0p, W, W + d.K0p, s,
-                            {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
-        else
-            SPN_TRY(tn_grad(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s,
-                            {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
-        if (d.sem && (i == 0 || i == d.skip)) {
-            hipLaunchKernelGGL(k_ray_rowsum, dim3(cdiv(W, 256), (unsigned)n_rays), dim3(256), 0, s, dZ, W, 0, W, S,
-                               c.at(i == 0 ? c.w.R0 : c.w.R4), W);
-            SPN_HIP(hipGetLastError());
-        }
-        if (i > 0) {
-            NTArgs g;
-            g.A = dZ; g.lda = W; g.K1 = W; g.B = c.pk(c.k.WTt[i]); g.ldb = W; g.C = dZn; g.ldc = W;
-            g.M = (int)P; g.N = W; g.K = W; g.Dmul = c.at(c.w.Db[i - 1]); g.ld_dmul = W;
-            SPN_TRY(gemm_nt(g, s));
-            std::swap(dZ, dZn);
-        }
-    }
+    if (d.bf) SPN_TRY(backward_points<bf16>(c, mode, packed, d_out, n_rays, grad, s));
+    else SPN_TRY(backward_points<float>(c, mode, packed, d_out, n_rays, grad, s));
     // 7. per-ray parameters: sun-direction columns, t columns, sky MLP, semantic embedding
     {
         const int sky_on = mode == 0;
         if (sky_on) {
-            hipLaunchKernelGGL(k_ray_rowsum, dim3(1, (unsigned)n_rays), dim3(256), 0, s, d_out, d.NO, 5, 3, S,
+            hipLaunchKernelGGL(k_ray_rowsum<float>, dim3(1, (unsigned)n_rays), dim3(256), 0, s, d_out, d.NO, 5, 3, S,
                                c.at(c.w.dsky), 4);
             SPN_HIP(hipGetLastError());
         }

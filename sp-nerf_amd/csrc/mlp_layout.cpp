@@ -3,6 +3,7 @@
 
 #include <algorithm>
 
+#include "gemm_bf16.h"
 #include "gemm_f32.h"
 
 namespace spn {
@@ -19,7 +20,7 @@ int32_t make_dims(const spnerf_model_cfg* c, Dims* d) {
     SPN_ARG((c->sem_classes == 0) == (c->sem_dim == 0), "sem_classes/sem_dim mismatch");
     SPN_ARG(c->sem_dim <= 64, "sem_dim %d too large", c->sem_dim);
     SPN_ARG(!c->beta || (c->t_dim > 0 && c->t_dim <= 64), "t_dim %d out of range", c->t_dim);
-    SPN_ARG(c->dtype == 0, "dtype %d not supported by this build (fp32 only)", c->dtype);
+    SPN_ARG(c->dtype == 0 || c->dtype == 1, "dtype %d not supported (0 = fp32, 1 = bf16)", c->dtype);
     d->W = c->width;
     d->H = c->width / 2;
     d->L = c->layers;
@@ -36,6 +37,7 @@ int32_t make_dims(const spnerf_model_cfg* c, Dims* d) {
     d->NO = 8 + (d->beta ? 1 : 0) + d->C;
     d->sem_col = 8 + (d->beta ? 1 : 0);
     d->HP = 6 + d->C;
+    d->bf = c->dtype == 1;
     return SPNERF_OK;
 }
 
@@ -143,6 +145,21 @@ Packed packed_layout(const Dims& d) {
     k.emb = take((int64_t)(d.C + 1) * (d.sd ? d.sd : 1));
     k.Wsun = take(3 * H);
     k.Wtt = take((int64_t)H * (d.td ? d.td : 1));
+    if (d.bf) {
+        auto take16 = [&](int64_t n) { return 2 * take((n + 1) / 2); };
+        for (int i = 0; i < d.L; ++i) {
+            k.Wt16.push_back(i == 0 ? -1 : take16((int64_t)W * k.Kp[i]));
+            k.WTt16.push_back(i == 0 ? -1 : take16((int64_t)W * W));
+        }
+        k.WG16 = take16((int64_t)d.NG * W);
+        k.WGT16 = take16((int64_t)W * d.NG);
+        k.WQ16 = take16((int64_t)d.NQ * W);
+        k.WQT16 = take16((int64_t)W * d.NQ);
+        k.Ws2_16 = take16((int64_t)H * H);
+        k.Ws2T16 = take16((int64_t)H * H);
+        k.Ws3_16 = take16((int64_t)H * H);
+        k.Ws3T16 = take16((int64_t)H * H);
+    }
     k.total = off;
     return k;
 }
@@ -159,23 +176,26 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         off += (n + 63) / 64 * 64;
         return o;
     };
+    // activation-sized buffers: fp32, or bf16 (half the floats) in the bf16 MLP
+    auto act = [&](int64_t n) { return d.bf ? take((n + 1) / 2) : take(n); };
     const int W = d.W, H = d.H;
     w.X0 = take(P * d.K0p);
+    w.X0b = d.bf ? act(P * d.K0p) : -1;
     if (save) {
-        for (int i = 0; i < d.L; ++i) w.Hb.push_back(take(P * W));
-        for (int i = 0; i < d.L; ++i) w.Db.push_back(take(P * W));
+        for (int i = 0; i < d.L; ++i) w.Hb.push_back(act(P * W));
+        for (int i = 0; i < d.L; ++i) w.Db.push_back(act(P * W));
     } else {
-        for (int i = 0; i < 3; ++i) w.Hb.push_back(take(P * W));
+        for (int i = 0; i < 3; ++i) w.Hb.push_back(act(P * W));
     }
-    w.G = take(P * d.NG);
-    w.DG = save ? take(P * d.NG) : -1;
-    w.Q = take(P * d.NQ);
-    w.DQ = save ? take(P * d.NQ) : -1;
+    w.G = act(P * d.NG);
+    w.DG = save ? act(P * d.NG) : -1;
+    w.Q = act(P * d.NQ);
+    w.DQ = save ? act(P * d.NQ) : -1;
     if (save) {
-        w.S2 = take(P * H);
-        w.DS2 = take(P * H);
-        w.S3 = take(P * H);
-        w.DS3 = take(P * H);
+        w.S2 = act(P * H);
+        w.DS2 = act(P * H);
+        w.S3 = act(P * H);
+        w.DS3 = act(P * H);
     } else {
         w.S2 = w.S3 = w.DS2 = w.DS3 = -1;  // ping-pong buffers are used
     }
@@ -186,17 +206,17 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
     w.skyh = take(B * H);
     w.sky = take(B * 4);
     if (save) {
-        w.dZG = take(P * d.NG);
-        w.dZQ = take(P * d.NQ);
-        w.dS3 = take(P * H);
-        w.dS2 = take(P * H);
-        w.dZa = take(P * W);
-        w.dZb = take(P * W);
+        w.dZG = act(P * d.NG);
+        w.dZQ = act(P * d.NQ);
+        w.dS3 = act(P * H);
+        w.dS2 = act(P * H);
+        w.dZa = act(P * W);
+        w.dZb = act(P * W);
         w.hpre = take(P * d.HP);
         // largest TN slab over every weight-gradient GEMM of the backward
         int64_t slab = 0, slab_b = 0;
         auto need = [&](int N, int K) {
-            const int sp = tn_splits((int)P, N, K);
+            const int sp = d.bf ? tn_splits_bf16((int)P, N, K) : tn_splits((int)P, N, K);
             slab = std::max(slab, (int64_t)sp * N * K);
             slab_b = std::max(slab_b, (int64_t)sp * N);
         };

@@ -18,6 +18,7 @@ struct Dims {
     int NO;             // outputs per point: 8 + beta + C
     int sem_col;        // first semantic-logit column of `out`
     int HP;             // per-point head pre-gradient row: [dσ, drgb3, dsun, dβ, dsem C]
+    bool bf;            // cfg.dtype == 1: bf16 activations and GEMM operands (layer 0 stays fp32)
 };
 
 int32_t make_dims(const spnerf_model_cfg* cfg, Dims* d);
@@ -41,22 +42,31 @@ struct PIdx {
 
 std::vector<PSpec> param_specs(const Dims& d, PIdx* idx);
 
-// Offsets (floats) inside the packed weight buffer.
-struct Packed {
-    std::vector<int64_t> Wt, bt, WTt;   // trunk: forward [W][Kp_i], bias, transposed h-part [W][W]
-    std::vector<int> Kp;                // padded K of each trunk layer
+// Offsets (floats) inside the packed weight buffer.  PackedOffs is the trivially copyable part
+// handed to kernels; Packed adds the per-layer vectors (host only).
+struct PackedOffs {
     int64_t WG, bG, WGT, WQ, bQ, WQT;
     int64_t Ws2, bs2, Ws2T, Ws3, bs3, Ws3T;
     int64_t wsig, bsig, Wr2, br2, ws4, bs4, Wm2, bm2, wb2, bb2;
     int64_t Wk1, bk1, Wk2, bk2, Wsem0, Wsem4, emb, Wsun, Wtt;
+    // bf16 copies (cfg.dtype == 1), offsets in bf16 elements from the packed base: the G, Q and
+    // sun_v 2/3 matrices (forward and transposed)
+    int64_t WG16 = -1, WGT16 = -1, WQ16 = -1, WQT16 = -1, Ws2_16 = -1, Ws2T16 = -1, Ws3_16 = -1, Ws3T16 = -1;
     int64_t total;
+};
+struct Packed : PackedOffs {
+    std::vector<int64_t> Wt, bt, WTt;   // trunk: forward [W][Kp_i], bias, transposed h-part [W][W]
+    std::vector<int> Kp;                // padded K of each trunk layer
+    std::vector<int64_t> Wt16, WTt16;   // bf16 trunk layers 1.. (bf16 units), -1 for layer 0
 };
 Packed packed_layout(const Dims& d);
 
 // Workspace offsets (floats).  SAVE keeps every activation + derivative for the backward.
+// With Dims::bf the activation / derivative / pre-activation-gradient buffers (Hb, Db, G, DG,
+// Q, DQ, S2, DS2, S3, DS3, dZG, dZQ, dS3, dS2, dZa, dZb, X0b) hold bf16 at the same float offset.
 struct WS {
     int64_t P, B;
-    int64_t X0;
+    int64_t X0, X0b;
     std::vector<int64_t> Hb, Db;        // H_1..H_L (save) or 3 ping-pong buffers; D_1..D_L
     int64_t G, DG, Q, DQ, S2, DS2, S3, DS3, hsave;
     int64_t rb0, rb4, rbQ, skyh, sky;

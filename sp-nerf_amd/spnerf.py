@@ -67,8 +67,16 @@ class SPNeRF(torch.nn.Module):
     """Same constructor and parameters as the reference SPNeRF (spnerf.py:162-271)."""
 
     def __init__(self, num_sem_classes=3, s_embedding_factor=1, layers=8, feat=256, mapping=False,
-                 mapping_sizes=[10, 4], skips=[4], siren=True, t_embedding_dims=16, beta=False, sem=False):
+                 mapping_sizes=[10, 4], skips=[4], siren=True, t_embedding_dims=16, beta=False, sem=False,
+                 precision="fp32"):
         super().__init__()
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        # MLP arithmetic (not a reference argument): "fp32" is the parity path; "bf16" keeps
+        # activations and GEMM operands in bf16 with fp32 accumulation, fp32 layer 0, fp32
+        # parameters and gradients — the counterpart of the reference's fp16 AMP training
+        # (main.py:334-336, precision=16)
+        self.precision = precision
         if not siren:
             raise NotImplementedError("the gfx950 trunk implements the SIREN activations (load_model never "
                                       "disables them, models/__init__.py:6-13)")
@@ -134,7 +142,7 @@ class SPNeRF(torch.nn.Module):
             c.sem_dim = self.semantic_size
             c.beta = 1 if self.beta else 0
             c.t_dim = self.t_embedding_dims if self.beta else 0
-            c.dtype = 0
+            c.dtype = 1 if self.precision == "bf16" else 0
             self._cfg = c
         return self._cfg
 
@@ -180,6 +188,14 @@ class SPNeRF(torch.nn.Module):
                                                      _lib.stream_of(self._packed)), "pack_params")
             self._pack_key = key
         return self._packed
+
+    def set_precision(self, precision: str) -> "SPNeRF":
+        """Switch the MLP arithmetic ("fp32" | "bf16"); parameters are unchanged."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.precision = precision
+        self._cfg, self._packed, self._pack_key = None, None, None
+        return self
 
     def _apply(self, fn, *args, **kwargs):
         self._packed, self._pack_key = None, None

@@ -19,23 +19,23 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def make_model(dims: ModelDims, seed: int):
+def make_model(dims: ModelDims, seed: int, precision: str = "fp32"):
     m = spnerf_amd.SPNeRF(num_sem_classes=dims.num_sem_classes, s_embedding_factor=dims.s_embedding_factor,
                           layers=dims.layers, feat=dims.width, mapping=dims.mapping, t_embedding_dims=dims.t_dim,
-                          beta=dims.beta, sem=dims.sem)
+                          beta=dims.beta, sem=dims.sem, precision=precision)
     m.load_state_dict({k: torch.tensor(v) for k, v in make_weights(dims, seed).items()})
     return m.to(DEV)
 
 
-def run_case(name):
+def run_case(name, precision="fp32"):
     data = gu.load(name)
     meta = data["meta"]
     dims, args = gu.dims_of(meta), gu.args_of(meta)
-    model = make_model(dims, meta["seed"])
+    model = make_model(dims, meta["seed"], precision)
     models = {"coarse": model}
     params = dict(model.named_parameters())
     if args.n_importance > 0:
-        models["fine"] = make_model(dims, meta["seed"] + 100)
+        models["fine"] = make_model(dims, meta["seed"] + 100, precision)
         params.update({"fine." + n: p for n, p in models["fine"].named_parameters()})
     if "in_t_embedding" in data:
         emb = torch.nn.Embedding(*data["in_t_embedding"].shape).to(DEV)

@@ -1,0 +1,198 @@
+// Correctness + timing of the bf16 MFMA GEMMs (tools only; not part of the library ABI).
+//   make -C tools gemm_bench_bf16 && ./tools/gemm_bench_bf16 [P]
+// Every shape is checked against an fp64 host product of the same bf16-rounded operands on a
+// sample of rows / entries; the first block of shapes covers the MLP's edge cases (split A / B
+// segments, N and K not multiples of the 128 tile, P not a multiple of the 64-point step).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../sp-nerf_amd/csrc/gemm_bf16.h"
+#include "../sp-nerf_amd/csrc/gemm_f32.h"
+
+using namespace spn;
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t e = (x);                                                \
+        if (e != hipSuccess) {                                             \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); \
+            exit(1);                                                       \
+        }                                                                  \
+    } while (0)
+
+static float bfr(float x) {  // round to bf16 (RNE), back to float
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+    float y;
+    memcpy(&y, &u, 4);
+    return y;
+}
+
+struct HMat {
+    int rows, cols;
+    std::vector<float> h;  // bf16-rounded values
+    bf16* d = nullptr;
+    HMat(int r, int c, float scale, unsigned seed) : rows(r), cols(c), h((size_t)r * c) {
+        srand(seed);
+        std::vector<uint16_t> raw(h.size());
+        for (size_t i = 0; i < h.size(); ++i) {
+            h[i] = bfr(scale * (2.f * (float)rand() / (float)RAND_MAX - 1.f));
+            uint32_t u;
+            memcpy(&u, &h[i], 4);
+            raw[i] = (uint16_t)(u >> 16);
+        }
+        CK(hipMalloc(&d, raw.size() * 2));
+        CK(hipMemcpy(d, raw.data(), raw.size() * 2, hipMemcpyHostToDevice));
+    }
+    float at(int r, int c) const { return h[(size_t)r * cols + c]; }
+};
+
+static std::vector<float> dl16(const bf16* d, size_t n) {
+    std::vector<uint16_t> raw(n);
+    CK(hipMemcpy(raw.data(), d, n * 2, hipMemcpyDeviceToHost));
+    std::vector<float> f(n);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t u = (uint32_t)raw[i] << 16;
+        memcpy(&f[i], &u, 4);
+    }
+    return f;
+}
+
+template <typename F>
+static double time_it(F f, int iters = 20) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) f();
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < iters; ++i) f();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return 1e3 * ms / iters;  // us
+}
+
+static int fails = 0;
+
+// C[M,N] = sin(A·B^T + bias) (act) or (A·B^T)·Dmul, A = [A1 | A2] split at K1
+static void check_nt(int M, int N, int K, int K1, bool sine, bool timing) {
+    HMat A1(M, K1, 1.f, 1), A2(M, std::max(8, K - K1), 1.f, 2), B(N, K, 0.1f, 3), Dm(M, N, 1.f, 4);
+    std::vector<float> bias(N);
+    for (int i = 0; i < N; ++i) bias[i] = 0.01f * (i % 17);
+    float* dbias;
+    CK(hipMalloc(&dbias, N * 4));
+    CK(hipMemcpy(dbias, bias.data(), N * 4, hipMemcpyHostToDevice));
+    bf16 *C, *D;
+    CK(hipMalloc(&C, (size_t)M * N * 2));
+    CK(hipMalloc(&D, (size_t)M * N * 2));
+    NT16Args g;
+    g.A = A1.d; g.lda = K1; g.A2 = A2.d; g.lda2 = A2.cols; g.K1 = K1;
+    g.B = B.d; g.ldb = K; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K;
+    if (sine) { g.bias = dbias; g.act = 1; g.w0 = 1.f; g.Dout = D; g.ld_dout = N; }
+    else { g.Dmul = Dm.d; g.ld_dmul = N; }
+    if (gemm_nt_bf16(g, 0) != 0) { printf("launch refused\n"); fails++; return; }
+    CK(hipDeviceSynchronize());
+    auto c = dl16(C, (size_t)M * N), dd = dl16(D, (size_t)M * N);
+    double worst = 0, worstd = 0;
+    for (int s = 0; s < 256; ++s) {
+        const int r = (int)((int64_t)s * 7919 % M);
+        for (int n = 0; n < N; ++n) {
+            double acc = 0;
+            for (int k = 0; k < K; ++k) acc += (double)(k < K1 ? A1.at(r, k) : A2.at(r, k - K1)) * B.at(n, k);
+            double ref, refd = 1;
+            if (sine) { ref = std::sin(acc + bias[n]); refd = std::cos(acc + bias[n]); }
+            else ref = acc * Dm.at(r, n);
+            worst = std::max(worst, std::fabs(ref - c[(size_t)r * N + n]));
+            if (sine) worstd = std::max(worstd, std::fabs(refd - dd[(size_t)r * N + n]));
+        }
+    }
+    const bool ok = worst < 2e-2 && worstd < 2e-2;  // bf16 output rounding: |y| <= ~2, ulp 2^-8
+    if (!ok) fails++;
+    printf("nt  M=%-7d N=%-4d K=%-4d K1=%-4d %s  max|err| C %.2e D %.2e  %s", M, N, K, K1, sine ? "sine" : "dmul", worst,
+           worstd, ok ? "ok" : "FAIL");
+    if (timing) {
+        const double us = time_it([&] { gemm_nt_bf16(g, 0); });
+        printf("   %8.1f us %7.1f TF/s", us, 2.0 * M * N * K / us * 1e-6);
+    }
+    printf("\n");
+    CK(hipFree(C)); CK(hipFree(D)); CK(hipFree(dbias));
+}
+
+// dW[n][k] = Σ_p A[p][n] B[p][k], B = [B1 | B2] split at K1; bias[n] = Σ_p A[p][n]
+static void check_tn(int P, int N, int K, int K1, bool timing) {
+    HMat A(P, N, 1.f, 5), B1(P, K1, 1.f, 6), B2(P, std::max(8, K - K1), 1.f, 7);
+    const int sp = tn_splits_bf16(P, N, K);
+    float *slab, *slab_b, *dW, *db;
+    CK(hipMalloc(&slab, (size_t)sp * N * K * 4));
+    CK(hipMalloc(&slab_b, (size_t)sp * N * 4));
+    CK(hipMalloc(&dW, (size_t)N * K * 4));
+    CK(hipMalloc(&db, (size_t)N * 4));
+    TN16Args t;
+    t.A = A.d; t.lda = N; t.B = B1.d; t.ldb = K1; t.B2 = B2.d; t.ldb2 = B2.cols; t.K1 = K1;
+    t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K; t.slab_b = slab_b; t.P = P; t.N = N; t.K = K;
+    ReduceArgs r;
+    r.slab = slab; r.ld_slab = K; r.slab_stride = t.slab_stride; r.splits = sp; r.N = N; r.slab_b = slab_b;
+    r.row0 = 0; r.nrows = N; r.ncols = K; r.dst = dW; r.ld_dst = K; r.dst_b = db;
+    if (gemm_tn_bf16(t, sp, 0) != 0 || reduce_slabs(r, 0) != 0) { printf("launch refused\n"); fails++; return; }
+    CK(hipDeviceSynchronize());
+    std::vector<float> w((size_t)N * K), b(N);
+    CK(hipMemcpy(w.data(), dW, w.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), db, N * 4, hipMemcpyDeviceToHost));
+    double worst = 0, worstb = 0, scale = std::sqrt((double)P);
+    for (int s = 0; s < 1024; ++s) {
+        const int n = (int)((int64_t)s * 131 % N), k = (int)((int64_t)s * 977 % K);
+        double acc = 0;
+        for (int p = 0; p < P; ++p) acc += (double)A.at(p, n) * (k < K1 ? B1.at(p, k) : B2.at(p, k - K1));
+        worst = std::max(worst, std::fabs(acc - w[(size_t)n * K + k]) / scale);
+    }
+    for (int n = 0; n < N; ++n) {
+        double acc = 0;
+        for (int p = 0; p < P; ++p) acc += A.at(p, n);
+        worstb = std::max(worstb, std::fabs(acc - b[n]) / scale);
+    }
+    const bool ok = worst < 1e-4 && worstb < 1e-4;  // fp32 accumulation of exact bf16 products
+    if (!ok) fails++;
+    printf("tn  P=%-7d N=%-4d K=%-4d K1=%-4d splits=%-2d max|err|/sqrt(P) W %.2e b %.2e  %s", P, N, K, K1, sp, worst,
+           worstb, ok ? "ok" : "FAIL");
+    if (timing) {
+        const double us = time_it([&] { gemm_tn_bf16(t, sp, 0); });
+        const double usr = time_it([&] { reduce_slabs(r, 0); });
+        printf("   %8.1f us %7.1f TF/s (+ reduce %.1f us)", us, 2.0 * P * N * K / us * 1e-6, usr);
+    }
+    printf("\n");
+    CK(hipFree(slab)); CK(hipFree(slab_b)); CK(hipFree(dW)); CK(hipFree(db));
+}
+
+int main(int argc, char** argv) {
+    const int P = argc > 1 ? atoi(argv[1]) : 131072;
+    // edge shapes (MLP at W=64 / nomap / skip layer)
+    check_nt(1000, 64, 64, 64, true, false);
+    check_nt(1000, 64, 128, 64, true, false);
+    check_nt(777, 96, 32, 32, false, false);
+    check_nt(4100, 512, 576, 512, true, false);
+    check_nt(4100, 512, 544, 512, true, false);
+    check_tn(1000, 64, 64, 64, false);
+    check_tn(1000, 64, 128, 64, false);
+    check_tn(4100, 512, 576, 512, false);
+    check_tn(2049, 96, 544, 512, false);
+    check_tn(300, 32, 64, 64, false);
+    // C3 shapes
+    check_nt(P, 512, 512, 512, true, true);
+    check_nt(P, 512, 512, 512, false, true);
+    check_nt(P, 512, 576, 512, true, true);
+    check_nt(P, 768, 512, 512, true, true);
+    check_tn(P, 512, 512, 512, true);
+    check_tn(P, 512, 576, 512, true);
+    check_tn(P, 768, 512, 512, true);
+    check_tn(P, 256, 256, 256, true);
+    printf("%s\n", fails ? "SOME CHECKS FAILED" : "all checks ok");
+    return fails ? 1 : 0;
+}
