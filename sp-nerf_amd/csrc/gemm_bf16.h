@@ -36,7 +36,9 @@ struct TN16Args {
     int p_per_split = 0;  // set by gemm_tn_bf16
 };
 
-int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s);
+// variant: prefetch depth in K-steps (1 or 2); <= 0 = library default (g_nt16_variant)
+extern int g_nt16_variant;
+int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);
 int tn_splits_bf16(int P, int N, int K);
 int32_t gemm_tn_bf16(const TN16Args& a, int splits, hipStream_t s);
 

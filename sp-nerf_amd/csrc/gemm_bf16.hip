@@ -10,6 +10,8 @@
 //    an XOR-swizzled LDS image and read back column-wise with ds_read_b64_tr_b16, so no
 //    activation is ever transposed in HBM.  Points are split over blockIdx.y into fp32 slabs
 //    reduced in a fixed order by k_reduce_slabs (deterministic).
+#include <algorithm>
+
 #include "common.h"
 #include "gemm_bf16.h"
 
@@ -40,50 +42,80 @@ __device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
     return u32x4{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
 }
 
+// sin / cos for bf16 outputs: reduce to [-1/2, 1/2] revolutions, then the hardware
+// v_sin_f32 / v_cos_f32 (argument in revolutions).  Absolute error ~1e-6 for |x| < 1e3,
+// far below the bf16 rounding of the result (2^-9 relative).
+__device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
+    float r = x * 0.15915494309189535f;
+    r -= __builtin_rintf(r);
+    *s = __builtin_amdgcn_sinf(r);
+    *c = __builtin_amdgcn_cosf(r);
+}
+
+// order LDS accesses of one wavefront (LDS is in order per wave; this stops the compiler
+// from moving accesses across the point)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ------------------------------------------------------------------------------------------
 // NT
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gemm_nt_bf16(NT16Args g) {
+// Persistent over tiles: block b walks tiles slot(b), slot(b) + G, ... (slot = XCD-aware remap,
+// so the column tiles of a row block run together on one XCD and share its L2).  The first
+// K-step of the next tile is loaded before the current tile's epilogue, so the epilogue's
+// stores overlap the next tile's load latency (two co-resident blocks otherwise run in lockstep
+// and never overlap loop and epilogue).  PF = register prefetch depth in K-steps (1 or 2).
+template <int PF>
+__global__ __launch_bounds__(256) void k_gemm_nt_bf16(NT16Args g, int ntiles) {
     __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * HB * HLK];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nN = (g.N + HB - 1) / HB;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
-    const int bm = (t / nN) * HB, bn = (t % nN) * HB;
+    const int G = gridDim.x;
     const int lr = tid >> 3, lc = (tid & 7) * 8;  // loader: row (+32 i), bf16 column within the K-step
+    int t = xcd_remap(blockIdx.x, G);
+    if (t >= ntiles) return;  // block-uniform
 
-    u32x4 ra[4], rb[4];
-    auto gload = [&](int k0) {
+    // Loads are unconditional (no branch → no per-load vmcnt(0)): rows past M / columns past N
+    // read a clamped row (they only feed output rows / columns that are never stored); the K
+    // tail past K is zeroed when the registers are written to LDS, after the K-step's MFMAs, so
+    // the loads stay in flight across them.  K1 is a multiple of the K-step, so the A / A2
+    // segment is uniform per step.
+    const int lda1 = g.lda, lda2 = g.lda2, K1 = g.K1, Kt = g.K;
+    struct Regs {
+        u32x4 a[4], b[4];
+        bool kin;
+    };
+    auto gload = [&](Regs& r, int tile, int k0) {
+        const int bm = (tile / nN) * HB, bn = (tile % nN) * HB;
         const int k = k0 + lc;
+        r.kin = k < Kt;
+        const int kc = r.kin ? k : Kt - 8;
+        const bool seg2 = k0 >= K1;
+        const bf16* pa = seg2 ? g.A2 + (kc - K1) : g.A + kc;
+        const int lda = seg2 ? lda2 : lda1;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int row = bm + lr + 32 * i;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (row < g.M && k < g.K) v = k < g.K1 ? ldg16(g.A + (int64_t)row * g.lda + k) : ldg16(g.A2 + (int64_t)row * g.lda2 + (k - g.K1));
-            ra[i] = v;
-            const int col = bn + lr + 32 * i;
-            u32x4 w = {0u, 0u, 0u, 0u};
-            if (col < g.N && k < g.K) w = ldg16(g.B + (int64_t)col * g.ldb + k);
-            rb[i] = w;
+            const int row = min(bm + lr + 32 * i, g.M - 1);
+            r.a[i] = ldg16(pa + (int64_t)row * lda);
+            const int col = min(bn + lr + 32 * i, g.N - 1);
+            r.b[i] = ldg16(g.B + (int64_t)col * g.ldb + kc);
         }
     };
-    auto sstore = [&](int stg) {
+    auto sstore = [&](const Regs& r, int stg) {
         bf16* sA = smem + stg * 2 * HB * HLK;
         bf16* sB = sA + HB * HLK;
+        const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            *reinterpret_cast<u32x4*>(sA + (lr + 32 * i) * HLK + lc) = ra[i];
-            *reinterpret_cast<u32x4*>(sB + (lr + 32 * i) * HLK + lc) = rb[i];
+            *reinterpret_cast<u32x4*>(sA + (lr + 32 * i) * HLK + lc) = r.kin ? r.a[i] : z;
+            *reinterpret_cast<u32x4*>(sB + (lr + 32 * i) * HLK + lc) = r.kin ? r.b[i] : z;
         }
     };
 
     f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
     const int wr = wid >> 1, wc = wid & 1, r32 = lane & 31, h = lane >> 5;
     auto compute = [&](int stg) {
         const bf16* sA = smem + stg * 2 * HB * HLK;
@@ -104,76 +136,149 @@ __global__ __launch_bounds__(256) void k_gemm_nt_bf16(NT16Args g) {
         }
     };
 
-    gload(0);
-    sstore(0);
-    __syncthreads();
+    // Epilogue geometry: a wave owns 64 rows x 64 columns, staged 32 rows at a time as a
+    // [32][68] fp32 image in its own LDS slice; lane (lane & 7) owns columns cq..cq+7 of rows
+    // (lane >> 3) + 8 q4, so each store instruction writes 8 full 128-B row segments.
+    const int cq = (lane & 7) * 8;
+    constexpr int SLD = 68;
+    float* stage = reinterpret_cast<float*>(smem) + wid * (32 * SLD);
     const int nk = (g.K + HK - 1) / HK;
-    for (int kt = 0; kt < nk; ++kt) {
-        const bool more = kt + 1 < nk;
-        if (more) gload((kt + 1) * HK);
-        compute(kt & 1);
-        if (more) sstore((kt + 1) & 1);
-        __syncthreads();
-    }
 
-    // Epilogue: each wave stages one 32x32 fp32 sub-tile at a time in LDS; a lane then owns two
-    // 8-column row chunks → 16-B bf16 loads (Dmul) and stores (C, D).
-    float* stage = reinterpret_cast<float*>(smem) + wid * 1024;
+    Regs r0, r1;
+    gload(r0, t, 0);
+    if constexpr (PF == 2) gload(r1, t, min(1, nk - 1) * HK);
+    sstore(r0, 0);
+    __syncthreads();
+    while (true) {
+        const int bm = (t / nN) * HB, bn = (t % nN) * HB;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            __syncthreads();
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + r32] = acc[i][j][r];
-            __syncthreads();
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        // No branch around a load (a join point makes hipcc drain vmcnt(0)): past the last
+        // K-step the loader re-reads the last step (L2 hit, never computed on).
+        if constexpr (PF == 1) {
+            for (int kt = 0; kt < nk; ++kt) {
+                gload(r0, t, min(kt + 1, nk - 1) * HK);
+                __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs
+                compute(kt & 1);
+                __builtin_amdgcn_sched_barrier(0);  // LDS writes (and their vmcnt waits) after the MFMAs
+                sstore(r0, (kt + 1) & 1);
+                __syncthreads();
+            }
+        } else {
+            int kt = 0;
+            for (; kt + 1 < nk; kt += 2) {
+                gload(r0, t, min(kt + 2, nk - 1) * HK);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(0);
+                __builtin_amdgcn_sched_barrier(0);
+                sstore(r1, 1);
+                __syncthreads();
+                gload(r1, t, min(kt + 3, nk - 1) * HK);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(1);
+                __builtin_amdgcn_sched_barrier(0);
+                sstore(r0, 0);
+                __syncthreads();
+            }
+            if (kt < nk) {  // odd step count: the last step sits in stage 0
+                compute(0);
+                __syncthreads();  // the epilogue reuses stage 0
+            }
+        }
+        // next tile: its first K-step(s) load during this tile's epilogue (clamped, unconditional)
+        const int tn = t + G;
+        const bool more = tn < ntiles;
+        const int tl = more ? tn : t;
+        gload(r0, tl, 0);
+        if constexpr (PF == 2) gload(r1, tl, min(1, nk - 1) * HK);
+
+        // ---- epilogue of tile t: all global loads first (vmcnt counts loads and stores in
+        // issue order, so a load issued after a store would wait for the store)
+        const int col = bn + wc * 64 + cq;
+        const bool colok = col < g.N;
+        const int colc = colok ? col : g.N - 8;
+        float bias8[8], r1v8[8];
 #pragma unroll
-            for (int q2 = 0; q2 < 2; ++q2) {
-                const int q = lane + 64 * q2;
-                const int rr = q >> 2, c8 = (q & 3) * 8;
+        for (int e = 0; e < 8; ++e) {
+            bias8[e] = g.bias ? g.bias[colc + e] : 0.f;
+            r1v8[e] = g.r1_a ? g.r1_v[colc + e] : 0.f;
+        }
+        u32x4 dm[2][4];
+        float r1a[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int row = min(bm + wr * 64 + i * 32 + (lane >> 3) + 8 * q4, g.M - 1);
+                dm[i][q4] = g.Dmul ? ldg16(g.Dmul + (int64_t)row * g.ld_dmul + colc) : u32x4{0u, 0u, 0u, 0u};
+                r1a[i][q4] = g.r1_a ? g.r1_a[(int64_t)row * g.r1_lda] : 0.f;
+            }
+        const bool sine_cols = g.act == 1 && col >= g.n_lin;  // n_lin is a multiple of 8
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * h) * SLD + j * 32 + r32] = acc[i][j][r];
+            wave_lds_sync();
+            u32x4 oc[4], od[4];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int rr = (lane >> 3) + 8 * q4;
                 const int row = bm + wr * 64 + i * 32 + rr;
-                const int col = bn + wc * 64 + j * 32 + c8;
-                if (row >= g.M || col >= g.N) continue;
                 float v[8];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = stage[rr * 32 + c8 + e];
-                if (g.bias) {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += g.bias[col + e];
-                }
+                for (int e = 0; e < 8; ++e) v[e] = stage[rr * SLD + cq + e] + bias8[e];
                 if (g.rowbias) {
-                    const float* rb = g.rowbias + (int64_t)(row / g.rows_per_ray) * g.ld_rb + col;
+                    const float* rb = g.rowbias + (int64_t)(min(row, g.M - 1) / g.rows_per_ray) * g.ld_rb + colc;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[e] += rb[e];
                 }
                 if (g.r1_a) {
-                    const float a = g.r1_a[(int64_t)row * g.r1_lda];
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += a * g.r1_v[col + e];
+                    for (int e = 0; e < 8; ++e) v[e] += r1a[i][q4] * r1v8[e];
                 }
-                if (g.act == 1 && col >= g.n_lin) {  // n_lin is a multiple of 8
-                    float d[8];
+                float d[8];
+                if (sine_cols) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         float sn, cs;
-                        sincosf(g.w0 * v[e], &sn, &cs);
+                        fast_sincos(g.w0 * v[e], &sn, &cs);
                         v[e] = sn;
                         d[e] = g.w0 * cs;
                     }
-                    if (g.Dout) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = pack8(d);
-                } else if (g.Dout) {
-                    const uint32_t one = 0x3f803f80u;
-                    *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = u32x4{one, one, one, one};
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) d[e] = 1.f;
                 }
                 if (g.Dmul) {
-                    float dm[8];
-                    unpack8(ldg16(g.Dmul + (int64_t)row * g.ld_dmul + col), dm);
+                    float m[8];
+                    unpack8(dm[i][q4], m);
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] *= dm[e];
+                    for (int e = 0; e < 8; ++e) v[e] *= m[e];
                 }
-                *reinterpret_cast<u32x4*>(g.C + (int64_t)row * g.ldc + col) = pack8(v);
+                oc[q4] = pack8(v);
+                od[q4] = pack8(d);
+            }
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int row = bm + wr * 64 + i * 32 + (lane >> 3) + 8 * q4;
+                if (row < g.M && colok) {
+                    *reinterpret_cast<u32x4*>(g.C + (int64_t)row * g.ldc + col) = oc[q4];
+                    if (g.Dout) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
+                }
             }
         }
+        if (!more) break;  // block-uniform
+        __syncthreads();   // every wave is done with its staging slice
+        sstore(r0, 0);
+        __syncthreads();
+        t = tn;
     }
 }
 
@@ -198,39 +303,43 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
     const int ch = tid & 15, lrow = tid >> 4;  // loader: 8 features (chunk ch), rows lrow + 16 i
     const bool do_bias = g.slab_b != nullptr && k0 == 0;
 
+    // Unconditional loads (see k_gemm_nt_bf16): features past N / K read a clamped column (their
+    // outputs are never stored); points past the split are zeroed, and the bias sums taken, when
+    // the registers are written to LDS, after the step's MFMAs.
     u32x4 ra[4], rb[4];
     float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int nc = min(n0 + 8 * ch, g.N - 8);
+    const int kc = min(k0 + 8 * ch, g.K - 8);
+    const bf16* pb = kc < g.K1 ? g.B + kc : g.B2 + (kc - g.K1);
+    const int ldb = kc < g.K1 ? g.ldb : g.ldb2;
+    const int lda = g.lda;
+    int p_ld = 0;
     auto gload = [&](int p0) {
-        const int n = n0 + 8 * ch, k = k0 + 8 * ch;
+        p_ld = p0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int p = p0 + lrow + 16 * i;
-            u32x4 v = {0u, 0u, 0u, 0u}, w = {0u, 0u, 0u, 0u};
-            if (p < p_end) {
-                if (n < g.N) v = ldg16(g.A + (int64_t)p * g.lda + n);
-                if (k < g.K) w = k < g.K1 ? ldg16(g.B + (int64_t)p * g.ldb + k) : ldg16(g.B2 + (int64_t)p * g.ldb2 + (k - g.K1));
-            }
-            ra[i] = v;
-            rb[i] = w;
-        }
-        if (do_bias) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float f[8];
-                unpack8(ra[i], f);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) bs[e] += f[e];
-            }
+            const int pc = min(p0 + lrow + 16 * i, p_end - 1);
+            ra[i] = ldg16(g.A + (int64_t)pc * lda + nc);
+            rb[i] = ldg16(pb + (int64_t)pc * ldb);
         }
     };
     auto sstore = [&](int stg) {
         char* sA = smem + stg * 2 * 64 * 256;
         char* sB = sA + 64 * 256;
+        const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+            const bool pin = p_ld + lrow + 16 * i < p_end;
+            const u32x4 v = pin ? ra[i] : z;
+            if (do_bias) {
+                float f[8];
+                unpack8(v, f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bs[e] += f[e];
+            }
             const int o = tn_off(lrow + 16 * i, ch);
-            *reinterpret_cast<u32x4*>(sA + o) = ra[i];
-            *reinterpret_cast<u32x4*>(sB + o) = rb[i];
+            *reinterpret_cast<u32x4*>(sA + o) = v;
+            *reinterpret_cast<u32x4*>(sB + o) = pin ? rb[i] : z;
         }
     };
 
@@ -274,18 +383,20 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
         }
     };
 
-    if (p_beg < p_end) {
+    if (p_beg < p_end) {  // block-uniform
+        const int ns = (p_end - p_beg + 63) / 64;
         gload(p_beg);
         sstore(0);
         __syncthreads();
-        int stg = 0;
-        for (int p0 = p_beg; p0 < p_end; p0 += 64) {
-            const bool more = p0 + 64 < p_end;
-            if (more) gload(p0 + 64);
-            compute(stg);
-            if (more) sstore(stg ^ 1);
+        for (int st = 0; st < ns; ++st) {
+            // unconditional (no branch around a load): past the split the addresses clamp and
+            // sstore zeroes the rows
+            gload(p_beg + 64 * (st + 1));
+            __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs
+            compute(st & 1);
+            __builtin_amdgcn_sched_barrier(0);  // LDS writes (and their vmcnt waits) after the MFMAs
+            sstore((st + 1) & 1);
             __syncthreads();
-            stg ^= 1;
         }
     }
 
@@ -320,7 +431,9 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
-int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s) {
+int g_nt16_variant = 3;
+
+int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt_bf16: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
     SPN_ARG(a.K % 8 == 0 && a.N % 8 == 0 && a.n_lin % 8 == 0, "gemm_nt_bf16: K, N, n_lin must be multiples of 8");
     SPN_ARG(a.K1 <= a.K && (a.K1 == a.K || (a.A2 != nullptr && a.K1 % HK == 0)),
@@ -329,12 +442,18 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s) {
             "gemm_nt_bf16: leading dims must be multiples of 8");
     SPN_ARG(!a.Dout || a.ld_dout % 8 == 0, "gemm_nt_bf16: ld_dout");
     SPN_ARG(!a.Dmul || a.ld_dmul % 8 == 0, "gemm_nt_bf16: ld_dmul");
-    SPN_ARG(a.rowbias == nullptr || a.rows_per_ray > 0, "gemm_nt_bf16: rows_per_ray");
+    SPN_ARG(a.rowbias == nullptr || (a.rows_per_ray > 0 && a.ld_rb % 4 == 0), "gemm_nt_bf16: rowbias");
     if (a.M == 0) return SPNERF_OK;
-    const int nb = cdiv(a.M, HB) * cdiv(a.N, HB);
+    const int ntiles = cdiv(a.M, HB) * cdiv(a.N, HB);
     ProfScope prof("gemm_nt_bf16", s, 2.0 * a.M * a.N * a.K,
                    2.0 * ((double)a.M * a.K + (double)a.N * a.K + (2.0 + (a.Dmul ? 1 : 0)) * a.M * a.N));
-    hipLaunchKernelGGL(k_gemm_nt_bf16, dim3(nb), dim3(256), 0, s, a);
+    // variants: 1 / 2 = one block per tile, prefetch depth 1 / 2; 3 / 4 = persistent grid of
+    // two blocks per CU (the LDS limit), depth 1 / 2
+    const int v = variant > 0 ? variant : g_nt16_variant;
+    const int resident = 2 * 256;
+    const int grid = v >= 3 ? std::min(ntiles, resident) : ntiles;
+    if (v == 1 || v == 3) hipLaunchKernelGGL(k_gemm_nt_bf16<1>, dim3(grid), dim3(256), 0, s, a, ntiles);
+    else hipLaunchKernelGGL(k_gemm_nt_bf16<2>, dim3(grid), dim3(256), 0, s, a, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -65,8 +65,10 @@ static std::vector<float> dl16(const bf16* d, size_t n) {
     return f;
 }
 
+static int g_iters = 20;
+
 template <typename F>
-static double time_it(F f, int iters = 20) {
+static double time_it(F f, int iters = g_iters) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
@@ -98,7 +100,9 @@ static void check_nt(int M, int N, int K, int K1, bool sine, bool timing) {
     g.B = B.d; g.ldb = K; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K;
     if (sine) { g.bias = dbias; g.act = 1; g.w0 = 1.f; g.Dout = D; g.ld_dout = N; }
     else { g.Dmul = Dm.d; g.ld_dmul = N; }
-    if (gemm_nt_bf16(g, 0) != 0) { printf("launch refused\n"); fails++; return; }
+    for (int v = 1; v <= 4; ++v) {
+    CK(hipMemset(C, 0, (size_t)M * N * 2));
+    if (gemm_nt_bf16(g, 0, v) != 0) { printf("launch refused\n"); fails++; return; }
     CK(hipDeviceSynchronize());
     auto c = dl16(C, (size_t)M * N), dd = dl16(D, (size_t)M * N);
     double worst = 0, worstd = 0;
@@ -116,13 +120,14 @@ static void check_nt(int M, int N, int K, int K1, bool sine, bool timing) {
     }
     const bool ok = worst < 2e-2 && worstd < 2e-2;  // bf16 output rounding: |y| <= ~2, ulp 2^-8
     if (!ok) fails++;
-    printf("nt  M=%-7d N=%-4d K=%-4d K1=%-4d %s  max|err| C %.2e D %.2e  %s", M, N, K, K1, sine ? "sine" : "dmul", worst,
+    printf("nt%d M=%-7d N=%-4d K=%-4d K1=%-4d %s  max|err| C %.2e D %.2e  %s", v, M, N, K, K1, sine ? "sine" : "dmul", worst,
            worstd, ok ? "ok" : "FAIL");
     if (timing) {
-        const double us = time_it([&] { gemm_nt_bf16(g, 0); });
+        const double us = time_it([&] { gemm_nt_bf16(g, 0, v); });
         printf("   %8.1f us %7.1f TF/s", us, 2.0 * M * N * K / us * 1e-6);
     }
     printf("\n");
+    }
     CK(hipFree(C)); CK(hipFree(D)); CK(hipFree(dbias));
 }
 
@@ -173,6 +178,7 @@ static void check_tn(int P, int N, int K, int K1, bool timing) {
 
 int main(int argc, char** argv) {
     const int P = argc > 1 ? atoi(argv[1]) : 131072;
+    if (argc > 2) g_iters = atoi(argv[2]);
     // edge shapes (MLP at W=64 / nomap / skip layer)
     check_nt(1000, 64, 64, 64, true, false);
     check_nt(1000, 64, 128, 64, true, false);
@@ -189,6 +195,26 @@ int main(int argc, char** argv) {
     check_nt(P, 512, 512, 512, false, true);
     check_nt(P, 512, 576, 512, true, true);
     check_nt(P, 768, 512, 512, true, true);
+    {   // timing-only ablations of the NT kernel (outputs not checked)
+        HMat A(P, 512, 1.f, 1), B(512, 512, 0.1f, 3);
+        bf16 *C, *D;
+        CK(hipMalloc(&C, (size_t)P * 512 * 2));
+        CK(hipMalloc(&D, (size_t)P * 512 * 2));
+        std::vector<float> bias(512, 0.01f);
+        float* dbias;
+        CK(hipMalloc(&dbias, 512 * 4));
+        CK(hipMemcpy(dbias, bias.data(), 512 * 4, hipMemcpyHostToDevice));
+        NT16Args g;
+        g.A = A.d; g.lda = 512; g.K1 = 512; g.B = B.d; g.ldb = 512; g.C = C; g.ldc = 512; g.M = P; g.N = 512; g.K = 512;
+        g.bias = dbias; g.act = 1; g.Dout = D; g.ld_dout = 512;
+        const char* names[] = {"PF1 tile-per-block", "PF2 tile-per-block", "PF1 persistent", "PF2 persistent"};
+        const int vs[] = {1, 2, 3, 4};
+        for (int i = 0; i < 4; ++i) {
+            const double us = time_it([&] { gemm_nt_bf16(g, 0, vs[i]); });
+            printf("variant %-20s %8.1f us %7.1f TF/s\n", names[i], us, 2.0 * P * 512 * 512 / us * 1e-6);
+        }
+        CK(hipFree(C)); CK(hipFree(D));
+    }
     check_tn(P, 512, 512, 512, true);
     check_tn(P, 512, 576, 512, true);
     check_tn(P, 768, 512, 512, true);
