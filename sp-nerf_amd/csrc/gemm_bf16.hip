@@ -19,46 +19,8 @@ namespace spn {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int HB = 128, HK = 64, HLK = HK + 8;  // NT LDS row: 72 bf16 = 144 B
-
-__device__ __forceinline__ u32x4 ldg16(const bf16* p) { return *reinterpret_cast<const u32x4*>(p); }
-
-__device__ __forceinline__ void unpack8(u32x4 v, float (&f)[8]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        f[2 * i] = __uint_as_float(v[i] << 16);
-        f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
-    }
-}
-
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-    const __bf16 a = (__bf16)lo, b = (__bf16)hi;
-    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
-}
-
-__device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
-    return u32x4{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
-}
-
-// sin / cos for bf16 outputs: reduce to [-1/2, 1/2] revolutions, then the hardware
-// v_sin_f32 / v_cos_f32 (argument in revolutions).  Absolute error ~1e-6 for |x| < 1e3,
-// far below the bf16 rounding of the result (2^-9 relative).
-__device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
-    float r = x * 0.15915494309189535f;
-    r -= __builtin_rintf(r);
-    *s = __builtin_amdgcn_sinf(r);
-    *c = __builtin_amdgcn_cosf(r);
-}
-
-// order LDS accesses of one wavefront (LDS is in order per wave; this stops the compiler
-// from moving accesses across the point)
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // ------------------------------------------------------------------------------------------
 // NT

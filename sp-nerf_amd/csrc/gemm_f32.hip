@@ -33,21 +33,21 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
     const int lr = tid / (KS / 4), lk = (tid % (KS / 4)) * 4;
     constexpr int RSTEP = 256 / (KS / 4);         // rows covered by one pass of the block
 
+    // Unconditional loads (a branch around a load makes hipcc drain vmcnt(0) in the K-loop):
+    // rows past M / columns past N read a clamped row; they only feed outputs never stored.
+    // K and K1 are multiples of KS, so the A / A2 segment is uniform per K-step.
+    const int lda1 = g.lda, lda2 = g.lda2, K1 = g.K1;
     f32x4 ra[NLD], rb[NLD];
     auto gload = [&](int k0) {
+        const bool seg2 = k0 >= K1;
+        const float* pa = seg2 ? g.A2 + (k0 - K1) + lk : g.A + k0 + lk;
+        const int lda = seg2 ? lda2 : lda1;
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
-            const int row = bm + lr + RSTEP * i;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (row < g.M) {
-                if (k0 < g.K1) v = ld4(g.A + (int64_t)row * g.lda + k0 + lk);
-                else v = ld4(g.A2 + (int64_t)row * g.lda2 + (k0 - g.K1) + lk);
-            }
-            ra[i] = v;
-            const int col = bn + lr + RSTEP * i;
-            f32x4 w = {0.f, 0.f, 0.f, 0.f};
-            if (col < g.N) w = ld4(g.B + (int64_t)col * g.ldb + k0 + lk);
-            rb[i] = w;
+            const int row = min(bm + lr + RSTEP * i, g.M - 1);
+            ra[i] = ld4(pa + (int64_t)row * lda);
+            const int col = min(bn + lr + RSTEP * i, g.N - 1);
+            rb[i] = ld4(g.B + (int64_t)col * g.ldb + k0 + lk);
         }
     };
     auto sstore = [&](int stg) {
@@ -100,12 +100,15 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
             compute(0);
         }
     } else {
+        // past the last step the loader re-reads it (L2 hit, never computed on): no branch
         sstore(0);
         __syncthreads();
         for (int kt = 0; kt < nk; ++kt) {
-            if (kt + 1 < nk) gload((kt + 1) * KS);
+            gload(min(kt + 1, nk - 1) * KS);
+            __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs
             compute(kt & 1);
-            if (kt + 1 < nk) sstore((kt + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);  // LDS writes (and their vmcnt waits) after them
+            sstore((kt + 1) & 1);
             __syncthreads();
         }
     }
@@ -143,6 +146,63 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
                     if (g.r1_a) v += r1[r] * r1v;
                     if (g.Dout) g.Dout[(int64_t)row * g.ld_dout + col] = 1.f;
                     g.C[(int64_t)row * g.ldc + col] = g.Dmul ? v * dm[r] : v;
+                }
+            }
+        }
+        return;
+    }
+    if (g.C16) {
+        // bf16 outputs (layer 0 of the bf16 MLP, sine epilogue only): as k_gemm_nt_bf16 — a
+        // wave stages 32 x 64 of its tile at a time, a lane owns 8 consecutive columns of rows
+        // (lane >> 3) + 8 q4, so every store is a full 128-B row segment; hardware sin/cos
+        // after range reduction (|w0 v| ~ 1e2 → ~1e-5 absolute, below bf16 rounding).
+        __syncthreads();  // every wave is done with the K-loop's LDS stages
+        constexpr int SLD = 68;
+        float* st = smem + wid * (32 * SLD);
+        const int cq = (lane & 7) * 8;
+        const int col = bn + wc * 64 + cq;
+        const bool colok = col < g.N;
+        const int colc = colok ? col : g.N - 8;
+        float bias8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bias8[e] = g.bias ? g.bias[colc + e] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) st[((r & 3) + 8 * (r >> 2) + 4 * h) * SLD + j * 32 + r32] = acc[i][j][r];
+            wave_lds_sync();
+            u32x4 oc[4], od[4];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int rr = (lane >> 3) + 8 * q4;
+                const int row = bm + wr * 64 + i * 32 + rr;
+                float v[8], d[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = st[rr * SLD + cq + e] + bias8[e];
+                if (g.rowbias) {
+                    const float* rb = g.rowbias + (int64_t)(min(row, g.M - 1) / g.rows_per_ray) * g.ld_rb + colc;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += rb[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float sn, cs;
+                    fast_sincos(g.w0 * v[e], &sn, &cs);
+                    v[e] = sn;
+                    d[e] = g.w0 * cs;
+                }
+                oc[q4] = pack8(v);
+                od[q4] = pack8(d);
+            }
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int row = bm + wr * 64 + i * 32 + (lane >> 3) + 8 * q4;
+                if (row < g.M && colok) {
+                    *reinterpret_cast<u32x4*>(g.C16 + (int64_t)row * g.ldc + col) = oc[q4];
+                    if (g.D16) *reinterpret_cast<u32x4*>(g.D16 + (int64_t)row * g.ld_dout + col) = od[q4];
                 }
             }
         }
@@ -206,31 +266,33 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
     const int p_end = min(g.P, p_beg + g.p_per_split);
     const int lr = tid >> 5, lc = (tid & 31) * 4;
 
+    // Unconditional loads (see k_gemm_nt): features past N / K read a clamped column (outputs
+    // never stored); points past the split are zeroed at the LDS write, after the MFMAs.
     f32x4 ra[4], rb[4];
+    const int nc = min(n0 + lc, g.N - 4);
+    const int kc = min(k0 + lc, g.K - 4);
+    const float* pb = kc < g.K1 ? g.B + kc : g.B2 + (kc - g.K1);
+    const int ldb = kc < g.K1 ? g.ldb : g.ldb2;
+    const int lda = g.lda;
+    int p_ld = 0;
     auto gload = [&](int p0) {
+        p_ld = p0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int p = p0 + lr + 8 * i;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
-            if (p < p_end) {
-                if (n0 + lc < g.N) v = ld4(g.A + (int64_t)p * g.lda + n0 + lc);
-                const int k = k0 + lc;
-                if (k < g.K) {
-                    if (k < g.K1) w = ld4(g.B + (int64_t)p * g.ldb + k);
-                    else w = ld4(g.B2 + (int64_t)p * g.ldb2 + (k - g.K1));
-                }
-            }
-            ra[i] = v;
-            rb[i] = w;
+            const int pc = min(p0 + lr + 8 * i, p_end - 1);
+            ra[i] = ld4(g.A + (int64_t)pc * lda + nc);
+            rb[i] = ld4(pb + (int64_t)pc * ldb);
         }
     };
     auto sstore = [&](int stg) {
         float* sA = smem + stg * 2 * BK * LDN;
         float* sB = sA + BK * LDN;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            *reinterpret_cast<f32x4*>(sA + (lr + 8 * i) * LDN + lc) = ra[i];
-            *reinterpret_cast<f32x4*>(sB + (lr + 8 * i) * LDN + lc) = rb[i];
+            const bool pin = p_ld + lr + 8 * i < p_end;
+            *reinterpret_cast<f32x4*>(sA + (lr + 8 * i) * LDN + lc) = pin ? ra[i] : z;
+            *reinterpret_cast<f32x4*>(sB + (lr + 8 * i) * LDN + lc) = pin ? rb[i] : z;
         }
     };
 
@@ -276,15 +338,16 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
             if (p0 + BK < p_end) gload(p0 + BK);
             compute(0);
         }
-    } else if (p_beg < p_end) {
+    } else if (p_beg < p_end) {  // block-uniform
         sstore(0);
         __syncthreads();
         int stg = 0;
         for (int p0 = p_beg; p0 < p_end; p0 += BK) {
-            const bool more = p0 + BK < p_end;
-            if (more) gload(p0 + BK);
+            gload(p0 + BK);  // unconditional: past the split the rows clamp and are zeroed
+            __builtin_amdgcn_sched_barrier(0);
             compute(stg);
-            if (more) sstore(stg ^ 1);
+            __builtin_amdgcn_sched_barrier(0);
+            sstore(stg ^ 1);
             __syncthreads();
             stg ^= 1;
         }
@@ -411,7 +474,9 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     SPN_ARG(a.K1 == a.K || a.A2 != nullptr, "gemm_nt: second A segment missing");
     SPN_ARG(a.lda % 4 == 0 && a.ldb % 4 == 0 && (a.K1 == a.K || a.lda2 % 4 == 0), "gemm_nt: leading dims must be /4");
     SPN_ARG(a.rowbias == nullptr || a.rows_per_ray > 0, "gemm_nt: rows_per_ray");
-    SPN_ARG(a.C16 == nullptr || (a.act == 1 && a.n_lin == 0 && a.Dmul == nullptr), "gemm_nt: bf16 output needs the sine epilogue");
+    SPN_ARG(a.C16 == nullptr || (a.act == 1 && a.n_lin == 0 && a.Dmul == nullptr && a.r1_a == nullptr && a.N % 8 == 0 &&
+                                 a.ldc % 8 == 0 && a.ld_dout % 8 == 0),
+            "gemm_nt: bf16 output needs the sine epilogue and 8-aligned N / ldc / ld_dout");
     if (a.M == 0) return SPNERF_OK;
     const int nb = cdiv(a.M, BM) * cdiv(a.N, BN);
     ProfScope prof("gemm_nt_f32", s, 2.0 * a.M * a.N * a.K, 4.0 * ((double)a.M * a.K + (double)a.N * a.K + 2.0 * a.M * a.N));

@@ -314,6 +314,40 @@ __global__ void k_ray_rowsum(const T* __restrict__ in, int ld, int c0, int N, in
     out[ray * ldo + n] = s;
 }
 
+// Same sum for bf16 rows with N, ld, c0 multiples of 8: one block per ray, a thread owns 8
+// columns (16-B loads) in one of 256/(N/8) row phases; phases combined in a fixed order.
+__global__ __launch_bounds__(256) void k_ray_rowsum16(const bf16* __restrict__ in, int ld, int c0, int N, int S,
+                                                      float* __restrict__ out, int ldo) {
+    __shared__ float part[256 * 8];
+    const int64_t ray = blockIdx.x;
+    const int nq = N >> 3;                   // column chunks (<= 256)
+    const int ph = threadIdx.x / nq, q = threadIdx.x % nq;
+    const int nph = 256 / nq;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ph < nph) {
+        const bf16* p = in + ray * S * (int64_t)ld + c0 + 8 * q;
+        for (int i = ph; i < S; i += nph) {
+            float f[8];
+            unpack8(ldg16(p + (int64_t)i * ld), f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += f[e];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[threadIdx.x * 8 + e] = acc[e];
+    __syncthreads();
+    if (threadIdx.x < nq) {
+        float r[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[e] = part[threadIdx.x * 8 + e];
+        for (int k = 1; k < nph; ++k)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] += part[(k * nq + threadIdx.x) * 8 + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) out[ray * ldo + 8 * threadIdx.x + e] = r[e];
+    }
+}
+
 struct RayBwdArgs {
     const float* packed; PackedOffs k; Dims d;
     const float *sky, *skyh, *dsky, *R0, *R4, *RQ;
@@ -381,16 +415,22 @@ __global__ __launch_bounds__(256) void k_ray_bwd(RayBwdArgs a) {
 
 // d_emb[c][j] = Σ_{rays with label c} gemb[ray][j]; the padding row (−100 → C) gets none
 // (nn.Embedding padding_idx, spnerf.py:191-194).
-__global__ void k_class_sum(int64_t B, const float* __restrict__ gemb, int sd, const int64_t* __restrict__ labels,
-                            int C, float* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (C + 1) * sd) return;
-    const int c = i / sd, j = i % sd;
+// One block per (class, j): rays strided over 256 threads, then a fixed-order tree in LDS.
+__global__ __launch_bounds__(256) void k_class_sum(int64_t B, const float* __restrict__ gemb, int sd,
+                                                   const int64_t* __restrict__ labels, int C, float* __restrict__ out) {
+    __shared__ float red[256];
+    const int c = blockIdx.x / sd, j = blockIdx.x % sd;
     float s = 0.f;
     if (c < C)
-        for (int64_t r = 0; r < B; ++r)
+        for (int64_t r = threadIdx.x; r < B; r += 256)
             if (labels[r] == c) s += gemb[r * sd + j];
-    out[i] = s;
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -739,6 +779,21 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
     return SPNERF_OK;
 }
 
+// per-ray sums of a point-major buffer (see k_ray_rowsum)
+template <typename T>
+static int32_t ray_rowsum(const T* in, int ld, int c0, int N, int S, int64_t n_rays, float* out, int ldo, hipStream_t s) {
+    if constexpr (std::is_same<T, bf16>::value) {
+        if (N % 8 == 0 && N <= 2048 && ld % 8 == 0 && c0 % 8 == 0) {
+            hipLaunchKernelGGL(k_ray_rowsum16, dim3((unsigned)n_rays), dim3(256), 0, s, in, ld, c0, N, S, out, ldo);
+            SPN_HIP(hipGetLastError());
+            return SPNERF_OK;
+        }
+    }
+    hipLaunchKernelGGL(k_ray_rowsum<T>, dim3(cdiv(N, 256), (unsigned)n_rays), dim3(256), 0, s, in, ld, c0, N, S, out, ldo);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
 // Backward of the per-point network (steps 1-6): narrow heads, head / sun_v / feat / trunk
 // weight gradients (split-P TN GEMMs + fixed-order slab reduction), dX GEMMs with the saved
 // sin' as Dmul, and the per-ray sums R0 / R4 / RQ feeding the per-ray parameters.
@@ -815,9 +870,7 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
             SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
         }
         // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns
-        hipLaunchKernelGGL(k_ray_rowsum<T>, dim3(cdiv(NQ, 256), (unsigned)n_rays), dim3(256), 0, s, dZQ, d.NQ, 0, NQ, S,
-                           c.at(c.w.RQ), d.NQ);
-        SPN_HIP(hipGetLastError());
+        SPN_TRY(ray_rowsum<T>(dZQ, d.NQ, 0, NQ, S, n_rays, c.at(c.w.RQ), d.NQ, s));
     }
     // 5. H_L: dH_L = dZ_G · WG + dσ ⊗ w_σ ;  dZ_{L-1} = dH_L ⊙ D_L ;  dWG = dZ_G^T · H_L
     const int NG = mode == 0 ? d.NG : W;
@@ -850,9 +903,7 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
             SPN_TRY(tn_grad<T>(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
         if (d.sem && (i == 0 || i == d.skip)) {
-            hipLaunchKernelGGL(k_ray_rowsum<T>, dim3(cdiv(W, 256), (unsigned)n_rays), dim3(256), 0, s, dZ, W, 0, W, S,
-                               c.at(i == 0 ? c.w.R0 : c.w.R4), W);
-            SPN_HIP(hipGetLastError());
+            SPN_TRY(ray_rowsum<T>(dZ, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s));
         }
         if (i > 0) {
             NT g;
@@ -913,8 +964,8 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
                            nullptr, nullptr, s));
             SPN_TRY(skinny(c, B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R4), W, W, gp(x.fcW[d.skip]) + W + d.K0,
                            ld(x.fcW[d.skip]), 1, nullptr, nullptr, s));
-            hipLaunchKernelGGL(k_class_sum, dim3(cdiv((d.C + 1) * d.sd, 64)), dim3(64), 0, s, n_rays, c.at(c.w.gemb),
-                               d.sd, labels, d.C, gp(x.emb));
+            hipLaunchKernelGGL(k_class_sum, dim3((d.C + 1) * d.sd), dim3(256), 0, s, n_rays, c.at(c.w.gemb), d.sd, labels,
+                               d.C, gp(x.emb));
             SPN_HIP(hipGetLastError());
         }
     }
