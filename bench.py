@@ -166,8 +166,8 @@ def main():
         if dloss is not None:
             loss = loss + dloss(res, R["depths"][idx, 0], R["depths"][idx, 1], R["valid_depth"][idx], R["depth_std"][idx])[0]
         if semloss is not None:
-            scale = dp.ce_scale(sem, R["sems"][gidx], world) if world > 1 else 1.0
-            loss = loss + scale * semloss(res, sem)[0]
+            sl = semloss(res, sem)[0]
+            loss = loss + (dp.shard_ce(sl, sem, R["sems"][gidx], world) if world > 1 else sl)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         dp.allreduce_grads(params, world)

@@ -74,8 +74,18 @@ def allreduce_grads(params, world: int, group=None):
             p.grad.copy_(g)
 
 
-def ce_scale(local_labels: torch.Tensor, global_labels: torch.Tensor, world: int) -> float:
-    """Factor turning the local ignore_index mean CE into its share of the global mean."""
-    lv = int((local_labels != -100).sum())
-    gv = int((global_labels != -100).sum())
-    return 0.0 if gv == 0 else world * lv / gv
+def ce_scale(local_labels: torch.Tensor, global_labels: torch.Tensor, world: int) -> torch.Tensor:
+    """Factor turning the local ignore_index mean CE into its share of the global mean
+    (metrics.py:166 does not decompose over shards; SURVEY §8e pitfall 2).  A 0-d tensor on
+    the labels' device — no host sync."""
+    lv = (local_labels != -100).sum().to(torch.float32)
+    gv = (global_labels != -100).sum().to(torch.float32)
+    return torch.where(gv > 0, world * lv / gv.clamp_min(1.0), torch.zeros_like(gv))
+
+
+def shard_ce(ce_local: torch.Tensor, local_labels: torch.Tensor, global_labels: torch.Tensor, world: int) -> torch.Tensor:
+    """``ce_scale · ce_local`` with a shard that holds no valid label contributing 0 (its local
+    ignore_index mean is NaN) — the term each rank adds to its loss before the gradient
+    all-reduce averages over ranks."""
+    scale = ce_scale(local_labels, global_labels, world)
+    return torch.where(scale > 0, scale * torch.nan_to_num(ce_local), torch.zeros_like(ce_local))

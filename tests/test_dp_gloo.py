@@ -114,3 +114,19 @@ def test_cross_entropy_rescale_recovers_global_mean():
         sl = slice(10 * r, 10 * r + 10)
         parts.append(dp.ce_scale(labels[sl], labels, 4) * ce(logits[sl], labels[sl]))
     np.testing.assert_allclose(float(sum(parts) / 4), float(glob), rtol=1e-6)
+
+
+def test_shard_ce_handles_a_shard_without_labels():
+    """A rank whose slice is all ignore_index (local CE = NaN) contributes 0, and the shards
+    still recover the global mean; the scale stays on the device (no host sync)."""
+    torch.manual_seed(1)
+    logits = torch.randn(40, 3)
+    labels = torch.randint(0, 3, (40,))
+    labels[:10] = -100                      # shard 0 has no valid label
+    ce = torch.nn.CrossEntropyLoss(ignore_index=-100)
+    glob = ce(logits, labels)
+    parts = [dp.shard_ce(ce(logits[10 * r:10 * r + 10], labels[10 * r:10 * r + 10]), labels[10 * r:10 * r + 10],
+                         labels, 4) for r in range(4)]
+    assert torch.is_tensor(dp.ce_scale(labels[:10], labels, 4))
+    assert torch.isfinite(parts[0]) and float(parts[0]) == 0.0
+    np.testing.assert_allclose(float(sum(parts) / 4), float(glob), rtol=1e-6)
