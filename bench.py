@@ -129,6 +129,10 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="replay render+loss+backward as a HIP graph (default)")
+    ap.add_argument("--eager", dest="graph", action="store_false", help="launch every kernel from Python")
+    ap.add_argument("--prof-steps", type=int, default=3, help="eager steps timed per kernel in graph mode")
     a = ap.parse_args()
 
     rank, local, world = dp.init_from_env("nccl")
@@ -153,13 +157,24 @@ def main():
     semloss = SemanticLoss(lambda_ss=1.0) if c["sem"] else None
     s_final = c["n_samples"] * (2 if c["guided"] else 1)
 
-    def step():
+    # Batch indices live in static buffers so that the captured step reads each new batch.
+    idx_s = torch.empty(B, dtype=torch.int64, device=dev)
+    gidx_s = torch.empty(B * world, dtype=torch.int64, device=dev)
+
+    def load_batch():
         gidx, idx = sampler.next()
+        gidx_s.copy_(gidx)
+        idx_s.copy_(idx)
+
+    def fwd_bwd():
+        """render + losses + backward for the batch in idx_s / gidx_s (grads are written, not
+        accumulated: the caller clears them before an eager call)."""
+        idx, gidx = idx_s, gidx_s
         rays = R["rays"][idx]
         kw = {}
         if c["guided"]:
             kw = dict(valid_depth=R["valid_depth"][idx], target_depths=R["depths"][idx], target_std=R["depth_std"][idx],
-                      clamp_near_far=R["rays"][gidx[0], 6:8])
+                      clamp_near_far=R["rays"].index_select(0, gidx[:1])[0, 6:8])
         sem = R["sems"][idx] if c["sem"] else None
         res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="train", **kw)
         loss, _ = sloss(res, R["rgbs"][idx])
@@ -168,20 +183,62 @@ def main():
         if semloss is not None:
             sl = semloss(res, sem)[0]
             loss = loss + (dp.shard_ce(sl, sem, R["sems"][gidx], world) if world > 1 else sl)
-        opt.zero_grad(set_to_none=True)
         loss.backward()
-        dp.allreduce_grads(params, world)
-        opt.step()
-        args.noise_std *= 0.9          # main.py:155
         return loss
 
-    for _ in range(a.warmup):
-        step()
+    def finish():
+        dp.allreduce_grads(params, world)   # one RCCL all-reduce of the flat gradient (N > 1)
+        opt.step()
+        args.noise_std *= 0.9               # main.py:155
+
+    def eager_step():
+        load_batch()
+        opt.zero_grad(set_to_none=True)
+        loss = fwd_bwd()
+        finish()
+        return loss
+
+    graph = None
+    if a.graph:
+        # HIP graph of render + losses + backward (≈400 launches, incl. the weight re-pack);
+        # the all-reduce and the fused Adam step stay eager.  Warm up on a side stream, then
+        # capture once; replays overwrite the same gradient tensors.
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, a.warmup)):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        opt.zero_grad(set_to_none=True)
+        model.invalidate_packed()           # the capture must contain the weight re-pack
+        load_batch()
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_loss = fwd_bwd()
+        except Exception as e:  # capture refused: run the same work eagerly, and say so
+            print(f"bench: HIP graph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
+            graph = None
+            a.graph = False
+            torch.cuda.synchronize()
+
+    if graph is not None:
+        def step():
+            load_batch()
+            graph.replay()
+            finish()
+            return static_loss
+    else:
+        step = eager_step
+        for _ in range(a.warmup):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    _lib.prof_reset()
-    _lib.prof_enable(True)
+    if not a.graph:
+        _lib.prof_reset()
+        _lib.prof_enable(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -190,18 +247,29 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    _lib.prof_enable(False)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
+    final_loss = float(loss.item())
+    prof_steps = a.steps
+    if a.graph:
+        # library kernels inside a graph replay carry no events: time them over eager steps
+        # of the same workload right after the timed region (same kernels, same shapes)
+        prof_steps = max(1, a.prof_steps)
+        _lib.prof_reset()
+        _lib.prof_enable(True)
+        for _ in range(prof_steps):
+            eager_step()
+        torch.cuda.synchronize()
+    _lib.prof_enable(False)
 
     kernels = {}
     for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "tn_skinny", "encode", "heads_fwd",
               "heads_bwd", "composite_fwd", "composite_bwd", "sample_guided"):
         s = _lib.prof_read(k)
         if s["launches"]:
-            kernels[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / a.steps,
+            kernels[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / prof_steps,
                           "avg_us": 1e3 * s["ms"] / s["launches"],
                           "tflops": s["flop"] / (s["ms"] * 1e-3) / 1e12 if s["flop"] else None,
                           "gbs": s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["bytes"] else None}
@@ -229,9 +297,11 @@ def main():
         "roofline": {"bound": "mfma", "kernel": f"{dom} ({dom_name})", "achieved": achieved,
                      "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": None, "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
-        "mlp_gemms": gemm_totals(a.steps),
+        "mlp_gemms": gemm_totals(prof_steps),
         "kernels": kernels,
-        "final_loss": float(loss.item()),
+        "final_loss": final_loss,
+        "execution": ("hip graph of render+loss+backward per step, eager all-reduce + fused Adam; kernel timings "
+                      f"from {prof_steps} eager steps right after the timed region") if a.graph else "eager",
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)

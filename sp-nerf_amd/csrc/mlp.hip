@@ -779,6 +779,20 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
     return SPNERF_OK;
 }
 
+// Zeroing with a kernel of our own instead of hipMemsetAsync: inside a captured HIP graph the
+// runtime's memset node (a blit kernel) did not survive later eager memsets on this ROCm —
+// replays then left every 4th float of the range stale (tests/test_gpu_graph.py).
+__global__ void k_zero(float* __restrict__ p, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0.f;
+}
+
+static int32_t zero_fill(float* p, int64_t n, hipStream_t s) {
+    if (n <= 0) return SPNERF_OK;
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0, s, p, n);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
 // per-ray sums of a point-major buffer (see k_ray_rowsum)
 template <typename T>
 static int32_t ray_rowsum(const T* in, int ld, int c0, int N, int S, int64_t n_rays, float* out, int ldo, hipStream_t s) {
@@ -928,8 +942,8 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
     PIdx x;
     auto specs = param_specs(d, &x);
     const int64_t total = specs.back().off + specs.back().numel();
-    SPN_HIP(hipMemsetAsync(grad, 0, total * sizeof(float), s));
-    if (grad_t && d.beta) SPN_HIP(hipMemsetAsync(grad_t, 0, n_rays * d.td * sizeof(float), s));
+    SPN_TRY(zero_fill(grad, total, s));
+    if (grad_t && d.beta) SPN_TRY(zero_fill(grad_t, n_rays * d.td, s));
     if (P == 0) return SPNERF_OK;
     auto gp = [&](int pi) { return grad + specs[pi].off; };
     auto ld = [&](int pi) { return (int)specs[pi].ld(); };

@@ -30,24 +30,30 @@ class SNerfLoss(torch.nn.Module):
 
 
 class DepthLoss(torch.nn.Module):
-    """Subset depth loss (usealldepth=False, MSE form, metrics.py:82-132,151-153)."""
+    """Subset depth loss (usealldepth=False — the trainer's default, opt.py:79 — MSE form,
+    metrics.py:82-132,151-153).
+
+    The reference selects the valid rays, then the rays outside the expected distribution,
+    and returns λ/3 · mean((n_apply / B) · tw · (pd − td)²) over the selected rays, i.e.
+    λ/3 · Σ_{valid ∧ apply} tw · (pd − td)² / B (0 when nothing is selected).  The same sum is
+    taken here with a 0/1 mask instead of boolean indexing, so it needs no host sync (boolean
+    indexing is a device→host count) and can be captured in a HIP graph.  The predicted std
+    only enters the comparison, so no gradient flows through its sqrt."""
 
     def __init__(self, lambda_ds=1.0):
         super().__init__()
         self.lambda_ds = lambda_ds / 3.0
 
     def forward(self, inputs, target_depth, target_weight, target_valid_depth, target_std):
-        valid = target_valid_depth > 0
-        z = inputs["z_vals_coarse"][valid]
-        pd = inputs["depth_coarse"][valid]
-        pw = inputs["weights_coarse"][valid]
-        pstd = (((z - pd.unsqueeze(-1)).pow(2) * pw).sum(-1)).sqrt()
-        tw, td, ts = target_weight[valid], target_depth[valid], target_std[valid]
-        apply = torch.logical_or((pd - td).abs() > ts, pstd > ts)
-        n_apply = apply.sum()
-        scale = n_apply.float() / float(target_valid_depth.shape[0])
-        per = tw[apply] * (pd[apply] - td[apply]) ** 2
-        loss = self.lambda_ds * torch.mean(scale * per) if per.numel() else pd.sum() * 0.0
+        z = inputs["z_vals_coarse"]
+        pd = inputs["depth_coarse"]
+        pw = inputs["weights_coarse"]
+        with torch.no_grad():
+            pstd = (((z - pd.unsqueeze(-1)).pow(2) * pw).sum(-1)).sqrt()
+            apply = (target_valid_depth > 0) & torch.logical_or((pd - target_depth).abs() > target_std,
+                                                                pstd > target_std)
+            m = apply.to(pd.dtype)
+        loss = self.lambda_ds * torch.sum(m * target_weight * (pd - target_depth) ** 2) / float(pd.shape[0])
         return loss, {"coarse_ds": loss}
 
 

@@ -129,7 +129,6 @@ class SPNeRF(torch.nn.Module):
         self._cfg = None
         self._order = None
         self._packed = None
-        self._pack_key = None
 
     # ---------------------------------------------------------------- library plumbing
     def cfg(self) -> _lib.ModelCfg:
@@ -171,34 +170,38 @@ class SPNeRF(torch.nn.Module):
         return [named[n] for n in self._order]
 
     def packed_weights(self) -> torch.Tensor:
-        """Kernel-layout copy of the weights, re-packed when any parameter changed (in-place
-        optimizer steps bump ``_version``)."""
+        """Kernel-layout copy of the weights, re-packed on every call (one ≈10 µs kernel).
+
+        Change detection is not possible: ``torch.optim.Adam(fused=True)`` updates parameters
+        in place without bumping ``_version``, so a version-keyed cache trains on stale weights.
+        Re-packing unconditionally is also what a captured HIP graph of a training step needs
+        (every replay re-packs the parameters the optimizer updated)."""
         params = self.canonical_parameters()
         _lib.require_device(params[0])
-        key = tuple((p.data_ptr(), p._version) for p in params)
-        if self._pack_key != key:
-            if self._packed is None or self._packed.device != params[0].device:
-                nbytes = _lib.lib().spnerf_packed_bytes(ctypes.byref(self.cfg()))
-                self._packed = torch.zeros(nbytes // 4, dtype=torch.float32, device=params[0].device)
-            for p in params:
-                if not p.is_contiguous() or p.dtype != torch.float32:
-                    raise _lib.SpnerfError("parameters must be contiguous float32")
-            arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
-            _lib.check(_lib.lib().spnerf_pack_params(ctypes.byref(self.cfg()), arr, _lib.ptr(self._packed),
-                                                     _lib.stream_of(self._packed)), "pack_params")
-            self._pack_key = key
+        if self._packed is None or self._packed.device != params[0].device:
+            nbytes = _lib.lib().spnerf_packed_bytes(ctypes.byref(self.cfg()))
+            self._packed = torch.zeros(nbytes // 4, dtype=torch.float32, device=params[0].device)
+        for p in params:
+            if not p.is_contiguous() or p.dtype != torch.float32:
+                raise _lib.SpnerfError("parameters must be contiguous float32")
+        arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+        _lib.check(_lib.lib().spnerf_pack_params(ctypes.byref(self.cfg()), arr, _lib.ptr(self._packed),
+                                                 _lib.stream_of(self._packed)), "pack_params")
         return self._packed
+
+    def invalidate_packed(self) -> None:
+        """Kept for callers that prepared a graph capture with it: packing is unconditional."""
 
     def set_precision(self, precision: str) -> "SPNeRF":
         """Switch the MLP arithmetic ("fp32" | "bf16"); parameters are unchanged."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
         self.precision = precision
-        self._cfg, self._packed, self._pack_key = None, None, None
+        self._cfg, self._packed = None, None
         return self
 
     def _apply(self, fn, *args, **kwargs):
-        self._packed, self._pack_key = None, None
+        self._packed = None
         return super()._apply(fn, *args, **kwargs)
 
     # ---------------------------------------------------------------- reference forward API
