@@ -105,6 +105,20 @@ def cpu_baseline(c, seconds: float):
             "sample": f"{n} train steps of {B} rays x {s_final} samples (oracle/ref_cpu.py, torch CPU, {threads} threads)"}
 
 
+def measured_traffic(config, kernel_class):
+    """HBM bytes per launch of ``kernel_class`` from the committed PMC profile of this workload
+    (tools/pmc_bench.sh + tools/traffic_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
+    bytes = 2*FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md's gfx950 correction).  PMC
+    counters cannot be read from inside the bench process, hence the profile file."""
+    path = os.path.join(ROOT, "profiles", "r01", f"traffic_{config}.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)[kernel_class]
+        return t["hbm_bytes_per_launch"], f"profiles/r01/traffic_{config}.json ({t['launches']} launches)"
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def gemm_totals(steps):
     """All MFMA GEMM launches of the timed steps: counted FLOP / summed kernel time, against the
     peak of each launch's dtype (time-weighted) — the MLP's MFMA utilisation."""
@@ -278,6 +292,7 @@ def main():
     nt = _lib.prof_read(dom)
     dom_name, peak = GEMM_CLASSES[dom]
     achieved = nt["flop"] / (nt["ms"] * 1e-3) / 1e12 if nt["ms"] else 0.0
+    traffic, traffic_src = measured_traffic(a.config, dom)
     total = world * B * s_final * a.steps
     out = {
         "metric": "ray-samples/sec (train step)",
@@ -296,7 +311,9 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": f"{dom} ({dom_name})", "achieved": achieved,
                      "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                     "traffic": None, "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
+                     "traffic": traffic, "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": nt["bytes"] / max(1, nt["launches"]),
+                     "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
         "mlp_gemms": gemm_totals(prof_steps),
         "kernels": kernels,
         "final_loss": final_loss,

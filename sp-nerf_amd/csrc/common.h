@@ -51,7 +51,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16;
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 // 4 consecutive activations as fp32 (the MLP keeps activations in fp32 or bf16, cfg.dtype)
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

@@ -8,7 +8,7 @@
 //  * k_gemm_tn_bf16 — weight gradients dW = dZᵀ·X summed over points.  Both operands stay in
 //    their natural [point][feature] layout: tiles are staged row-major (coalesced 16-B loads) in
 //    an XOR-swizzled LDS image and read back column-wise with ds_read_b64_tr_b16, so no
-//    activation is ever transposed in HBM.  Points are split over blockIdx.y into fp32 slabs
+//    activation is ever transposed in HBM.  Points are split over blocks into fp32 slabs
 //    reduced in a fixed order by k_reduce_slabs (deterministic).
 #include <algorithm>
 
@@ -257,10 +257,16 @@ __device__ __forceinline__ int tn_off(int row, int ch) {
 __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 256];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // 1-D grid of tiles x splits, split-major after the XCD remap: all tiles of one split run
+    // on one XCD, roughly in step through the points, so each operand slice is fetched into
+    // that XCD's L2 once (a (tile, split) grid spread every split over the 8 XCDs: 2.5x the
+    // algorithmic HBM/fabric traffic, profiles/r01/traffic_c3.json before this change)
     const int nK = (g.K + HB - 1) / HB;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntiles = cdiv(g.N, HB) * nK;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = w / ntiles, t = w % ntiles;
     const int n0 = (t / nK) * HB, k0 = (t % nK) * HB;
-    const int p_beg = blockIdx.y * g.p_per_split;
+    const int p_beg = split * g.p_per_split;
     const int p_end = min(g.P, p_beg + g.p_per_split);
     const int ch = tid & 15, lrow = tid >> 4;  // loader: 8 features (chunk ch), rows lrow + 16 i
     const bool do_bias = g.slab_b != nullptr && k0 == 0;
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
         }
     }
 
-    float* slab = g.slab + (int64_t)blockIdx.y * g.slab_stride;
+    float* slab = g.slab + (int64_t)split * g.slab_stride;
     const int r32 = lane & 31;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
         if (tid < 128 && n0 + tid < g.N) {
             float s = 0.f;
             for (int ph = 0; ph < 16; ++ph) s += red[ph * 128 + tid];
-            g.slab_b[(int64_t)blockIdx.y * g.N + n0 + tid] = s;
+            g.slab_b[(int64_t)split * g.N + n0 + tid] = s;
         }
     }
 }
@@ -441,7 +447,7 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     const int nb = cdiv(a.N, HB) * cdiv(a.K, HB);
     ProfScope prof("gemm_tn_bf16", s, 2.0 * a.P * a.N * a.K,
                    2.0 * (double)a.P * (a.N + a.K) + 4.0 * splits * (double)a.N * a.K);
-    hipLaunchKernelGGL(k_gemm_tn_bf16, dim3(nb, splits), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gemm_tn_bf16, dim3(nb * splits), dim3(256), 0, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

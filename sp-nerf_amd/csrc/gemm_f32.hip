@@ -258,10 +258,13 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
     constexpr int LDN = 128;
     __shared__ __attribute__((aligned(16))) float smem[ST * 2 * BK * LDN];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // 1-D grid, split-major after the XCD remap: the tiles of one split share one XCD's L2
+    // (see k_gemm_tn_bf16)
     const int nK = (g.K + 127) / 128;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntiles = cdiv(g.N, 128) * nK;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = w / ntiles, t = w % ntiles;
     const int n0 = (t / nK) * 128, k0 = (t % nK) * 128;
-    const int split = blockIdx.y;
     const int p_beg = split * g.p_per_split;
     const int p_end = min(g.P, p_beg + g.p_per_split);
     const int lr = tid >> 5, lc = (tid & 31) * 4;
@@ -538,8 +541,8 @@ int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s, int variant) {
     const int nb = cdiv(a.N, 128) * cdiv(a.K, 128);
     ProfScope prof("gemm_tn_f32", s, 2.0 * a.P * a.N * a.K, 4.0 * ((double)a.P * (a.N + a.K) + (double)splits * a.N * a.K));
     const int v = variant >= 0 ? variant : g_tn_variant;
-    if (v == 1) hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nb, splits), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nb, splits), dim3(256), 0, s, a);
+    if (v == 1) hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nb * splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nb * splits), dim3(256), 0, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
