@@ -52,6 +52,11 @@ CONFIGS = {
                         "samples, solar pass, depth + semantic (C=3) heads, W=512, bf16 MLP (fp32 accumulate / params)",
                img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True,
                precision="bf16"),
+    "c5": dict(workload="C5: whole-image inference render (no grad) of a synthetic 4k RPC camera: JAX_269_006 RPC at x5 "
+                        "(4065 x 3965 = 16.1M rays), 128 stratified samples/ray, semantic head on (C=3), W=512, bf16 MLP; "
+                        "rays sharded by image rows across ranks, each step renders the next 32768-ray chunk of the shard",
+               img_downscale=0.2, view="JAX_269_006_RGB", batch=32768, n_samples=128, sem=True, guided=False,
+               sc_lambda=0.0, depth=False, precision="bf16", inference=True),
     "c3_fp32": dict(workload="C3 flags at fp32 (parity arithmetic): as c3 with the fp32 MLP",
                     img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True,
                     precision="fp32"),
@@ -76,7 +81,7 @@ def cpu_baseline(c, seconds: float):
     dims = ModelDims(width=512, sem=c["sem"])
     p = ref_cpu.to_params(make_weights(dims, 0), requires_grad=True)
     opt = torch.optim.Adam(list(p.values()), lr=5e-4)
-    scene = synthetic_scene(c["img_downscale"], seed=1, device="cuda").to("cpu")
+    scene = synthetic_scene(c["img_downscale"] if not c.get("inference") else 4.0, seed=1, device="cuda").to("cpu")
     args = make_args(c)
     B = 256
     g = torch.Generator().manual_seed(0)
@@ -87,6 +92,10 @@ def cpu_baseline(c, seconds: float):
         kw = {}
         if c["guided"]:
             kw = dict(valid_depth=scene.valid_depth[idx], target_depths=scene.depths[idx], target_std=scene.depth_std[idx])
+        if c.get("inference"):
+            with torch.no_grad():
+                ref_cpu.render_rays(p, dims, args, scene.rays[idx], None, scene.sems[idx] if c["sem"] else None, "test")
+            return
         res = ref_cpu.render_rays(p, dims, args, scene.rays[idx], None, scene.sems[idx] if c["sem"] else None, "train", **kw)
         loss = torch.mean((res["rgb_coarse"] - scene.rgbs[idx]) ** 2)
         opt.zero_grad()
@@ -101,8 +110,9 @@ def cpu_baseline(c, seconds: float):
         if time.perf_counter() - t0 >= seconds or n >= 200:
             break
     dt = time.perf_counter() - t0
+    what = "inference renders" if c.get("inference") else "train steps"
     return {"value": B * s_final * n / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} train steps of {B} rays x {s_final} samples (oracle/ref_cpu.py, torch CPU, {threads} threads)"}
+            "sample": f"{n} {what} of {B} rays x {s_final} samples (oracle/ref_cpu.py, torch CPU, {threads} threads)"}
 
 
 def measured_traffic(config, kernel_class):
@@ -135,6 +145,82 @@ def gemm_totals(steps):
     return {"tflops": tf, "peak": peak, "frac": tf / peak, "ms_per_step": ms / steps}
 
 
+def run_inference(a, c, rank, world, dev):
+    """Config 5: ray-sharded whole-image inference.  Rank r generates rows [r·h/N, (r+1)·h/N)
+    of the image with the GPU RPC ray generator, then each step renders the next chunk of its
+    shard (render_rays in test mode: stratified samples, MLP without saved activations,
+    compositing).  No collective: the ranks only meet at the timing barriers."""
+    from spnerf_amd.satellite import image_rays, load_cameras
+    cams = load_cameras()
+    meta = cams["images"][c["view"]]
+    h, w = int(meta["height"] // c["img_downscale"]), int(meta["width"] // c["img_downscale"])
+    r0, r1 = rank * h // world, (rank + 1) * h // world
+    rays = image_rays(meta, c["img_downscale"], cams["scene_loc"], crop=(r0, 0, r1 - r0, w), device=dev)
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    sems = torch.multinomial(torch.tensor([0.45, 0.3, 0.15, 0.1]), rays.shape[0], replacement=True, generator=g)
+    sems = torch.where(sems == 3, torch.full_like(sems, -100), sems).to(dev)
+    torch.manual_seed(0)
+    model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"],
+                              precision=c["precision"]).to(dev)
+    args = make_args(c)
+    B, n = c["batch"], rays.shape[0]
+    pos = [0]
+
+    @torch.no_grad()
+    def step():
+        i0 = pos[0]
+        idx = torch.arange(i0, i0 + B, device=dev) % n
+        pos[0] = (i0 + B) % n
+        return spnerf_amd.render_rays({"coarse": model}, args, rays[idx], None, semantics=sems[idx], mode="test")
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _lib.prof_reset()
+    _lib.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    _lib.prof_enable(False)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    dom = max(GEMM_CLASSES, key=lambda k: _lib.prof_read(k)["ms"])
+    nt = _lib.prof_read(dom)
+    dom_name, peak = GEMM_CLASSES[dom]
+    achieved = nt["flop"] / (nt["ms"] * 1e-3) / 1e12 if nt["ms"] else 0.0
+    total = world * B * c["n_samples"] * a.steps
+    value = total / elapsed
+    out = {
+        "metric": "ray-samples/sec (inference render)", "value": value, "unit": "ray-samples/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": c["precision"],
+        "data": "synthetic RPC camera rays (JAX_269_006 RPC at x5), synthetic semantic labels, seeded-random SPNeRF init",
+        "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": c["n_samples"],
+                   "parallelism": f"ray-shard{world}", "image_rays": h * w},
+        "image_seconds_projected": h * w * c["n_samples"] / value,
+        "roofline": {"bound": "mfma", "kernel": f"{dom} ({dom_name})", "achieved": achieved, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                     "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
+        "mlp_gemms": gemm_totals(a.steps),
+        "finite": bool(torch.isfinite(res["rgb_coarse"]).all()),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,6 +239,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     c = CONFIGS[a.config]
+    if c.get("inference"):
+        return run_inference(a, c, rank, world, dev)
     scene = synthetic_scene(c["img_downscale"], seed=0, device=dev)
     R = {k: getattr(scene, k) for k in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")}
     torch.manual_seed(0)

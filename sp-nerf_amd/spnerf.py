@@ -287,7 +287,29 @@ def run_mlp(model: SPNeRF, rays: torch.Tensor, z: torch.Tensor, dir_offset: int,
         if sigma_only:
             raise _lib.SpnerfError("sigma-only passes are not differentiable (run them under torch.no_grad())")
         flags |= SPNERF_MLP_SAVE
-    return _MLP.apply(model, rays, dir_offset, z, labels, temb, flags, *params)
+        return _MLP.apply(model, rays, dir_offset, z, labels, temb, flags, *params)
+    # No autograd: ray chunks of at most max_points_per_call() points each write a slice of one
+    # output (the reference's args.chunk loop, spnerf.py:98, with chunks sized by the library's
+    # per-call limit instead of 5120 points).
+    B, S = z.shape
+    cb = max(1, max_points_per_call(model) // S)
+    if B <= cb:
+        return _MLP.apply(model, rays, dir_offset, z, labels, temb, flags, *params)
+    out = torch.empty(B * S, model.number_of_outputs, dtype=torch.float32, device=rays.device)
+    for i0 in range(0, B, cb):
+        i1 = min(B, i0 + cb)
+        out[i0 * S:i1 * S] = _MLP.apply(model, rays[i0:i1], dir_offset, z[i0:i1],
+                                        None if labels is None else labels[i0:i1],
+                                        None if temb is None else temb[i0:i1], flags, *params)
+    return out
+
+
+def max_points_per_call(model: SPNeRF) -> int:
+    """Largest B·S one spnerf_mlp_forward accepts (mlp.hip: P < 2^31 / max(NQ, NG))."""
+    H = model.feat // 2
+    nq = 2 * H + (H if model.beta else 0)
+    ng = model.feat + (H if model.sem else 0)
+    return ((1 << 31) - 1) // max(nq, ng)
 
 
 class _Composite(torch.autograd.Function):

@@ -234,3 +234,25 @@ def test_full_size_invariants():
     loss.backward()
     for n, p in model.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), n
+
+
+def test_nograd_chunking_matches_single_call(monkeypatch):
+    """No-grad MLP calls above the library's per-call point limit run in ray chunks (the
+    reference's args.chunk loop); forcing tiny chunks must not change a single bit."""
+    import spnerf_amd.spnerf as sp
+    dims = ModelDims(width=128, sem=True)
+    args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                                    sc_lambda=0.0, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+    rays, draws = c2_batch(n_rays=300, seed=4)
+    sem = torch.tensor(np.random.default_rng(0).integers(0, 3, 300), device=DEV)
+    model = make_model(dims, 5)
+    outs = []
+    for limit in (None, 64 * 37):
+        if limit is not None:
+            monkeypatch.setattr(sp, "max_points_per_call", lambda m: limit)
+        with torch.no_grad(), random_source(ReplayRandom(draws)):
+            res = spnerf_amd.render_rays({"coarse": model}, args, torch.tensor(rays, device=DEV), None, semantics=sem,
+                                         mode="test")
+        outs.append({k: v.cpu() for k, v in res.items()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
