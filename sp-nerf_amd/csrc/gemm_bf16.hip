@@ -244,6 +244,195 @@ __global__ __launch_bounds__(256) void k_gemm_nt_bf16(NT16Args g, int ntiles) {
     }
 }
 
+// Generalised NT tile: BM x BN per block, WGM x WGN waves each owning (BM/WGM) x (BN/WGN) =
+// MI x NJ 32x32 MFMA tiles.  Bigger wave tiles re-use every LDS fragment more (LDS bytes per
+// MFMA: (MI + NJ) / (MI · NJ) KB) and bigger block tiles halve the L2 re-reads of the weights;
+// with 256 x 256 / 8 waves one block fills a CU (147 KB of LDS).  Same loader, fences,
+// persistence and store-last epilogue as k_gemm_nt_bf16.
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_bf16w(NT16Args g, int ntiles) {
+    constexpr int T = 64 * WGM * WGN;
+    constexpr int MI = BM / WGM / 32, NJ = BN / WGN / 32;
+    constexpr int RP = T / 8;                       // rows per loader pass (8 16-B chunks per row)
+    constexpr int PA = BM / RP, PB = BN / RP;       // loader passes per operand
+    static_assert(BM % RP == 0 && BN % RP == 0, "loader geometry");
+    __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * HLK];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nN = (g.N + BN - 1) / BN;
+    const int G = gridDim.x;
+    const int lr = tid >> 3, lc = (tid & 7) * 8;
+    int t = xcd_remap(blockIdx.x, G);
+    if (t >= ntiles) return;  // block-uniform
+
+    const int lda1 = g.lda, lda2 = g.lda2, K1 = g.K1, Kt = g.K;
+    struct Regs {
+        u32x4 a[PA], b[PB];
+        bool kin;
+    };
+    auto gload = [&](Regs& r, int tile, int k0) {
+        const int bm = (tile / nN) * BM, bn = (tile % nN) * BN;
+        const int k = k0 + lc;
+        r.kin = k < Kt;
+        const int kc = r.kin ? k : Kt - 8;
+        const bool seg2 = k0 >= K1;
+        const bf16* pa = seg2 ? g.A2 + (kc - K1) : g.A + kc;
+        const int lda = seg2 ? lda2 : lda1;
+#pragma unroll
+        for (int i = 0; i < PA; ++i) r.a[i] = ldg16(pa + (int64_t)min(bm + lr + RP * i, g.M - 1) * lda);
+#pragma unroll
+        for (int i = 0; i < PB; ++i) r.b[i] = ldg16(g.B + (int64_t)min(bn + lr + RP * i, g.N - 1) * g.ldb + kc);
+    };
+    auto sstore = [&](const Regs& r, int stg) {
+        bf16* sA = smem + stg * (BM + BN) * HLK;
+        bf16* sB = sA + BM * HLK;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < PA; ++i) *reinterpret_cast<u32x4*>(sA + (lr + RP * i) * HLK + lc) = r.kin ? r.a[i] : z;
+#pragma unroll
+        for (int i = 0; i < PB; ++i) *reinterpret_cast<u32x4*>(sB + (lr + RP * i) * HLK + lc) = r.kin ? r.b[i] : z;
+    };
+
+    f32x16 acc[MI][NJ];
+    const int wr = wid / WGN, wc = wid % WGN, r32 = lane & 31, h = lane >> 5;
+    auto compute = [&](int stg) {
+        const bf16* sA = smem + stg * (BM + BN) * HLK + (wr * MI * 32 + r32) * HLK + 8 * h;
+        const bf16* sB = smem + stg * (BM + BN) * HLK + BM * HLK + (wc * NJ * 32 + r32) * HLK + 8 * h;
+#pragma unroll
+        for (int ks = 0; ks < HK / 16; ++ks) {
+            bf16x8 a[MI], b[NJ];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(sA + i * 32 * HLK + 16 * ks);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(sB + j * 32 * HLK + 16 * ks);
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    const int cq = (lane & 7) * 8;
+    constexpr int SLD = 68;
+    static_assert(WGM * WGN * 32 * SLD * 4 <= 2 * (BM + BN) * HLK * 2, "epilogue staging fits in the LDS");
+    float* stage = reinterpret_cast<float*>(smem) + wid * (32 * SLD);
+    const int nk = (g.K + HK - 1) / HK;
+
+    Regs r0;
+    gload(r0, t, 0);
+    sstore(r0, 0);
+    __syncthreads();
+    while (true) {
+        const int bm = (t / nN) * BM, bn = (t % nN) * BN;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int kt = 0; kt < nk; ++kt) {
+            gload(r0, t, min(kt + 1, nk - 1) * HK);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(kt & 1);
+            __builtin_amdgcn_sched_barrier(0);
+            sstore(r0, (kt + 1) & 1);
+            __syncthreads();
+        }
+        const int tn = t + G;
+        const bool more = tn < ntiles;
+        gload(r0, more ? tn : t, 0);
+
+        // epilogue: the wave's (MI·32) x (NJ·32) outputs, 32 rows x 64 columns at a time
+        const int col0 = bn + wc * NJ * 32;
+        float bias8[NJ / 2][8], r1v8[NJ / 2][8];
+#pragma unroll
+        for (int jp = 0; jp < NJ / 2; ++jp) {
+            const int colc = min(col0 + 64 * jp + cq, g.N - 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                bias8[jp][e] = g.bias ? g.bias[colc + e] : 0.f;
+                r1v8[jp][e] = g.r1_a ? g.r1_v[colc + e] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+            for (int jp = 0; jp < NJ / 2; ++jp) {
+                const int col = col0 + 64 * jp + cq;
+                const bool colok = col < g.N;
+                const int colc = colok ? col : g.N - 8;
+                // global loads of this 32 x 64 piece before its stores
+                u32x4 dm[4];
+                float r1a[4];
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int row = min(bm + wr * MI * 32 + i * 32 + (lane >> 3) + 8 * q4, g.M - 1);
+                    dm[q4] = g.Dmul ? ldg16(g.Dmul + (int64_t)row * g.ld_dmul + colc) : u32x4{0u, 0u, 0u, 0u};
+                    r1a[q4] = g.r1_a ? g.r1_a[(int64_t)row * g.r1_lda] : 0.f;
+                }
+                wave_lds_sync();
+#pragma unroll
+                for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        stage[((r & 3) + 8 * (r >> 2) + 4 * h) * SLD + j2 * 32 + r32] = acc[i][2 * jp + j2][r];
+                wave_lds_sync();
+                const bool sine_cols = g.act == 1 && col >= g.n_lin;
+                u32x4 oc[4], od[4];
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int rr = (lane >> 3) + 8 * q4;
+                    const int row = bm + wr * MI * 32 + i * 32 + rr;
+                    float v[8], d[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = stage[rr * SLD + cq + e] + bias8[jp][e];
+                    if (g.rowbias) {
+                        const float* rb = g.rowbias + (int64_t)(min(row, g.M - 1) / g.rows_per_ray) * g.ld_rb + colc;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] += rb[e];
+                    }
+                    if (g.r1_a) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] += r1a[q4] * r1v8[jp][e];
+                    }
+                    if (sine_cols) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            float sn, cs;
+                            fast_sincos(g.w0 * v[e], &sn, &cs);
+                            v[e] = sn;
+                            d[e] = g.w0 * cs;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) d[e] = 1.f;
+                    }
+                    if (g.Dmul) {
+                        float m[8];
+                        unpack8(dm[q4], m);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] *= m[e];
+                    }
+                    oc[q4] = pack8(v);
+                    od[q4] = pack8(d);
+                }
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int row = bm + wr * MI * 32 + i * 32 + (lane >> 3) + 8 * q4;
+                    if (row < g.M && colok) {
+                        *reinterpret_cast<u32x4*>(g.C + (int64_t)row * g.ldc + col) = oc[q4];
+                        if (g.Dout) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
+                    }
+                }
+            }
+        }
+        if (!more) break;
+        __syncthreads();
+        sstore(r0, 0);
+        __syncthreads();
+        t = tn;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // TN (weight gradients)
 // ------------------------------------------------------------------------------------------
@@ -399,7 +588,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
-int g_nt16_variant = 3;
+int g_nt16_variant = 5;
 
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt_bf16: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
@@ -418,6 +607,20 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     // variants: 1 / 2 = one block per tile, prefetch depth 1 / 2; 3 / 4 = persistent grid of
     // two blocks per CU (the LDS limit), depth 1 / 2
     const int v = variant > 0 ? variant : g_nt16_variant;
+    if (v >= 5) {  // generalised tiles, persistent with one block per CU
+        if (v == 5) {
+            const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
+            hipLaunchKernelGGL((k_gemm_nt_bf16w<256, 256, 2, 4>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        } else if (v == 6) {
+            const int nt = cdiv(a.M, 256) * cdiv(a.N, 128);
+            hipLaunchKernelGGL((k_gemm_nt_bf16w<256, 128, 4, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        } else {
+            const int nt = cdiv(a.M, 128) * cdiv(a.N, 256);
+            hipLaunchKernelGGL((k_gemm_nt_bf16w<128, 256, 2, 2>), dim3(std::min(nt, 256)), dim3(256), 0, s, a, nt);
+        }
+        SPN_HIP(hipGetLastError());
+        return SPNERF_OK;
+    }
     const int resident = 2 * 256;
     const int grid = v >= 3 ? std::min(ntiles, resident) : ntiles;
     if (v == 1 || v == 3) hipLaunchKernelGGL(k_gemm_nt_bf16<1>, dim3(grid), dim3(256), 0, s, a, ntiles);

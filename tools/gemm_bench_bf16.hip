@@ -100,7 +100,7 @@ static void check_nt(int M, int N, int K, int K1, bool sine, bool timing) {
     g.B = B.d; g.ldb = K; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K;
     if (sine) { g.bias = dbias; g.act = 1; g.w0 = 1.f; g.Dout = D; g.ld_dout = N; }
     else { g.Dmul = Dm.d; g.ld_dmul = N; }
-    for (int v = 1; v <= 4; ++v) {
+    for (int v : {1, 3, 5, 6, 7}) {
     CK(hipMemset(C, 0, (size_t)M * N * 2));
     if (gemm_nt_bf16(g, 0, v) != 0) { printf("launch refused\n"); fails++; return; }
     CK(hipDeviceSynchronize());
@@ -207,8 +207,8 @@ int main(int argc, char** argv) {
         NT16Args g;
         g.A = A.d; g.lda = 512; g.K1 = 512; g.B = B.d; g.ldb = 512; g.C = C; g.ldc = 512; g.M = P; g.N = 512; g.K = 512;
         g.bias = dbias; g.act = 1; g.Dout = D; g.ld_dout = 512;
-        const char* names[] = {"PF1 tile-per-block", "PF2 tile-per-block", "PF1 persistent", "PF2 persistent"};
-        const int vs[] = {1, 2, 3, 4};
+        const char* names[] = {"128x128 persistent", "256x256 8 waves", "256x128 8 waves", "128x256 4 waves"};
+        const int vs[] = {3, 5, 6, 7};
         for (int i = 0; i < 4; ++i) {
             const double us = time_it([&] { gemm_nt_bf16(g, 0, vs[i]); });
             printf("variant %-20s %8.1f us %7.1f TF/s\n", names[i], us, 2.0 * P * 512 * 512 / us * 1e-6);
