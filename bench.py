@@ -42,7 +42,8 @@ HBM_PEAK_GBS = 8000.0
 GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt (fp32 MFMA)", FP32_MFMA_PEAK_TFLOPS),
                 "gemm_tn_f32": ("k_gemm_tn (fp32 MFMA, weight gradients)", FP32_MFMA_PEAK_TFLOPS),
                 "gemm_nt_bf16": ("k_gemm_nt_bf16 (bf16 MFMA)", BF16_MFMA_PEAK_TFLOPS),
-                "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA, weight gradients)", BF16_MFMA_PEAK_TFLOPS)}
+                "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA, weight gradients)", BF16_MFMA_PEAK_TFLOPS),
+                "trunk_bf16": ("k_trunk_bf16 (fused bf16 trunk, layers 1..7 LDS-resident)", BF16_MFMA_PEAK_TFLOPS)}
 
 CONFIGS = {
     "c2": dict(workload="C2: JAX_214-shape scene (3 JAX_269 RPC cameras, GPU-generated rays), img_downscale=4, "
@@ -233,7 +234,12 @@ def main():
                     help="replay render+loss+backward as a HIP graph (default)")
     ap.add_argument("--eager", dest="graph", action="store_false", help="launch every kernel from Python")
     ap.add_argument("--prof-steps", type=int, default=3, help="eager steps timed per kernel in graph mode")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="library kernel switch (spnerf_set_option), e.g. fused_trunk=0, nt_f32_variant=4")
     a = ap.parse_args()
+    for o in a.option:
+        name, value = o.split("=")
+        _lib.set_option(name, int(value))
 
     rank, local, world = dp.init_from_env("nccl")
     torch.cuda.set_device(local)
@@ -367,7 +373,7 @@ def main():
     _lib.prof_enable(False)
 
     kernels = {}
-    for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "tn_skinny", "encode", "heads_fwd",
+    for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "trunk_bf16", "tn_skinny", "encode", "heads_fwd",
               "heads_bwd", "composite_fwd", "composite_bwd", "sample_guided"):
         s = _lib.prof_read(k)
         if s["launches"]:

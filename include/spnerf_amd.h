@@ -131,6 +131,13 @@ int32_t spnerf_rpc_rays(const double* rpc, double downscale, double min_alt, dou
                         const float* center, float range, const float* sun, float* rays, int32_t ray_stride,
                         void* stream);
 
+/* ---- kernel selection (no reference counterpart: A/B switches for tests and benches) ----
+ *      "fused_trunk" (1 = bf16 trunk layers 1..L-1 in one persistent LDS-resident launch,
+ *      the default; 0 = layer by layer), "nt_f32_variant", "tn_f32_variant",
+ *      "nt_bf16_variant" (GEMM tilings).  Process-wide; unknown names fail. */
+int32_t spnerf_set_option(const char* name, int32_t value);
+int32_t spnerf_get_option(const char* name, int32_t* value);
+
 /* ---- in-library kernel timing (HIP events on the launch stream) ------------------------- */
 int32_t spnerf_prof_enable(int32_t on);
 int32_t spnerf_prof_reset(void);

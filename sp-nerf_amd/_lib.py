@@ -56,6 +56,8 @@ SIGNATURES = {
     "spnerf_rpc_rays": (c_int32, [POINTER(c_double), c_double, c_double, c_double, c_int32, c_int32, c_int32, c_int32,
                                   c_void_p, c_int64, POINTER(c_float), c_float, POINTER(c_float), c_void_p, c_int32,
                                   c_void_p]),
+    "spnerf_set_option": (c_int32, [c_char_p, c_int32]),
+    "spnerf_get_option": (c_int32, [c_char_p, POINTER(c_int32)]),
     "spnerf_prof_enable": (c_int32, [c_int32]),
     "spnerf_prof_reset": (c_int32, []),
     "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
@@ -105,6 +107,17 @@ def require_device(*tensors) -> None:
         if t is not None and not t.is_cuda:
             raise SpnerfError("spnerf_amd runs the render path on the MI355X (HIP) only; got a tensor on "
                               f"{t.device}. Move rays / models to the GPU.")
+
+
+def set_option(name: str, value: int) -> None:
+    """Kernel-selection switch (spnerf_set_option): "fused_trunk", "nt_f32_variant", ..."""
+    check(lib().spnerf_set_option(name.encode(), int(value)), f"set_option({name})")
+
+
+def get_option(name: str) -> int:
+    v = ctypes.c_int32()
+    check(lib().spnerf_get_option(name.encode(), ctypes.byref(v)), f"get_option({name})")
+    return v.value
 
 
 def prof_enable(on: bool = True) -> None:

@@ -102,6 +102,18 @@ __device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
     *c = __builtin_amdgcn_cosf(r);
 }
 
+// the sine / cosine halves of fast_sincos (bit-identical results)
+__device__ __forceinline__ float fast_sin(float x) {
+    float r = x * 0.15915494309189535f;
+    r -= __builtin_rintf(r);
+    return __builtin_amdgcn_sinf(r);
+}
+__device__ __forceinline__ float fast_cos(float x) {
+    float r = x * 0.15915494309189535f;
+    r -= __builtin_rintf(r);
+    return __builtin_amdgcn_cosf(r);
+}
+
 // order LDS accesses of one wavefront (LDS is in order per wave; this stops the compiler
 // from moving accesses across the point)
 __device__ __forceinline__ void wave_lds_sync() {

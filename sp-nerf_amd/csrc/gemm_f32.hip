@@ -253,6 +253,207 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
     }
 }
 
+// Wide NT tile: BM x BN per block, WGM x WGN waves each owning (BM/WGM) x (BN/WGN) = MI x NJ
+// 32x32 MFMA tiles; K-step 32, double-buffered LDS (rows padded to 36 floats), persistent over
+// tiles (one block per CU at 256 x 256: 147 KB of LDS), the next tile's first K-step loading
+// during the epilogue.  Same k permutation as k_gemm_nt (lane half h takes k = 8g + 4h + s at
+// MFMA step s), so the accumulation order — and every output bit — equals k_gemm_nt's.
+// Epilogue: a wave stages 32 rows x 64 columns at a time in its own LDS slice; a lane owns 8
+// consecutive columns of rows (lane >> 3) + 8 q4, so every access is a 256-B (fp32) or 128-B
+// (bf16) row segment; all global loads of a piece are issued before its stores.
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntiles) {
+    constexpr int T = 64 * WGM * WGN;
+    constexpr int MI = BM / WGM / 32, NJ = BN / WGN / 32;
+    constexpr int KS = 32, LK = KS + 4;
+    constexpr int RP = T / 8;                  // rows per loader pass (8 float4 chunks per row)
+    constexpr int PA = BM / RP, PB = BN / RP;  // loader passes per operand
+    static_assert(BM % RP == 0 && BN % RP == 0 && NJ % 2 == 0, "tile geometry");
+    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LK];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nN = (g.N + BN - 1) / BN;
+    const int G = gridDim.x;
+    const int lr = tid >> 3, lk = (tid & 7) * 4;
+    int t = xcd_remap(blockIdx.x, G);
+    if (t >= ntiles) return;  // block-uniform
+
+    // unconditional loads from clamped rows (see k_gemm_nt); K, K1 are multiples of KS
+    const int lda1 = g.lda, lda2 = g.lda2, K1 = g.K1;
+    struct Regs {
+        f32x4 a[PA], b[PB];
+    };
+    auto gload = [&](Regs& r, int tile, int k0) {
+        const int bm = (tile / nN) * BM, bn = (tile % nN) * BN;
+        const bool seg2 = k0 >= K1;
+        const float* pa = seg2 ? g.A2 + (k0 - K1) + lk : g.A + k0 + lk;
+        const int lda = seg2 ? lda2 : lda1;
+#pragma unroll
+        for (int i = 0; i < PA; ++i) r.a[i] = ld4(pa + (int64_t)min(bm + lr + RP * i, g.M - 1) * lda);
+#pragma unroll
+        for (int i = 0; i < PB; ++i) r.b[i] = ld4(g.B + (int64_t)min(bn + lr + RP * i, g.N - 1) * g.ldb + k0 + lk);
+    };
+    auto sstore = [&](const Regs& r, int stg) {
+        float* sA = smem + stg * (BM + BN) * LK;
+        float* sB = sA + BM * LK;
+#pragma unroll
+        for (int i = 0; i < PA; ++i) *reinterpret_cast<f32x4*>(sA + (lr + RP * i) * LK + lk) = r.a[i];
+#pragma unroll
+        for (int i = 0; i < PB; ++i) *reinterpret_cast<f32x4*>(sB + (lr + RP * i) * LK + lk) = r.b[i];
+    };
+
+    f32x16 acc[MI][NJ];
+    const int wr = wid / WGN, wc = wid % WGN, r32 = lane & 31, h = lane >> 5;
+    auto compute = [&](int stg) {
+        const float* sA = smem + stg * (BM + BN) * LK + (wr * MI * 32 + r32) * LK + 4 * h;
+        const float* sB = smem + stg * (BM + BN) * LK + BM * LK + (wc * NJ * 32 + r32) * LK + 4 * h;
+#pragma unroll
+        for (int kg = 0; kg < KS / 8; ++kg) {
+            f32x4 a[MI], b[NJ];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) a[i] = ld4(sA + i * 32 * LK + kg * 8);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b[j] = ld4(sB + j * 32 * LK + kg * 8);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    const int cq = (lane & 7) * 8;
+    constexpr int SLD = 68;
+    static_assert(WGM * WGN * 32 * SLD <= 2 * (BM + BN) * LK, "epilogue staging fits in the LDS");
+    float* stage = smem + wid * (32 * SLD);
+    const int nk = g.K / KS;
+    const bool out16 = g.C16 != nullptr;
+
+    Regs r0;
+    gload(r0, t, 0);
+    sstore(r0, 0);
+    __syncthreads();
+    while (true) {
+        const int bm = (t / nN) * BM, bn = (t % nN) * BN;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int kt = 0; kt < nk; ++kt) {
+            gload(r0, t, min(kt + 1, nk - 1) * KS);  // past the last step: re-read it (L2 hit)
+            __builtin_amdgcn_sched_barrier(0);         // issue the loads before the MFMAs
+            compute(kt & 1);
+            __builtin_amdgcn_sched_barrier(0);         // LDS writes (and their vmcnt waits) after
+            sstore(r0, (kt + 1) & 1);
+            __syncthreads();
+        }
+        const int tn = t + G;
+        const bool more = tn < ntiles;
+        gload(r0, more ? tn : t, 0);  // the next tile's first K-step loads during the epilogue
+
+        const int col0 = bn + wc * NJ * 32;
+        float bias8[NJ / 2][8], r1v8[NJ / 2][8];
+#pragma unroll
+        for (int jp = 0; jp < NJ / 2; ++jp) {
+            const int colc = min(col0 + 64 * jp + cq, g.N - 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                bias8[jp][e] = g.bias ? g.bias[colc + e] : 0.f;
+                r1v8[jp][e] = g.r1_a ? g.r1_v[colc + e] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+            for (int jp = 0; jp < NJ / 2; ++jp) {
+                const int col = col0 + 64 * jp + cq;
+                const bool colok = col < g.N;
+                const int colc = colok ? col : g.N - 8;
+                const int rbase = bm + wr * MI * 32 + i * 32 + (lane >> 3);
+                f32x4 dm[4][2];
+                float r1a[4];
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int row = min(rbase + 8 * q4, g.M - 1);
+                    if (g.Dmul) {
+                        dm[q4][0] = ld4(g.Dmul + (int64_t)row * g.ld_dmul + colc);
+                        dm[q4][1] = ld4(g.Dmul + (int64_t)row * g.ld_dmul + colc + 4);
+                    }
+                    r1a[q4] = g.r1_a ? g.r1_a[(int64_t)row * g.r1_lda] : 0.f;
+                }
+                wave_lds_sync();
+#pragma unroll
+                for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        stage[((r & 3) + 8 * (r >> 2) + 4 * h) * SLD + j2 * 32 + r32] = acc[i][2 * jp + j2][r];
+                wave_lds_sync();
+                const bool sine_cols = g.act == 1 && col >= g.n_lin;  // n_lin is a multiple of 8
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int rr = (lane >> 3) + 8 * q4;
+                    const int row = rbase + 8 * q4;
+                    float v[8], d[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = stage[rr * SLD + cq + e] + bias8[jp][e];
+                    if (g.rowbias) {
+                        const float* rb = g.rowbias + (int64_t)(min(row, g.M - 1) / g.rows_per_ray) * g.ld_rb + colc;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] += rb[e];
+                    }
+                    if (g.r1_a) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] += r1a[q4] * r1v8[jp][e];
+                    }
+                    if (sine_cols) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            float sn, cs;
+                            if (out16) {
+                                fast_sincos(g.w0 * v[e], &sn, &cs);
+                            } else {
+                                sincosf(g.w0 * v[e], &sn, &cs);
+                            }
+                            v[e] = sn;
+                            d[e] = g.w0 * cs;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) d[e] = 1.f;
+                    }
+                    if (g.Dmul) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] *= dm[q4][e >> 2][e & 3];
+                    }
+                    if (row < g.M && colok) {
+                        if (out16) {
+                            *reinterpret_cast<u32x4*>(g.C16 + (int64_t)row * g.ldc + col) = pack8(v);
+                            if (g.D16) *reinterpret_cast<u32x4*>(g.D16 + (int64_t)row * g.ld_dout + col) = pack8(d);
+                        } else {
+                            float* pc = g.C + (int64_t)row * g.ldc + col;
+                            st4(pc, f32x4{v[0], v[1], v[2], v[3]});
+                            st4(pc + 4, f32x4{v[4], v[5], v[6], v[7]});
+                            if (g.Dout) {
+                                float* pd = g.Dout + (int64_t)row * g.ld_dout + col;
+                                st4(pd, f32x4{d[0], d[1], d[2], d[3]});
+                                st4(pd + 4, f32x4{d[4], d[5], d[6], d[7]});
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (!more) break;  // block-uniform
+        __syncthreads();   // every wave is done with its staging slice
+        sstore(r0, 0);
+        __syncthreads();
+        t = tn;
+    }
+}
+
 template <int ST>
 __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
     constexpr int LDN = 128;
@@ -483,8 +684,18 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     if (a.M == 0) return SPNERF_OK;
     const int nb = cdiv(a.M, BM) * cdiv(a.N, BN);
     ProfScope prof("gemm_nt_f32", s, 2.0 * a.M * a.N * a.K, 4.0 * ((double)a.M * a.K + (double)a.N * a.K + 2.0 * a.M * a.N));
-    const int v = variant >= 0 ? variant : g_nt_variant;
-    if (v == 1 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 1>), dim3(nb), dim3(256), 0, s, a);
+    int v = variant >= 0 ? variant : g_nt_variant;
+    if (v >= 4) {  // wide persistent tiles: 8-column epilogue rows need 16-B aligned row segments
+        const bool ok = a.N % 8 == 0 && a.n_lin % 8 == 0 && a.ldc % 4 == 0 && (!a.Dout || a.ld_dout % 4 == 0) &&
+                        (!a.Dmul || a.ld_dmul % 4 == 0) && (!a.rowbias || a.ld_rb % 4 == 0);
+        if (!ok) v = 2;
+    }
+    if (v == 4 || v == 5) {
+        const int bm = 256, bn = v == 4 ? 256 : 128;
+        const int nt = cdiv(a.M, bm) * cdiv(a.N, bn);
+        if (v == 4) hipLaunchKernelGGL((k_gemm_nt_w<256, 256, 2, 4>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+    } else if (v == 1 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 1>), dim3(nb), dim3(256), 0, s, a);
     else if (v == 2) hipLaunchKernelGGL((k_gemm_nt<32, 2>), dim3(nb), dim3(256), 0, s, a);
     else if (v == 3 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 2>), dim3(nb), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_gemm_nt<32, 1>), dim3(nb), dim3(256), 0, s, a);

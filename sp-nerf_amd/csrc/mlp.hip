@@ -19,6 +19,7 @@
 #include "gemm_bf16.h"
 #include "gemm_f32.h"
 #include "mlp_layout.h"
+#include "trunk.h"
 
 namespace spn {
 
@@ -28,7 +29,9 @@ namespace spn {
 
 struct PackPiece {
     const float* src;
-    int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;  // bf: bf16 destination, dst in bf16 units
+    // bf: 1 = bf16 destination (dst in bf16 units); 2 = bf16 in the fused trunk's MFMA fragment
+    // order (trunk_frag_off, dst_ld = the layer's padded K)
+    int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;
     int64_t dst;
 };
 constexpr int kMaxPieces = 24;
@@ -43,7 +46,9 @@ __global__ void k_pack(PackArgs a) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int r = (int)(i / pc.cols), c = (int)(i % pc.cols);
         const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
-        const int64_t o = pc.dst + (pc.transpose ? (int64_t)c * pc.dst_ld + r : (int64_t)r * pc.dst_ld + c);
+        const int64_t o = pc.dst + (pc.bf == 2        ? trunk_frag_off(r, c, pc.dst_ld)
+                                    : pc.transpose ? (int64_t)c * pc.dst_ld + r
+                                                   : (int64_t)r * pc.dst_ld + c);
         if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)v;
         else a.packed[o] = v;
     }
@@ -520,6 +525,7 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
             const int kreal = i == d.skip ? W + d.K0 : W;
             SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wt16[i], k.Kp[i], 0, 1));
             SPN_TRY(piece(x.fcW[i], 0, W, W, k.WTt16[i], W, 1, 1));
+            if (k.Wf16[i] >= 0) SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wf16[i], k.Kp[i], 0, 2));
         }
         if (d.sem) {
             SPN_TRY(piece(x.m1W, 0, H, W, k.WG16 + (int64_t)W * W, W, 0, 1));
@@ -648,7 +654,29 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
     const T* X0 = BF ? G::buf(c, c.w.X0b) : G::buf(c, c.w.X0);
     const T* h = nullptr;
     T* HL = nullptr;
+    const bool fused = BF && g_fused_trunk && !c.k.Wf16.empty() && c.k.Wf16[1] >= 0;
     for (int i = 0; i < d.L; ++i) {
+        if (fused && i == 1) {
+            // layers 1 .. L-1 in one persistent launch, activations resident in LDS
+            TrunkArgs a;
+            a.H1 = reinterpret_cast<const bf16*>(h);
+            a.X0b = c.hb(c.w.X0b);
+            double ksum = 0.0;
+            for (int l = 1; l < d.L; ++l) {
+                a.Wf[l] = c.pk16(c.k.Wf16[l]);
+                a.bias[l] = c.pk(c.k.bt[l]);
+                a.Hs[l] = save ? c.hb(c.w.Hb[l]) : (l == d.L - 1 ? c.hb(c.w.Hb[l & 1]) : nullptr);
+                a.Ds[l] = save ? c.hb(c.w.Db[l]) : nullptr;
+                ksum += c.k.Kp[l];
+            }
+            a.rb_skip = d.sem ? c.at(c.w.rb4) : nullptr;
+            a.P = P; a.S = S; a.L = d.L; a.skip = d.skip; a.K0p = d.K0p;
+            // algorithmic HBM bytes: the H_1 and PE tiles in, H (and D) of every layer out when saving
+            const double bytes = 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0)) + 2.0 * P * W * (save ? 2.0 * (d.L - 1) : 1.0);
+            SPN_TRY(trunk_bf16(a, s, 2.0 * P * W * ksum, bytes));
+            HL = reinterpret_cast<T*>(a.Hs[d.L - 1]);
+            break;
+        }
         T* dst = save ? G::buf(c, c.w.Hb[i]) : G::buf(c, c.w.Hb[i & 1]);
         T* dd = save ? G::buf(c, c.w.Db[i]) : nullptr;
         const float* rb = (d.sem && (i == 0 || i == d.skip)) ? c.at(i == 0 ? c.w.rb0 : c.w.rb4) : nullptr;
@@ -992,6 +1020,31 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
 // C ABI
 // ------------------------------------------------------------------------------------------
 using namespace spn;
+
+static int* option_slot(const char* name) {
+    const std::string n(name);
+    if (n == "fused_trunk") return &g_fused_trunk;
+    if (n == "nt_f32_variant") return &g_nt_variant;
+    if (n == "tn_f32_variant") return &g_tn_variant;
+    if (n == "nt_bf16_variant") return &g_nt16_variant;
+    return nullptr;
+}
+
+extern "C" int32_t spnerf_set_option(const char* name, int32_t value) {
+    SPN_ARG(name != nullptr, "set_option: NULL name");
+    int* slot = option_slot(name);
+    SPN_ARG(slot != nullptr, "set_option: unknown option '%s'", name);
+    *slot = value;
+    return SPNERF_OK;
+}
+
+extern "C" int32_t spnerf_get_option(const char* name, int32_t* value) {
+    SPN_ARG(name != nullptr && value != nullptr, "get_option: NULL pointer");
+    int* slot = option_slot(name);
+    SPN_ARG(slot != nullptr, "get_option: unknown option '%s'", name);
+    *value = *slot;
+    return SPNERF_OK;
+}
 
 extern "C" int32_t spnerf_param_count(const spnerf_model_cfg* cfg) {
     Dims d;

@@ -5,6 +5,7 @@
 
 #include "gemm_bf16.h"
 #include "gemm_f32.h"
+#include "trunk.h"
 
 namespace spn {
 
@@ -147,9 +148,11 @@ Packed packed_layout(const Dims& d) {
     k.Wtt = take((int64_t)H * (d.td ? d.td : 1));
     if (d.bf) {
         auto take16 = [&](int64_t n) { return 2 * take((n + 1) / 2); };
+        const bool fused = trunk_bf16_supported(W, d.L, d.skip, d.K0p);
         for (int i = 0; i < d.L; ++i) {
             k.Wt16.push_back(i == 0 ? -1 : take16((int64_t)W * k.Kp[i]));
             k.WTt16.push_back(i == 0 ? -1 : take16((int64_t)W * W));
+            k.Wf16.push_back(i == 0 || !fused ? -1 : take16((int64_t)W * k.Kp[i]));
         }
         k.WG16 = take16((int64_t)d.NG * W);
         k.WGT16 = take16((int64_t)W * d.NG);

@@ -58,6 +58,7 @@ struct Packed : PackedOffs {
     std::vector<int64_t> Wt, bt, WTt;   // trunk: forward [W][Kp_i], bias, transposed h-part [W][W]
     std::vector<int> Kp;                // padded K of each trunk layer
     std::vector<int64_t> Wt16, WTt16;   // bf16 trunk layers 1.. (bf16 units), -1 for layer 0
+    std::vector<int64_t> Wf16;          // the same in MFMA fragment order for the fused trunk (-1: none)
 };
 Packed packed_layout(const Dims& d);
 

@@ -1,0 +1,96 @@
+"""Fused bf16 trunk (k_trunk_bf16: fc_net layers 1..L-1 in one persistent launch, activations
+resident in LDS) vs the layer-by-layer bf16 GEMMs it replaces — needs an MI355X.
+
+Both paths do the same arithmetic in the same k-order (fp32 accumulation of the same bf16
+products, the same epilogue), so renders and gradients must agree to fp32 rounding; the bf16
+path itself is held to the reference by tests/test_gpu_bf16.py.  Covered: the guided-sampling
+pass 1 (no saved activations, sigma only), pass 2 and the solar pass (saved H / D feeding the
+backward), the skip layer's PE columns and per-ray semantic rows, point counts that are not a
+multiple of the 128-point tile, and PE off (K0p = 32).
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+import spnerf_amd
+from spnerf_amd import _lib
+from oracle.weights import ModelDims
+from test_gpu_parity import DEV, gu_rays, make_model
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5  # norm-relative
+
+
+def _render(fused: bool, dims: ModelDims, n_rays: int, guided: bool, sc: float, seed: int = 0):
+    _lib.set_option("fused_trunk", int(fused))
+    try:
+        args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=guided,
+                                        sc_lambda=sc, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+        rays = torch.tensor(gu_rays(n_rays, 9 + seed), device=DEV)
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        kw = {}
+        if guided:
+            kw = dict(valid_depth=(torch.rand(n_rays, generator=g) < 0.68).long().to(DEV),
+                      target_depths=torch.stack([rays[:, 7] * 0.5, torch.ones(n_rays, device=DEV)], 1),
+                      target_std=torch.full((n_rays,), 0.01, device=DEV))
+        sem = torch.randint(-1, 3, (n_rays,), generator=g).to(DEV) if dims.sem else None
+        if sem is not None:
+            sem = torch.where(sem < 0, torch.full_like(sem, -100), sem)
+        model = make_model(dims, 2, "bf16")
+        torch.manual_seed(123)  # same device draws for both runs
+        res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="train", **kw)
+        loss = sum((v.float() ** 2).mean() for k, v in sorted(res.items()) if v.requires_grad)
+        loss.backward()
+        torch.cuda.synchronize()
+        return ({k: v.detach().cpu() for k, v in res.items()},
+                {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None})
+    finally:
+        _lib.set_option("fused_trunk", 1)
+
+
+@pytest.mark.parametrize("dims,n_rays,guided,sc", [
+    (ModelDims(width=512, sem=True), 257, True, 0.1),     # C3 flags; 257·64 points: ragged last tile
+    (ModelDims(width=512), 1024, False, 0.0),             # C2 flags at bf16
+    (ModelDims(width=512, mapping=False), 130, False, 0.1),  # no PE: K0p = 32 skip columns
+])
+def test_fused_trunk_matches_layerwise(dims, n_rays, guided, sc):
+    assert _lib.get_option("fused_trunk") == 1
+    r1, g1 = _render(True, dims, n_rays, guided, sc)
+    r0, g0 = _render(False, dims, n_rays, guided, sc)
+    assert sorted(r1) == sorted(r0) and sorted(g1) == sorted(g0)
+    same = True
+    for k in r0:
+        assert torch.isfinite(r1[k]).all(), k
+        e = gu.rel_err(r1[k].numpy(), r0[k].numpy())
+        same &= torch.equal(r1[k], r0[k])
+        assert e <= TOL, (k, e)
+    worst = 0.0
+    for n in g0:
+        e = gu.rel_err(g1[n].numpy(), g0[n].numpy()) if g0[n].abs().sum() > 0 else float(g1[n].abs().sum())
+        same &= torch.equal(g1[n], g0[n])
+        worst = max(worst, e)
+        assert e <= TOL, (n, e)
+    print(f"fused vs layer-by-layer: bitwise={same} worst grad rel err {worst:.2e}")
+
+
+def test_fused_trunk_point_network_bitwise_vs_layerwise():
+    """SPNeRF.forward on 3000 points (S = 1: every point its own ray, semantic + beta heads)."""
+    dims = ModelDims(width=512, sem=True, beta=True)
+    rng = np.random.default_rng(5)
+    P = 3000
+    xyz = torch.tensor(rng.uniform(-1, 1, (P, 3)).astype(np.float32), device=DEV)
+    sun = torch.tensor(rng.normal(size=(P, 3)).astype(np.float32), device=DEV)
+    lab = torch.tensor(rng.choice([0, 1, 2, -100], size=P).astype(np.int64), device=DEV)
+    t = torch.tensor(rng.normal(size=(P, dims.t_dim)).astype(np.float32), device=DEV)
+    m = make_model(dims, 4, "bf16")
+    outs = []
+    for fused in (1, 0):
+        _lib.set_option("fused_trunk", fused)
+        try:
+            with torch.no_grad():
+                outs.append(m(xyz, input_sun_dir=sun, input_t=t, input_s=lab).cpu())
+        finally:
+            _lib.set_option("fused_trunk", 1)
+    assert torch.isfinite(outs[0]).all()
+    assert gu.rel_err(outs[0].numpy(), outs[1].numpy()) <= TOL
