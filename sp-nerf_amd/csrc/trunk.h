@@ -20,6 +20,7 @@ struct TrunkArgs {
     const float* rb_skip = nullptr;
     int64_t P = 0;
     int S = 1, L = 0, skip = -1, K0p = 0;
+    int dbg = 0;  // set from g_trunk_dbg by trunk_bf16
 };
 
 // Offset (bf16 elements) of W[n][k] of a [512][Kp] layer in MFMA A-fragment order: wave w =
@@ -32,6 +33,8 @@ __host__ __device__ inline int64_t trunk_frag_off(int n, int k, int Kp) {
 }
 
 extern int g_fused_trunk;  // 1 = bf16 forwards use the fused trunk where supported (default)
+extern int g_trunk_tile;   // 0 = tile by mode; 64 / 128 = force
+extern int g_trunk_dbg;    // profiling ablations (outputs invalid): 1 = no HBM copy-outs
 bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes);
 

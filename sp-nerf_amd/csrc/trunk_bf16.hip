@@ -1,23 +1,32 @@
 // Fused SIREN trunk of the bf16 MLP (cfg.dtype = 1, W = 512): fc_net layers 1 .. L-1
-// (models/spnerf.py:201-209, 323-330) for a tile of 128 points per workgroup, with the
+// (models/spnerf.py:201-209, 323-330) for a tile of TMt points per workgroup, with the
 // activations resident in LDS from layer to layer — the persistent MFMA MLP kernel of DESIGN.md.
 //
 // Formulation: every layer computes Hᵀ_next = sin(W·Hᵀ + b) with the WEIGHTS as the MFMA A
 // operand and the activation tile as B (v_mfma_f32_32x32x16_bf16).  A 32x32 accumulator then
 // holds, per lane, 4 runs of 4 consecutive output features of ONE point: each run is an 8-byte
 // piece of a row of the next layer's [point][feature] image, written with one ds_write_b64.
-//  * LDS (148 KB): the [128][512] bf16 activation image (16-B chunks XOR-swizzled by row & 15:
-//    conflict-free ds_read_b128 B fragments and ds_write_b64 epilogue writes), the [128][K0p]
-//    PE tile of the skip layer, and two bias slots (layer parity).
+//  * LDS: the [TMt][512] bf16 activation image (16-B chunks XOR-swizzled by row & 15:
+//    conflict-free ds_read_b128 B fragments and ds_write_b64 epilogue writes), when saving a
+//    second image for D = cos, the [TMt][K0p] PE tile of the skip layer, two bias slots.
 //  * Weights stream from L2 (every CU walks the same 512 KB per layer), packed by
 //    spnerf_pack_params in MFMA fragment order (trunk_frag_off): wave w's A fragments of k-step
 //    ks are one contiguous 2 KB, loaded TPD k-steps ahead into a register ring.  The next
 //    layer's first k-steps load during the current layer's epilogue.
-//  * 8 waves; wave w owns output features [64w, 64w + 64) of all 128 points (2 x 4 tiles).
+//  * 8 waves; wave w owns output features [64w, 64w + 64) of all TMt points (2 x TMt/32 tiles).
 //  * Epilogue = the unfused k_gemm_nt_bf16 arithmetic (fp32 accumulator + bias (+ the per-ray
-//    semantic rows at the skip layer), fast_sincos, bf16 rounding) over the same k-order: sin
-//    goes to the LDS image and, when saving for the backward, H_i / D_i = cos go to HBM; the
-//    last layer's H always goes to HBM (the heads read it).
+//    semantic rows at the skip layer), fast_sincos, bf16 rounding) over the same k-order, so the
+//    outputs equal the layer-by-layer path's bit for bit.
+//  * Outputs leave through the images: a wave writes its 8-byte pieces to LDS, and whole 1-KB
+//    rows are copied to HBM (one row per store instruction; scattered 8-byte stores straight
+//    from the accumulator layout cost ~2x the whole layer) behind the NEXT layer's MFMAs, which
+//    read the same image.
+// Two tilings:
+//  * TMt = 128 (inference: nothing saved but the last layer's H): 148 KB of LDS, 4 B fragments
+//    per weight fragment (32 B/clk/CU of L2 weight traffic at the MFMA peak);
+//  * TMt = 64 (training: H_i and D_i of every layer saved for the backward): the H and D images
+//    (64 KB each) both drain behind the next layer's k-loop, instead of D leaving between two
+//    barriers; twice the weight traffic per point.
 #include <algorithm>
 #include <type_traits>
 
@@ -28,18 +37,27 @@ namespace spn {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 int g_fused_trunk = 1;
+int g_trunk_tile = 0;  // 0 = by mode (64 when saving, else 128); 64 / 128 force a tiling (A/B runs)
+int g_trunk_dbg = 0;   // profiling ablation, outputs invalid when set: 1 = skip the HBM copy-outs
 
-constexpr int TW = 512;                      // trunk width of the fused kernel
-constexpr int TM = 128;                      // points per tile
-constexpr int TPD = 4;                       // weight prefetch depth (k-steps)
-constexpr int ACT_BYTES = TM * TW * 2;       // 131072
-constexpr int X0_BYTES = TM * 64 * 2;        // 16384 (K0p <= 64)
-constexpr int TRUNK_LDS = ACT_BYTES + X0_BYTES + 2 * TW * 4;
+constexpr int TW = 512;  // trunk width of the fused kernel
+
+template <int TMt>
+struct TrunkGeo {
+    static constexpr int NJ = TMt / 32;                        // point tiles per wave
+    static constexpr bool DIMG = TMt == 64;                    // a D image beside the H image
+    static constexpr int TPD = TMt == 64 ? 8 : 4;              // weight prefetch depth (k-steps)
+    static constexpr int IMG = TMt * TW * 2;                   // one [TMt][512] bf16 image
+    static constexpr int X0_OFF = IMG * (DIMG ? 2 : 1);
+    static constexpr int BIAS_OFF = X0_OFF + TMt * 64 * 2;     // K0p <= 64
+    static constexpr int LDS = BIAS_OFF + 2 * TW * 4;
+    static constexpr int CPT = TMt * 64 / 512;                 // 16-B chunks of an image per thread
+};
 
 __device__ __forceinline__ int act_off(int row, int ch) { return row * 1024 + ((ch ^ (row & 15)) << 4); }
 // PE rows are 8 chunks (128 B): XOR with (row >> 1) & 7 keeps the 16 rows of a ds_read_b128
 // lane group on distinct 16-B slots of the bank row
-__device__ __forceinline__ int x0_off(int row, int ch) { return ACT_BYTES + row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int x0_rel(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 
 // a copy of x the compiler cannot see through: lane-derived addresses are recomputed in each
 // region (staging, k-loop, epilogue) instead of being hoisted out of all loops and kept live
@@ -49,13 +67,17 @@ __device__ __forceinline__ int opaque(int x) {
     return x;
 }
 
+template <int TMt>
 __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
-    __shared__ __attribute__((aligned(16))) char smem[TRUNK_LDS];
+    using Geo = TrunkGeo<TMt>;
+    constexpr int NJ = Geo::NJ, TPD = Geo::TPD, IMG = Geo::IMG, CPT = Geo::CPT;
+    __shared__ __attribute__((aligned(16))) char smem[Geo::LDS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
-    float* sbias = reinterpret_cast<float*>(smem + ACT_BYTES + X0_BYTES);
+    float* sbias = reinterpret_cast<float*>(smem + Geo::BIAS_OFF);
+    char* sx0 = smem + Geo::X0_OFF;
     const int x0ch = g.K0p >> 3;
-    constexpr int nmain = TW / 16;                // k-steps over the activation image
-    const int ntail = g.K0p >> 4;                 // extra k-steps over the PE at the skip layer
+    constexpr int nmain = TW / 16;  // k-steps over the activation image
+    const int ntail = g.K0p >> 4;   // extra k-steps over the PE at the skip layer
     const int sw = r32 & 15;
     // per-layer pointers indexed by the (runtime) layer: scalar loads straight from the kernarg
     // segment (indexing the by-value struct copies its arrays to scratch)
@@ -76,73 +98,97 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             ring[d][1] = ldg16(src + d * 1024 + 512);
         }
     };
+    // copy chunks [q0, q0 + n) (per thread) of an image to HBM rows p0 + row
+    auto copy_out = [&](const char* img, bf16* dst, int64_t p0, int q0, auto kn) {
+        constexpr int n = decltype(kn)::value;
+        const int ct = opaque(tid);
+        u32x4 v[n];
+#pragma unroll
+        for (int q = 0; q < n; ++q) {
+            const int c = ct + 512 * (q0 + q);
+            v[q] = *reinterpret_cast<const u32x4*>(img + act_off(c >> 6, c & 63));
+        }
+#pragma unroll
+        for (int q = 0; q < n; ++q) {
+            const int c = ct + 512 * (q0 + q);
+            if (p0 + (c >> 6) < g.P) *reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8) = v[q];
+        }
+    };
+
+    // a whole image, 4 chunks per thread at a time (the accumulators may still be live)
+    auto copy_all = [&](const char* img, bf16* dst, int64_t p0) {
+        if (g.dbg & 1) return;
+#pragma unroll
+        for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(img, dst, p0, q0, std::integral_constant<int, 4>{});
+    };
 
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
     prime(1);
     for (; tile < ntiles; tile += gridDim.x) {
-        const int64_t p0 = (int64_t)tile * TM;
+        const int64_t p0 = (int64_t)tile * TMt;
         const int st = opaque(tid);
         // stage the layer-1 input and the PE tile; rows past P read a clamped row (their
         // outputs are never stored)
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
+        for (int q0 = 0; q0 < CPT; q0 += 8) {
             u32x4 v[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const int c = st + 512 * (8 * half + q), row = c >> 6, ch = c & 63;
+                const int c = st + 512 * (q0 + q), row = c >> 6, ch = c & 63;
                 v[q] = ldg16(g.H1 + std::min<int64_t>(p0 + row, g.P - 1) * TW + ch * 8);
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const int c = st + 512 * (8 * half + q), row = c >> 6, ch = c & 63;
+                const int c = st + 512 * (q0 + q), row = c >> 6, ch = c & 63;
                 *reinterpret_cast<u32x4*>(smem + act_off(row, ch)) = v[q];
             }
         }
         if (g.skip > 0) {
-            for (int c = st; c < TM * x0ch; c += 512) {
+            for (int c = st; c < TMt * x0ch; c += 512) {
                 const int row = c / x0ch, ch = c % x0ch;
-                *reinterpret_cast<u32x4*>(smem + x0_off(row, ch)) =
+                *reinterpret_cast<u32x4*>(sx0 + x0_rel(row, ch)) =
                     ldg16(g.X0b + std::min<int64_t>(p0 + row, g.P - 1) * g.K0p + ch * 8);
             }
         }
 
-        bf16* hpend = nullptr;  // H of the previous layer: copied to HBM during this layer's k-loop
+        bf16* hpend = nullptr;  // H (and D) of the previous layer: copied out during this k-loop
+        bf16* dpend = nullptr;
         for (int i = 1; i < g.L; ++i) {
             const bool skip = i == g.skip;
             const bf16* wsrc = wstream(i);
             const int nks = nmain + (skip ? ntail : 0);
             float* sb = sbias + (i & 1) * TW;  // slot (i-1)&1 may still be read by the previous epilogue
             sb[tid] = ka->bias[i][tid];
-            f32x16 acc[2][4];
+            f32x16 acc[2][NJ];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < NJ; ++j)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) acc[a][j][r] = 0.f;
             __syncthreads();  // the image (and the bias slot) of layer i are complete
 
             // B fragments are double-buffered: step ks+1's image reads are issued between step
-            // ks's MFMAs (past the image's last step the read lands in the PE area: in bounds,
-            // unused)
+            // ks's MFMAs (past the image's last step the read lands in the next LDS region: in
+            // bounds, unused)
             const char* brow = smem + r32 * 1024;
-            bf16x8 bc[4];
+            bf16x8 bc[NJ];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
+            for (int j = 0; j < NJ; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
 #pragma unroll 1
             for (int ks0 = 0; ks0 < nmain; ks0 += TPD) {
 #pragma unroll
                 for (int d = 0; d < TPD; ++d) {
                     const int ks = ks0 + d;
                     const int offn = ((2 * (ks + 1) + h) ^ sw) << 4;
-                    bf16x8 bn[4];
+                    bf16x8 bn[NJ];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
+                    for (int j = 0; j < NJ; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
                     const bf16x8 a0 = __builtin_bit_cast(bf16x8, ring[d][0]);
                     const bf16x8 a1 = __builtin_bit_cast(bf16x8, ring[d][1]);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < NJ; ++j) {
                         acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bc[j], acc[0][j], 0, 0, 0);
                         acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bc[j], acc[1][j], 0, 0, 0);
                     }
@@ -151,50 +197,41 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                     const int kn = std::min(ks + TPD, nks - 1);
                     ring[d][0] = ldg16(wsrc + kn * 1024);
                     ring[d][1] = ldg16(wsrc + kn * 1024 + 512);
-                    // order: (1 image read, 2 MFMAs) x 4, then the 2 weight loads
+                    // order: (1 image read, 2 MFMAs) x NJ, then the 2 weight loads
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < NJ; ++j) {
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                     }
                     __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) bc[j] = bn[j];
+                    for (int j = 0; j < NJ; ++j) bc[j] = bn[j];
                 }
-                if (hpend) {  // block-uniform: 2 of the image's 16 row chunks per thread
-                    const int ct = opaque(tid);
-#pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        const int c = ct + 512 * (2 * (ks0 / TPD) + q);
-                        const u32x4 v = *reinterpret_cast<const u32x4*>(smem + act_off(c >> 6, c & 63));
-                        if (p0 + (c >> 6) < g.P) *reinterpret_cast<u32x4*>(hpend + (p0 + (c >> 6)) * TW + (c & 63) * 8) = v;
-                    }
-                }
+                // drain the previous layer's outputs: CPT / (nmain / TPD) chunks per thread
+                constexpr int per = CPT / (nmain / TPD);
+                static_assert(per * (nmain / TPD) == CPT && per >= 1, "copy slices");
+                if (hpend && !(g.dbg & 1)) copy_out(smem, hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                if (Geo::DIMG && dpend && !(g.dbg & 1)) copy_out(smem + IMG, dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
             }
-            static_assert(TW / 16 / TPD * 2 == 16, "the k-loop copies the 16 chunks per thread of the image");
-            // the x0 columns of the skip layer's input [h | x0] (nks == nmain elsewhere); ntail
-            // is a multiple of TPD (K0p is 32 or 64)
+            // the x0 columns of the skip layer's input [h | x0] (nks == nmain elsewhere)
 #pragma unroll 1
             for (int ks0 = nmain; ks0 < nks; ks0 += TPD) {
 #pragma unroll
                 for (int d = 0; d < TPD; ++d) {
                     const int ks = ks0 + d;
-                    bf16x8 b[4];
+                    if (ks < nks) {  // block-uniform
+                        bf16x8 b[NJ];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        b[j] = *reinterpret_cast<const bf16x8*>(smem + x0_off(32 * j + r32, 2 * (ks - nmain) + h));
-                    const bf16x8 a0 = __builtin_bit_cast(bf16x8, ring[d][0]);
-                    const bf16x8 a1 = __builtin_bit_cast(bf16x8, ring[d][1]);
+                        for (int j = 0; j < NJ; ++j)
+                            b[j] = *reinterpret_cast<const bf16x8*>(sx0 + x0_rel(32 * j + r32, 2 * (ks - nmain) + h));
+                        const bf16x8 a0 = __builtin_bit_cast(bf16x8, ring[d][0]);
+                        const bf16x8 a1 = __builtin_bit_cast(bf16x8, ring[d][1]);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[j], acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[j], acc[1][j], 0, 0, 0);
+                        for (int j = 0; j < NJ; ++j) {
+                            acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[j], acc[0][j], 0, 0, 0);
+                            acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[j], acc[1][j], 0, 0, 0);
+                        }
                     }
-                    __builtin_amdgcn_sched_barrier(0);
-                    const int kn = std::min(ks + TPD, nks - 1);
-                    ring[d][0] = ldg16(wsrc + kn * 1024);
-                    ring[d][1] = ldg16(wsrc + kn * 1024 + 512);
-                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
             // the next layer's (or the next tile's layer-1) first k-steps load during the epilogue
@@ -202,16 +239,12 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             if (!last) prime(i + 1);
             else if (tile + (int)gridDim.x < ntiles) prime(1);
 
-            __syncthreads();  // every wave is done reading the image of layer i
+            __syncthreads();  // every wave is done reading the images of layer i
             bf16* Hs = ka->Hs[i];
             bf16* Ds = ka->Ds[i];
             const float* rb = skip ? g.rb_skip : nullptr;
-            // Outputs leave through the image: a wave writes its 8-byte pieces to LDS, then every
-            // wave copies whole 1-KB rows to HBM (one row per store instruction; scattered 8-byte
-            // stores from the accumulator layout cost ~2x the whole layer).  Pass 0 (saving only)
-            // writes cos = D_i and copies it out between two barriers; pass 1 writes sin, the next
-            // layer's input, which that layer's k-loop copies out as H_i behind its MFMAs (the last
-            // layer copies its H here).
+            // kpass 0: cos into the image (TMt = 128 when saving: it leaves between two
+            // barriers); 1: sin into the image; 2: sin into the image and cos into the D image
             auto epilogue = [&](auto kpass) {
                 constexpr int pass = decltype(kpass)::value;
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
@@ -222,7 +255,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                         const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
                         const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + f0);
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
+                        for (int j = 0; j < NJ; ++j) {
                             const int row = 32 * j + er32;
                             float v[4];
 #pragma unroll
@@ -232,45 +265,50 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) v[e] += rv[e];
                             }
-                            float y[4];
+                            const int o = act_off(row, f0 >> 3) + 8 * eh;
+                            float y[4], c[4];
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) y[e] = pass ? fast_sin(v[e]) : fast_cos(v[e]);
-                            const u32x2 o = {pack2(y[0], y[1]), pack2(y[2], y[3])};
-                            *reinterpret_cast<u32x2*>(smem + act_off(row, f0 >> 3) + 8 * eh) = o;
+                            for (int e = 0; e < 4; ++e) {
+                                if (pass == 2) fast_sincos(v[e], &y[e], &c[e]);
+                                else y[e] = pass ? fast_sin(v[e]) : fast_cos(v[e]);
+                            }
+                            *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                            if (pass == 2) *reinterpret_cast<u32x2*>(smem + IMG + o) = u32x2{pack2(c[0], c[1]), pack2(c[2], c[3])};
                         }
                         __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
                     }
-                bf16* dst = pass ? (last ? Hs : nullptr) : Ds;
-                if (dst) {  // block-uniform
-                    __syncthreads();
-                    const int ct = opaque(tid);
-#pragma unroll
-                    for (int q0 = 0; q0 < 16; q0 += 4) {
-                        u32x4 v[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int c = ct + 512 * (q0 + q);
-                            v[q] = *reinterpret_cast<const u32x4*>(smem + act_off(c >> 6, c & 63));
-                        }
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int c = ct + 512 * (q0 + q);
-                            if (p0 + (c >> 6) < g.P) *reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8) = v[q];
-                        }
-                    }
-                    if (pass == 0) __syncthreads();  // the sin pass overwrites the image
-                }
             };
-            if (Ds) epilogue(std::integral_constant<int, 0>{});  // block-uniform
-            epilogue(std::integral_constant<int, 1>{});
-            hpend = last ? nullptr : Hs;
+            if constexpr (Geo::DIMG) {
+                if (Ds) epilogue(std::integral_constant<int, 2>{});  // block-uniform
+                else epilogue(std::integral_constant<int, 1>{});
+                if (last) {
+                    __syncthreads();
+                    copy_all(smem, Hs, p0);
+                    if (Ds) copy_all(smem + IMG, Ds, p0);
+                }
+                hpend = last ? nullptr : Hs;
+                dpend = last ? nullptr : Ds;
+            } else {
+                if (Ds) {  // block-uniform
+                    epilogue(std::integral_constant<int, 0>{});
+                    __syncthreads();
+                    copy_all(smem, Ds, p0);
+                    __syncthreads();  // the sin pass overwrites the image
+                }
+                epilogue(std::integral_constant<int, 1>{});
+                if (last) {
+                    __syncthreads();
+                    copy_all(smem, Hs, p0);
+                }
+                hpend = last ? nullptr : Hs;
+            }
         }
         __syncthreads();  // the next tile restages the image and reuses the bias slots
     }
 }
 
 bool trunk_bf16_supported(int W, int L, int skip, int K0p) {
-    return W == TW && L >= 2 && L <= kTrunkMaxL && K0p <= 64 && K0p % (16 * TPD) == 0 && skip < L;
+    return W == TW && L >= 2 && L <= kTrunkMaxL && K0p <= 64 && K0p % 16 == 0 && skip < L;
 }
 
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes) {
@@ -280,9 +318,15 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     SPN_ARG(a.Hs[a.L - 1] != nullptr, "trunk_bf16: the last layer's output is required");
     if (a.P == 0) return SPNERF_OK;
     SPN_ARG(a.P < (1ll << 31) / TW, "trunk_bf16: too many points (%lld)", (long long)a.P);
-    const int ntiles = cdiv(a.P, TM);
+    bool save = false;
+    for (int i = 1; i < a.L; ++i) save |= a.Ds[i] != nullptr;
+    const int tm = g_trunk_tile ? g_trunk_tile : (save ? 64 : 128);
+    TrunkArgs ad = a;
+    ad.dbg = g_trunk_dbg;
+    const int ntiles = cdiv(a.P, tm);
     ProfScope prof("trunk_bf16", s, flop, bytes);
-    hipLaunchKernelGGL(k_trunk_bf16, dim3(std::min(ntiles, 256)), dim3(512), 0, s, a, ntiles);
+    if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else hipLaunchKernelGGL(k_trunk_bf16<128>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -11,8 +11,8 @@ import sys
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_bench"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01"
-CLASSES = {"k_gemm_nt<": "gemm_nt_f32", "k_gemm_tn<": "gemm_tn_f32", "k_gemm_nt_bf16": "gemm_nt_bf16",
-           "k_gemm_tn_bf16": "gemm_tn_bf16"}
+CLASSES = {"k_gemm_nt<": "gemm_nt_f32", "k_gemm_nt_w<": "gemm_nt_f32", "k_gemm_tn<": "gemm_tn_f32",
+           "k_gemm_nt_bf16": "gemm_nt_bf16", "k_gemm_tn_bf16": "gemm_tn_bf16", "k_trunk_bf16": "trunk_bf16"}
 for cfg in ("c2", "c3"):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):

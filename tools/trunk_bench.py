@@ -25,7 +25,11 @@ def main():
     ap.add_argument("--rays", type=int, default=1024)
     ap.add_argument("--samples", type=int, default=128)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE")
     a = ap.parse_args()
+    for o in a.option:
+        k, v = o.split("=")
+        _lib.set_option(k, int(v))
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True, precision="bf16").to(dev)
@@ -40,7 +44,7 @@ def main():
     lab = torch.randint(0, 3, (B,), device=dev)
     classes = ["trunk_bf16", "gemm_nt_bf16", "gemm_nt_f32", "heads_fwd", "encode"]
     for mode in ("save", "nosave", "sigma"):
-        for fused in (1, 0):
+        for fused in ((1,) if a.option else (1, 0)):
             _lib.set_option("fused_trunk", fused)
 
             def call():
