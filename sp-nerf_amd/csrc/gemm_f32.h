@@ -57,7 +57,9 @@ struct ReduceArgs {
 };
 
 // variant: -1 = library default (g_nt_variant); 0 = K-step 32, 1 LDS stage; 1 = 64/1;
-// 2 = 32 with double-buffered LDS; 3 = 64 double-buffered
+// 2 = 32 with double-buffered LDS; 3 = 64 double-buffered; 4 / 5 = persistent k_gemm_nt_w with
+// 256x256 / 256x128 tiles of 8 waves (one block per CU; falls back to 2 when N, n_lin or a
+// leading dimension is not 8 / 4 aligned)
 extern int g_nt_variant;
 int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant = -1);
 int tn_splits(int P, int N, int K);

@@ -670,7 +670,7 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __res
     }
 }
 
-int g_nt_variant = 2;
+int g_nt_variant = 5;  // 256x128 persistent (k_gemm_nt_w): C2 11.2 -> 10.4 ms/step over variant 2
 
 int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
