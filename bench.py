@@ -116,6 +116,83 @@ def cpu_baseline(c, seconds: float):
             "sample": f"{n} {what} of {B} rays x {s_final} samples (oracle/ref_cpu.py, torch CPU, {threads} threads)"}
 
 
+def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int = 3, dev="cuda:0"):
+    """BASELINE.json's second metric, PSNR vs the reference: the HIP path (fp32) and the oracle
+    (the reference's render path restated on the CPU, oracle/ref_cpu.py, pinned to its golden
+    fixtures) train the same SPNeRF (W=512, config-2 flags, Adam lr 5e-4) from the same init on
+    the same ray batches and random draws of the synthetic JAX_269-camera scene (JAX_214 data is
+    not in the container), then render the same held-out rays.  Returns both PSNRs and their
+    difference (the north star asks for |delta| <= 0.05 dB)."""
+    import numpy as np
+    from oracle import ref_cpu
+    from oracle.weights import ModelDims, make_weights
+    from spnerf_amd import ReplayRandom, random_source
+
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
+    dims = ModelDims(width=512)
+    w = make_weights(dims, seed)
+    model = spnerf_amd.SPNeRF(feat=512, mapping=True).to(dev)
+    model.load_state_dict({k: torch.tensor(v) for k, v in w.items()})
+    p = ref_cpu.to_params(w, requires_grad=True)
+    opt_g = torch.optim.Adam(model.parameters(), lr=5e-4)
+    opt_c = torch.optim.Adam(list(p.values()), lr=5e-4)
+    args = make_args(CONFIGS["c2"])
+    scene = synthetic_scene(4.0, seed=0, device=dev)
+    rays, rgbs = scene.rays.cpu(), scene.rgbs.cpu()
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(rays.shape[0])
+    held, pool = perm[:n_eval], perm[n_eval:]
+    S = args.n_samples
+
+    def draws(n):
+        return [("rand", rng.uniform(size=(n, S)).astype(np.float32)),
+                ("randn", rng.standard_normal((n, S)).astype(np.float32))]
+
+    def psnr(mse):
+        return float(-10.0 * np.log10(mse))
+
+    losses = []
+    for _ in range(steps):
+        idx = torch.as_tensor(rng.choice(pool, batch, replace=False))
+        dr = draws(batch)
+        with random_source(ReplayRandom(dr)):
+            res = spnerf_amd.render_rays({"coarse": model}, args, rays[idx].to(dev), None, mode="train")
+        lg = torch.mean((res["rgb_coarse"] - rgbs[idx].to(dev)) ** 2)
+        opt_g.zero_grad()
+        lg.backward()
+        opt_g.step()
+        rc = ref_cpu.render_rays(p, dims, args, rays[idx], None, None, "train", draw=ref_cpu_replay(dr))
+        lc = torch.mean((rc["rgb_coarse"] - rgbs[idx]) ** 2)
+        opt_c.zero_grad()
+        lc.backward()
+        opt_c.step()
+        losses.append((float(lg.item()), float(lc.item())))
+    idx = torch.as_tensor(held)
+    dr = draws(n_eval)
+    with torch.no_grad(), random_source(ReplayRandom(dr)):
+        eg = spnerf_amd.render_rays({"coarse": model}, args, rays[idx].to(dev), None, mode="test")["rgb_coarse"].cpu()
+    with torch.no_grad():
+        ec = ref_cpu.render_rays(p, dims, args, rays[idx], None, None, "test", draw=ref_cpu_replay(dr))["rgb_coarse"]
+    pg = psnr(float(torch.mean((eg - rgbs[idx]) ** 2)))
+    pc = psnr(float(torch.mean((ec - rgbs[idx]) ** 2)))
+    return {"psnr_gpu_db": pg, "psnr_cpu_reference_db": pc, "delta_db": pg - pc, "steps": steps, "batch_rays": batch,
+            "held_out_rays": n_eval, "loss_first_last": [losses[0], losses[-1]],
+            "max_train_loss_rel_diff": max(abs(a - b) / max(abs(b), 1e-12) for a, b in losses),
+            "setup": "W=512 config-2 flags, same init (oracle/weights.py seed 3), same batches and draws, Adam lr 5e-4; "
+                     "synthetic JAX_269-camera scene (JAX_214 absent); CPU side = oracle/ref_cpu.py"}
+
+
+def ref_cpu_replay(draws):
+    """The oracle's draw(kind, shape) callable over a recorded list of draws."""
+    it = iter(draws)
+
+    def draw(kind, shape):
+        k, arr = next(it)
+        assert k == kind and tuple(arr.shape) == tuple(shape), (k, kind, arr.shape, shape)
+        return torch.as_tensor(arr)
+    return draw
+
+
 def measured_traffic(config, kernel_class):
     """HBM bytes per launch of ``kernel_class`` from the committed PMC profile of this workload
     (tools/pmc_bench.sh + tools/traffic_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
@@ -416,6 +493,8 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
+        if a.config == "c2":
+            out["psnr_parity"] = psnr_parity(dev=dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
