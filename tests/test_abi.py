@@ -117,3 +117,16 @@ def test_seeded_init_matches_reference():
             assert abs(p.detach().double().sum().item() - ref[f"{tag}|{n}|sum"]) <= 1e-9 * max(1.0, abs(ref[f"{tag}|{n}|sum"])), n
             proj = (p.detach().double() * torch.tensor(Q[n]).double()).sum().item()
             assert abs(proj - ref[f"{tag}|{n}|proj"]) <= 1e-9 * max(1.0, abs(ref[f"{tag}|{n}|proj"])), n
+
+
+def test_kernel_options_roundtrip_and_reject_unknown_names():
+    L = _lib.lib()
+    for name in ("fused_trunk", "trunk_tile", "nt_f32_variant", "tn_f32_variant", "nt_bf16_variant"):
+        old = _lib.get_option(name)
+        _lib.set_option(name, old)
+        assert _lib.get_option(name) == old
+    assert _lib.get_option("fused_trunk") == 1 and _lib.get_option("nt_f32_variant") == 5
+    assert L.spnerf_set_option(b"no_such_option", 1) < 0
+    assert b"unknown option" in L.spnerf_last_error()
+    with pytest.raises(_lib.SpnerfError):
+        _lib.get_option("no_such_option")
