@@ -114,6 +114,14 @@ __device__ __forceinline__ float fast_cos(float x) {
     return __builtin_amdgcn_cosf(r);
 }
 
+// a copy of x the compiler cannot see through: lane-derived addresses computed from it are
+// recomputed where used instead of being hoisted out of every loop and kept live across the
+// MFMA main loop (where the accumulators need the registers)
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // order LDS accesses of one wavefront (LDS is in order per wave; this stops the compiler
 // from moving accesses across the point)
 __device__ __forceinline__ void wave_lds_sync() {

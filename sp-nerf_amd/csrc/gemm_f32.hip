@@ -323,7 +323,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         }
     };
 
-    const int cq = (lane & 7) * 8;
     constexpr int SLD = 68;
     static_assert(WGM * WGN * 32 * SLD <= 2 * (BM + BN) * LK, "epilogue staging fits in the LDS");
     float* stage = smem + wid * (32 * SLD);
@@ -354,6 +353,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         const bool more = tn < ntiles;
         gload(r0, more ? tn : t, 0);  // the next tile's first K-step loads during the epilogue
 
+        // epilogue lane geometry from an opaque lane id (recomputed per tile, not held live
+        // across the main loop)
+        const int el = opaque(lane), cq = (el & 7) * 8, er32 = el & 31, eh = el >> 5, erow = el >> 3;
         const int col0 = bn + wc * NJ * 32;
         float bias8[NJ / 2][8], r1v8[NJ / 2][8];
 #pragma unroll
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
                 const int col = col0 + 64 * jp + cq;
                 const bool colok = col < g.N;
                 const int colc = colok ? col : g.N - 8;
-                const int rbase = bm + wr * MI * 32 + i * 32 + (lane >> 3);
+                const int rbase = bm + wr * MI * 32 + i * 32 + erow;
                 f32x4 dm[4][2];
                 float r1a[4];
 #pragma unroll
@@ -389,12 +391,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
                 for (int j2 = 0; j2 < 2; ++j2)
 #pragma unroll
                     for (int r = 0; r < 16; ++r)
-                        stage[((r & 3) + 8 * (r >> 2) + 4 * h) * SLD + j2 * 32 + r32] = acc[i][2 * jp + j2][r];
+                        stage[((r & 3) + 8 * (r >> 2) + 4 * eh) * SLD + j2 * 32 + er32] = acc[i][2 * jp + j2][r];
                 wave_lds_sync();
                 const bool sine_cols = g.act == 1 && col >= g.n_lin;  // n_lin is a multiple of 8
 #pragma unroll
                 for (int q4 = 0; q4 < 4; ++q4) {
-                    const int rr = (lane >> 3) + 8 * q4;
+                    const int rr = erow + 8 * q4;
                     const int row = rbase + 8 * q4;
                     float v[8], d[8];
 #pragma unroll

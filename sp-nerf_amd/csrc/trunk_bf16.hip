@@ -59,14 +59,6 @@ __device__ __forceinline__ int act_off(int row, int ch) { return row * 1024 + ((
 // lane group on distinct 16-B slots of the bank row
 __device__ __forceinline__ int x0_rel(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 
-// a copy of x the compiler cannot see through: lane-derived addresses are recomputed in each
-// region (staging, k-loop, epilogue) instead of being hoisted out of all loops and kept live
-// across the k-loop, where the accumulators and the weight ring need the registers
-__device__ __forceinline__ int opaque(int x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
 template <int TMt>
 __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     using Geo = TrunkGeo<TMt>;
