@@ -134,7 +134,8 @@ int32_t spnerf_rpc_rays(const double* rpc, double downscale, double min_alt, dou
 /* ---- kernel selection (no reference counterpart: A/B switches for tests and benches) ----
  *      "fused_trunk" (1 = bf16 trunk layers 1..L-1 in one persistent LDS-resident launch,
  *      the default; 0 = layer by layer), "nt_f32_variant", "tn_f32_variant",
- *      "nt_bf16_variant" (GEMM tilings).  Process-wide; unknown names fail. */
+ *      "nt_bf16_variant" (GEMM tilings), "heads_variant" (1 = prefetching
+ *      output heads, the default; 0 = one point at a time).  Process-wide; unknown names fail. */
 int32_t spnerf_set_option(const char* name, int32_t value);
 int32_t spnerf_get_option(const char* name, int32_t* value);
 

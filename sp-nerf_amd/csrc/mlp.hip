@@ -230,6 +230,187 @@ __global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs<T> a, PackedOffs k)
     }
 }
 
+int g_heads_variant = 1;  // 0 = the one-point-at-a-time k_heads_fwd (ablation)
+
+// Sum over the wavefront, returned to every lane: DPP adds inside each row of 16 lanes, then
+// the four row sums read out as scalars (no LDS traffic, unlike a shuffle butterfly).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_total(float v) {
+    v += dpp_f<0xb1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4e>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x124>(v);  // row_ror:4
+    v += dpp_f<0x128>(v);  // row_ror:8
+    const int b = __float_as_int(v);
+    return (__int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16))) +
+           (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
+}
+
+template <typename T> struct RawOf;
+template <> struct RawOf<float> { using type = f32x4; };
+template <> struct RawOf<bf16> { using type = u32x2; };
+template <typename T>
+__device__ __forceinline__ typename RawOf<T>::type ld_raw(const T* p) {
+    return *reinterpret_cast<const typename RawOf<T>::type*>(p);
+}
+__device__ __forceinline__ f32x4 raw_f32(f32x4 v) { return v; }
+__device__ __forceinline__ f32x4 raw_f32(u32x2 v) {
+    return f32x4{__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u), __uint_as_float(v[1] << 16),
+                 __uint_as_float(v[1] & 0xffff0000u)};
+}
+__device__ __forceinline__ float dot4(f32x4 a, f32x4 b) { return (a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3]); }
+
+// The rows one point's heads read: its last trunk row (σ), sun_v.3 output, rgb / β hidden
+// (Q) and semantic hidden (G); lane `l` holds columns 4l + 256i.
+template <typename T, int NC, int NH>
+struct HeadRows {
+    typename RawOf<T>::type hl[NC], s3[NH], r1[NH], b1[NH], m1[NH];
+};
+
+// Narrow output heads (spnerf.py:333-367): σ = softplus, albedo = sigmoid·1.002−0.001,
+// sun = sigmoid, β = softplus, semantic logits; sky broadcast per ray.  One wavefront per
+// point, W ≤ 256·NC.  HBM-latency bound, so the rows of point p + nw are in flight while
+// point p's dot products and DPP reductions run: two register sets in turn (no copies, which
+// would wait on the loads), a fixed number of row loads per point (rows a mode does not use
+// are re-reads of the σ row, so the wait counts are static), and every other operand in
+// registers or LDS (σ / sun / rgb / β weights in VGPRs, semantic weights staged in LDS) so no
+// vector-memory load is issued behind the prefetch.  A point's output row leaves as one
+// coalesced store.
+template <typename T, int NC>
+__global__ __launch_bounds__(256) void k_heads_fwd_v(HeadsArgs<T> a, PackedOffs k) {
+    constexpr int NH = (NC + 1) / 2;
+    extern __shared__ float wsem[];  // [C][H] semantic weights + [C] biases (mode 0, semantic model)
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const Dims& d = a.d;
+    const float* Pk = a.packed;
+    const int W = d.W, H = d.H;
+    const bool sun_on = a.mode != 1, full = a.mode == 0, beta = full && d.beta, sem = full && d.sem;
+    if (sem) {
+        for (int i = threadIdx.x; i < d.C * H; i += 256) wsem[i] = Pk[k.Wm2 + i];
+        if (threadIdx.x < d.C) wsem[d.C * H + threadIdx.x] = Pk[k.bm2 + threadIdx.x];
+        __syncthreads();
+    }
+    int cw[NC], ch[NH];
+    bool vw[NC], vh[NH];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+        vw[i] = 4 * lane + 256 * i < W;
+        cw[i] = vw[i] ? 4 * lane + 256 * i : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        vh[i] = 4 * lane + 256 * i < H;
+        ch[i] = vh[i] ? 4 * lane + 256 * i : 0;
+    }
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 wsg[NC], w4[NH], wr[3][NH], wb[NH];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) wsg[i] = vw[i] ? ld4(Pk + k.wsig + cw[i]) : z4;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        w4[i] = vh[i] && sun_on ? ld4(Pk + k.ws4 + ch[i]) : z4;
+        for (int c = 0; c < 3; ++c) wr[c][i] = vh[i] && full ? ld4(Pk + k.Wr2 + c * H + ch[i]) : z4;
+        wb[i] = vh[i] && beta ? ld4(Pk + k.wb2 + ch[i]) : z4;
+    }
+    const float bsig = Pk[k.bsig];
+    const float bs4 = sun_on ? Pk[k.bs4] : 0.f;
+    const float br0 = full ? Pk[k.br2] : 0.f, br1 = full ? Pk[k.br2 + 1] : 0.f, br2 = full ? Pk[k.br2 + 2] : 0.f;
+    const float bb = beta ? Pk[k.bb2] : 0.f;
+
+    // row bases of point p; unused rows alias the σ row
+    auto load = [&](int64_t p, HeadRows<T, NC, NH>& r) {
+        const T* hl = a.HL + p * W;
+        const T* q = a.Q + p * d.NQ;
+        const T* s3 = sun_on ? a.S3 + p * H : hl;
+        const T* r1 = full ? q + H : hl;
+        const T* b1 = beta ? q + 2 * H : hl;
+        const T* m1 = sem ? a.G + p * d.NG + W : hl;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) r.hl[i] = ld_raw(hl + cw[i]);
+#pragma unroll
+        for (int i = 0; i < NH; ++i) {
+            r.s3[i] = ld_raw(s3 + ch[i]);
+            r.r1[i] = ld_raw(r1 + ch[i]);
+            r.b1[i] = ld_raw(b1 + ch[i]);
+            r.m1[i] = ld_raw(m1 + ch[i]);
+        }
+    };
+
+    auto body = [&](int64_t p, const HeadRows<T, NC, NH>& cur, HeadRows<T, NC, NH>& nxt) {
+        // this point's sky colour before the prefetch, so waiting on it leaves the prefetch in flight
+        float sky = 0.f;
+        if (full && lane >= 5 && lane <= 7) sky = a.sky[(int64_t)((int)p / a.S) * 4 + lane - 5];
+        load(std::min(p + nw, a.P - 1), nxt);
+        // lane-partial dot products (masked columns carry zero weights)
+        float ps = 0.f, pu = 0.f, pr0 = 0.f, pr1 = 0.f, pr2 = 0.f, pb = 0.f;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) ps += dot4(raw_f32(cur.hl[i]), wsg[i]);
+#pragma unroll
+        for (int i = 0; i < NH; ++i) {
+            pu += dot4(raw_f32(cur.s3[i]), w4[i]);
+            const f32x4 r = raw_f32(cur.r1[i]);
+            pr0 += dot4(r, wr[0][i]);
+            pr1 += dot4(r, wr[1][i]);
+            pr2 += dot4(r, wr[2][i]);
+            pb += dot4(raw_f32(cur.b1[i]), wb[i]);
+        }
+        const float spre = wave_total(ps) + bsig;
+        float ov = lane == 3 ? softplusf_(spre) : 0.f;  // this lane's output column
+        float hv = spre;                                // this lane's hsave column (lane 0: σ pre-activation)
+        float* o = a.out + p * d.NO;
+        float* hs = a.hsave + p * 8;
+        if (!sun_on) {
+            if (lane == 3) o[3] = ov;
+            if (lane == 0) hs[0] = hv;
+            return;
+        }
+        const float sun = sigmoidf_(wave_total(pu) + bs4);
+        if (lane == 4) ov = hv = sun;
+        if (full) {
+            const float g0 = sigmoidf_(wave_total(pr0) + br0), g1 = sigmoidf_(wave_total(pr1) + br1),
+                        g2 = sigmoidf_(wave_total(pr2) + br2);
+            const float g = lane == 0 ? g0 : lane == 1 ? g1 : g2;
+            if (lane < 3) ov = __fsub_rn(__fmul_rn(g, 1.002f), 0.001f);
+            if (lane >= 1 && lane <= 3) hv = lane == 1 ? g0 : lane == 2 ? g1 : g2;  // hsave[1 + c] = rgb c
+            if (lane >= 5 && lane <= 7) ov = sky;
+            if (beta) {
+                const float bpre = wave_total(pb) + bb;
+                if (lane == 8) ov = softplusf_(bpre);
+                if (lane == 5) hv = bpre;
+            }
+            if (sem) {
+                for (int c = 0; c < d.C; ++c) {
+                    float pm = 0.f;
+#pragma unroll
+                    for (int i = 0; i < NH; ++i)
+                        pm += dot4(raw_f32(cur.m1[i]), vh[i] ? *reinterpret_cast<const f32x4*>(wsem + c * H + ch[i]) : z4);
+                    const float v = wave_total(pm) + wsem[d.C * H + c];
+                    if (lane == d.sem_col + c) ov = v;
+                }
+            }
+        }
+        if (lane < d.NO) o[lane] = ov;
+        if (lane == 0 || lane == 4 || (full && (lane <= 3 || (lane == 5 && d.beta)))) hs[lane] = hv;
+    };
+
+    // the point index is wave-uniform: keep it (and every row address) in scalar registers;
+    // P < 2^31 (spnerf_mlp_forward checks it)
+    int64_t p = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+    if (p >= a.P) return;
+    // two register sets in turn (a third, prefetching two points ahead, measured no faster)
+    HeadRows<T, NC, NH> ra, rb;
+    load(p, ra);
+    for (;;) {
+        body(p, ra, rb);
+        if ((p += nw) >= a.P) break;
+        body(p, rb, ra);
+        if ((p += nw) >= a.P) break;
+    }
+}
+
 template <typename T>
 struct HeadsBwdArgs {
     const float* packed; Dims d;
@@ -795,13 +976,20 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
         const int grid = (int)std::min<int64_t>(cdiv(P, 4), 8192);
         ProfScope prof("heads_fwd", s, 2.0 * P * (W + (mode != 1 ? 4 * H + H * d.C : 0)),
                        (d.bf ? 2.0 : 4.0) * P * (W + 3 * H) + 4.0 * P * d.NO);
-        if (d.bf) {
-            HeadsArgs<bf16> a{packed, d, c.hb(hl), c.hb(c.w.G), c.hb(c.w.Q), c.hb(s3), c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode};
-            hipLaunchKernelGGL(k_heads_fwd<bf16>, dim3(grid), dim3(256), 0, s, a, (PackedOffs)c.k);
-        } else {
-            HeadsArgs<float> a{packed, d, c.at(hl), c.at(c.w.G), c.at(c.w.Q), c.at(s3), c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode};
-            hipLaunchKernelGGL(k_heads_fwd<float>, dim3(grid), dim3(256), 0, s, a, (PackedOffs)c.k);
-        }
+        const int nc = g_heads_variant == 0 ? 0 : cdiv(W, 256);
+        const size_t lds = mode == 0 && d.sem ? sizeof(float) * d.C * (H + 1) : 0;  // ≤ 32 × 513 floats when nc ≤ 4
+        auto launch = [&](auto a) {
+            using T = std::remove_cv_t<std::remove_pointer_t<decltype(a.HL)>>;
+            switch (nc) {
+                case 1: hipLaunchKernelGGL((k_heads_fwd_v<T, 1>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k); break;
+                case 2: hipLaunchKernelGGL((k_heads_fwd_v<T, 2>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k); break;
+                case 3: hipLaunchKernelGGL((k_heads_fwd_v<T, 3>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k); break;
+                case 4: hipLaunchKernelGGL((k_heads_fwd_v<T, 4>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k); break;
+                default: hipLaunchKernelGGL(k_heads_fwd<T>, dim3(grid), dim3(256), 0, s, a, (PackedOffs)c.k);
+            }
+        };
+        if (d.bf) launch(HeadsArgs<bf16>{packed, d, c.hb(hl), c.hb(c.w.G), c.hb(c.w.Q), c.hb(s3), c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode});
+        else launch(HeadsArgs<float>{packed, d, c.at(hl), c.at(c.w.G), c.at(c.w.Q), c.at(s3), c.at(c.w.sky), out, c.at(c.w.hsave), P, S, mode});
         SPN_HIP(hipGetLastError());
     }
     return SPNERF_OK;
@@ -1029,6 +1217,7 @@ static int* option_slot(const char* name) {
     if (n == "nt_f32_variant") return &g_nt_variant;
     if (n == "tn_f32_variant") return &g_tn_variant;
     if (n == "nt_bf16_variant") return &g_nt16_variant;
+    if (n == "heads_variant") return &g_heads_variant;
     return nullptr;
 }
 
