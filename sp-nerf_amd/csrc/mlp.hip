@@ -30,7 +30,9 @@ namespace spn {
 struct PackPiece {
     const float* src;
     // bf: 1 = bf16 destination (dst in bf16 units); 2 = bf16 in the fused trunk's MFMA fragment
-    // order (trunk_frag_off, dst_ld = the layer's padded K)
+    // order (trunk_frag_off, dst_ld = the layer's padded K); 3 = split into bf16 planes
+    // [hi | hi | lo | lo] of width dst_ld / 4 each (hi = bf16(v), lo = bf16(v − hi)); 4 = the
+    // same planes in the fused trunk's fragment order (dst_ld = 4·K0p)
     int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;
     int64_t dst;
 };
@@ -46,6 +48,15 @@ __global__ void k_pack(PackArgs a) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int r = (int)(i / pc.cols), c = (int)(i % pc.cols);
         const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
+        if (pc.bf >= 3) {
+            bf16* dst = reinterpret_cast<bf16*>(a.packed) + pc.dst;
+            const int kp = pc.dst_ld / 4;
+            const bf16 hi = (bf16)v, lo = (bf16)(v - (float)hi);
+            const bf16 pl[4] = {hi, hi, lo, lo};
+            for (int j = 0; j < 4; ++j)
+                dst[pc.bf == 4 ? trunk_frag_off(r, c + j * kp, pc.dst_ld) : (int64_t)r * pc.dst_ld + c + j * kp] = pl[j];
+            continue;
+        }
         const int64_t o = pc.dst + (pc.bf == 2        ? trunk_frag_off(r, c, pc.dst_ld)
                                     : pc.transpose ? (int64_t)c * pc.dst_ld + r
                                                    : (int64_t)r * pc.dst_ld + c);
@@ -55,10 +66,13 @@ __global__ void k_pack(PackArgs a) {
 }
 
 // X0[p][c]: positional encoding of xyz = o + dir*z (rendering.py:147; spnerf.py:32-37), one
-// output element per thread.  o + dir*z is evaluated as two rounded ops like the reference
+// output element per thread.  Each of the fp32 row X0, its bf16 copy X0b and its split planes
+// X0s = [hi | lo | hi | lo] (hi = bf16(v), lo = bf16(v − hi), row length 4·K0p) is written when
+// non-null.  o + dir*z is evaluated as two rounded ops like the reference
 // (no FMA contraction: sin(2^9 x) amplifies a 1-ulp difference in x by 512).
 __global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, const float* __restrict__ z, int S,
-                         int64_t P, int n_freq, int K0, int K0p, float* __restrict__ X0, bf16* __restrict__ X0b) {
+                         int64_t P, int n_freq, int K0, int K0p, float* __restrict__ X0, bf16* __restrict__ X0b,
+                         bf16* __restrict__ X0s) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= P * K0p) return;
     const int64_t p = i / K0p;
@@ -76,8 +90,17 @@ __global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, co
             v = j < 3 ? sinf(arg) : cosf(arg);
         }
     }
-    X0[i] = v;
-    if (X0b) X0b[i] = (bf16)v;
+    if (X0) X0[i] = v;
+    const bf16 hi = (bf16)v;
+    if (X0b) X0b[i] = hi;
+    if (X0s) {
+        bf16* r = X0s + p * 4 * K0p + c;
+        const bf16 lo = (bf16)(v - (float)hi);
+        r[0] = hi;
+        r[K0p] = lo;
+        r[2 * K0p] = hi;
+        r[3 * K0p] = lo;
+    }
 }
 
 struct RayFwdArgs {
@@ -231,6 +254,9 @@ __global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs<T> a, PackedOffs k)
 }
 
 int g_heads_variant = 1;  // 0 = the one-point-at-a-time k_heads_fwd (ablation)
+int g_l0_split = 1;       // bf16 MLP: fc_net.0 on bf16 hi/lo planes (0 = fp32 MFMA GEMM)
+int g_trunk_l0 = 1;       // ... and inside the fused trunk launch: 1 = when nothing is saved (inference;
+                          // saving, 64-point tiles, it measured slower than the separate GEMM), 2 = always
 
 // Sum over the wavefront, returned to every lane: DPP adds inside each row of 16 lanes, then
 // the four row sums read out as scalars (no LDS traffic, unlike a shuffle butterfly).
@@ -702,6 +728,8 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
     SPN_TRY(piece(x.k2W, 0, 3, H, k.Wk2, H, 0));
     SPN_TRY(piece(x.k2b, 0, 1, 3, k.bk2, 3, 0));
     if (d.bf) {  // bf16 GEMM operands (same shapes as their fp32 counterparts above)
+        SPN_TRY(piece(x.fcW[0], 0, W, d.K0, k.W0s16, 4 * k.Kp[0], 0, 3));
+        if (k.Wf16[0] >= 0) SPN_TRY(piece(x.fcW[0], 0, W, d.K0, k.Wf16[0], 4 * k.Kp[0], 0, 4));
         for (int i = 1; i < d.L; ++i) {
             const int kreal = i == d.skip ? W + d.K0 : W;
             SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wt16[i], k.Kp[i], 0, 1));
@@ -824,6 +852,15 @@ static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int M
 
 // Trunk + G/Q/sun_v GEMMs of the forward (spnerf.py:323-355).  In the bf16 MLP, layer 0 stays
 // an fp32 GEMM (sin(30·x) amplifies operand rounding 30x) that writes bf16 H_1 / D_1.
+// bf16 MLP: layer 0 runs inside the fused trunk launch (reading the fp32 PE rows itself)
+static bool fused_trunk_on(const Ctx& c) {
+    return c.d.bf && g_fused_trunk && !c.k.Wf16.empty() && c.k.Wf16[1] >= 0;
+}
+static bool trunk_l0_on(const Ctx& c, bool save) {
+    return fused_trunk_on(c) && g_l0_split && (g_trunk_l0 == 2 || (g_trunk_l0 == 1 && !save)) && c.k.Wf16[0] >= 0 &&
+           trunk_l0_supported(c.d.K0p, save);
+}
+
 template <typename T>
 static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
     using G = Gemms<T>;
@@ -835,25 +872,32 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
     const T* X0 = BF ? G::buf(c, c.w.X0b) : G::buf(c, c.w.X0);
     const T* h = nullptr;
     T* HL = nullptr;
-    const bool fused = BF && g_fused_trunk && !c.k.Wf16.empty() && c.k.Wf16[1] >= 0;
+    const bool fused = BF && fused_trunk_on(c);
+    const int first = fused && trunk_l0_on(c, save) ? 0 : 1;  // first layer of the fused launch
     for (int i = 0; i < d.L; ++i) {
-        if (fused && i == 1) {
-            // layers 1 .. L-1 in one persistent launch, activations resident in LDS
+        if (fused && i == first) {
+            // layers first .. L-1 in one persistent launch, activations resident in LDS
             TrunkArgs a;
             a.H1 = reinterpret_cast<const bf16*>(h);
             a.X0b = c.hb(c.w.X0b);
+            if (first == 0) {
+                a.X0 = c.at(c.w.X0);
+                a.rb0 = d.sem ? c.at(c.w.rb0) : nullptr;
+            }
             double ksum = 0.0;
-            for (int l = 1; l < d.L; ++l) {
+            for (int l = first; l < d.L; ++l) {
                 a.Wf[l] = c.pk16(c.k.Wf16[l]);
                 a.bias[l] = c.pk(c.k.bt[l]);
                 a.Hs[l] = save ? c.hb(c.w.Hb[l]) : (l == d.L - 1 ? c.hb(c.w.Hb[l & 1]) : nullptr);
                 a.Ds[l] = save ? c.hb(c.w.Db[l]) : nullptr;
-                ksum += c.k.Kp[l];
+                ksum += l == 0 ? 4 * d.K0p : c.k.Kp[l];
             }
             a.rb_skip = d.sem ? c.at(c.w.rb4) : nullptr;
             a.P = P; a.S = S; a.L = d.L; a.skip = d.skip; a.K0p = d.K0p;
-            // algorithmic HBM bytes: the H_1 and PE tiles in, H (and D) of every layer out when saving
-            const double bytes = 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0)) + 2.0 * P * W * (save ? 2.0 * (d.L - 1) : 1.0);
+            // algorithmic HBM bytes: the first layer's input (fp32 PE, or H_1 and the bf16 PE)
+            // in, H (and D) of every layer out when saving
+            const double in = first == 0 ? 4.0 * P * d.K0p : 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0));
+            const double bytes = in + 2.0 * P * W * (save ? 2.0 * (d.L - first) : 1.0);
             SPN_TRY(trunk_bf16(a, s, 2.0 * P * W * ksum, bytes));
             HL = reinterpret_cast<T*>(a.Hs[d.L - 1]);
             break;
@@ -861,7 +905,21 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
         T* dst = save ? G::buf(c, c.w.Hb[i]) : G::buf(c, c.w.Hb[i & 1]);
         T* dd = save ? G::buf(c, c.w.Db[i]) : nullptr;
         const float* rb = (d.sem && (i == 0 || i == d.skip)) ? c.at(i == 0 ? c.w.rb0 : c.w.rb4) : nullptr;
-        if (i == 0) {
+        if (i == 0 && BF && g_l0_split) {
+            // fc_net.0 on MFMA bf16 as (x_hi + x_lo)·(w_hi + w_lo), K = 4·K0p: relative error
+            // ≈ 2^-17 per product (the split's remainder) against the fp32 GEMM's 2^-24, far
+            // inside the bf16 output's 2^-9, at bf16 MFMA rates instead of fp32 ones
+            NT16Args g;
+            g.A = c.hb(c.w.X0s); g.lda = 4 * d.K0p; g.K1 = 4 * d.K0p;
+            g.B = c.pk16(c.k.W0s16); g.ldb = 4 * d.K0p;
+            g.C = reinterpret_cast<bf16*>(dst); g.ldc = W;
+            g.M = (int)P; g.N = W; g.K = 4 * d.K0p;
+            g.bias = c.pk(c.k.bt[0]);
+            if (rb) { g.rowbias = rb; g.ld_rb = W; g.rows_per_ray = S; }
+            g.act = 1; g.w0 = 30.f; g.n_lin = 0;
+            if (save) { g.Dout = reinterpret_cast<bf16*>(dd); g.ld_dout = W; }
+            SPN_TRY(gemm_nt_bf16(g, s));
+        } else if (i == 0) {
             NTArgs g;
             g.A = c.at(c.w.X0); g.lda = d.K0p; g.K1 = d.K0p;
             g.B = c.pk(c.k.Wt[0]); g.ldb = d.K0p;
@@ -962,9 +1020,14 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
     // positional encoding (fp32 for layer 0, plus a bf16 copy for the skip layer / dW_0)
     {
         const int64_t n = P * d.K0p;
-        ProfScope prof("encode", s, 0.0, (d.bf ? 6.0 : 4.0) * n);
+        // bf16 MLP, layer 0 on bf16 planes: a separate GEMM reads the planes X0s; inside the
+        // fused trunk it splits the fp32 rows itself
+        const bool l0t = trunk_l0_on(c, save);
+        const bool planes = d.bf && g_l0_split && !l0t;
+        ProfScope prof("encode", s, 0.0, (planes ? 10.0 : 4.0 + (d.bf ? 2.0 : 0.0)) * n);
         hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rays, rs, dir_off, z, S, P,
-                           d.K0 == 3 ? 0 : d.K0 / 6, d.K0, d.K0p, c.at(c.w.X0), d.bf ? c.hb(c.w.X0b) : nullptr);
+                           d.K0 == 3 ? 0 : d.K0 / 6, d.K0, d.K0p, planes ? nullptr : c.at(c.w.X0),
+                           d.bf ? c.hb(c.w.X0b) : nullptr, planes ? c.hb(c.w.X0s) : nullptr);
         SPN_HIP(hipGetLastError());
     }
     if (d.bf) SPN_TRY(forward_gemms<bf16>(c, save, mode, s));
@@ -1218,6 +1281,8 @@ static int* option_slot(const char* name) {
     if (n == "tn_f32_variant") return &g_tn_variant;
     if (n == "nt_bf16_variant") return &g_nt16_variant;
     if (n == "heads_variant") return &g_heads_variant;
+    if (n == "l0_split") return &g_l0_split;
+    if (n == "trunk_l0") return &g_trunk_l0;
     return nullptr;
 }
 

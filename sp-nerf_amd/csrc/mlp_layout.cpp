@@ -152,7 +152,7 @@ Packed packed_layout(const Dims& d) {
         for (int i = 0; i < d.L; ++i) {
             k.Wt16.push_back(i == 0 ? -1 : take16((int64_t)W * k.Kp[i]));
             k.WTt16.push_back(i == 0 ? -1 : take16((int64_t)W * W));
-            k.Wf16.push_back(i == 0 || !fused ? -1 : take16((int64_t)W * k.Kp[i]));
+            k.Wf16.push_back(!fused ? -1 : take16((int64_t)W * (i == 0 ? 4 * k.Kp[0] : k.Kp[i])));
         }
         k.WG16 = take16((int64_t)d.NG * W);
         k.WGT16 = take16((int64_t)W * d.NG);
@@ -162,6 +162,7 @@ Packed packed_layout(const Dims& d) {
         k.Ws2T16 = take16((int64_t)H * H);
         k.Ws3_16 = take16((int64_t)H * H);
         k.Ws3T16 = take16((int64_t)H * H);
+        k.W0s16 = take16((int64_t)W * 4 * k.Kp[0]);
     }
     k.total = off;
     return k;
@@ -184,6 +185,7 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
     const int W = d.W, H = d.H;
     w.X0 = take(P * d.K0p);
     w.X0b = d.bf ? act(P * d.K0p) : -1;
+    w.X0s = d.bf ? act(P * 4 * d.K0p) : -1;
     if (save) {
         for (int i = 0; i < d.L; ++i) w.Hb.push_back(act(P * W));
         for (int i = 0; i < d.L; ++i) w.Db.push_back(act(P * W));

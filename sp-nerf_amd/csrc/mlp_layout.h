@@ -52,13 +52,16 @@ struct PackedOffs {
     // bf16 copies (cfg.dtype == 1), offsets in bf16 elements from the packed base: the G, Q and
     // sun_v 2/3 matrices (forward and transposed)
     int64_t WG16 = -1, WGT16 = -1, WQ16 = -1, WQT16 = -1, Ws2_16 = -1, Ws2T16 = -1, Ws3_16 = -1, Ws3T16 = -1;
+    // fc_net.0 as four bf16 planes [W][4·K0p] = [hi | hi | lo | lo] for the split layer 0
+    int64_t W0s16 = -1;
     int64_t total;
 };
 struct Packed : PackedOffs {
     std::vector<int64_t> Wt, bt, WTt;   // trunk: forward [W][Kp_i], bias, transposed h-part [W][W]
     std::vector<int> Kp;                // padded K of each trunk layer
     std::vector<int64_t> Wt16, WTt16;   // bf16 trunk layers 1.. (bf16 units), -1 for layer 0
-    std::vector<int64_t> Wf16;          // the same in MFMA fragment order for the fused trunk (-1: none)
+    std::vector<int64_t> Wf16;          // the same in MFMA fragment order for the fused trunk (-1: none);
+                                        // layer 0: the split planes [hi | hi | lo | lo], K = 4·K0p
 };
 Packed packed_layout(const Dims& d);
 
@@ -68,6 +71,7 @@ Packed packed_layout(const Dims& d);
 struct WS {
     int64_t P, B;
     int64_t X0, X0b;
+    int64_t X0s;                        // bf16 MLP: encoded input as [hi | lo | hi | lo] bf16 planes, [P][4·K0p]
     std::vector<int64_t> Hb, Db;        // H_1..H_L (save) or 3 ping-pong buffers; D_1..D_L
     int64_t G, DG, Q, DQ, S2, DS2, S3, DS3, hsave;
     int64_t rb0, rb4, rbQ, skyh, sky;

@@ -70,6 +70,10 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     const int x0ch = g.K0p >> 3;
     constexpr int nmain = TW / 16;  // k-steps over the activation image
     const int ntail = g.K0p >> 4;   // extra k-steps over the PE at the skip layer
+    const bool l0 = g.X0 != nullptr;  // layer 0 in this launch (block-uniform)
+    const int first = l0 ? 0 : 1;
+    const int nk0 = g.K0p >> 2;     // layer 0's k-steps: the 4·K0p split planes
+    auto nks_of = [&](int i) { return i == 0 ? nk0 : nmain + (i == g.skip ? ntail : 0); };
     const int sw = r32 & 15;
     // per-layer pointers indexed by the (runtime) layer: scalar loads straight from the kernarg
     // segment (indexing the by-value struct copies its arrays to scratch)
@@ -78,10 +82,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 
     u32x4 ring[TPD][2];
     // wave w's fragment stream of layer i: k-step ks at + ks * 1024, feature tile a at + 512 * a
-    auto wstream = [&](int i) {
-        const int nks = nmain + (i == g.skip ? ntail : 0);
-        return ka->Wf[i] + (int64_t)w * nks * 1024 + lane * 8;
-    };
+    auto wstream = [&](int i) { return ka->Wf[i] + (int64_t)w * nks_of(i) * 1024 + lane * 8; };
     auto prime = [&](int i) {
         const bf16* src = wstream(i);
 #pragma unroll
@@ -116,12 +117,35 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
-    prime(1);
+    prime(first);
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TMt;
         const int st = opaque(tid);
-        // stage the layer-1 input and the PE tile; rows past P read a clamped row (their
+        // stage the first layer's input and the PE tile; rows past P read a clamped row (their
         // outputs are never stored)
+        if (l0) {
+            // 8 fp32 PE values per unit → 16-B hi and lo chunks: image columns [hi | lo | hi | lo]
+            // (layer 0's B operand) and the skip layer's PE tile (= hi, as X0b)
+            for (int u = st; u < TMt * x0ch; u += 512) {
+                const int row = u / x0ch, q = u % x0ch;
+                const float* src = g.X0 + std::min<int64_t>(p0 + row, g.P - 1) * g.K0p + q * 8;
+                const f32x4 v0 = ld4(src), v1 = ld4(src + 4);
+                float hf[8], lf[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float x = e < 4 ? v0[e] : v1[e - 4];
+                    hf[e] = (float)(bf16)x;
+                    lf[e] = x - hf[e];
+                }
+                const u32x4 hi = {pack2(hf[0], hf[1]), pack2(hf[2], hf[3]), pack2(hf[4], hf[5]), pack2(hf[6], hf[7])};
+                const u32x4 lo = {pack2(lf[0], lf[1]), pack2(lf[2], lf[3]), pack2(lf[4], lf[5]), pack2(lf[6], lf[7])};
+                *reinterpret_cast<u32x4*>(smem + act_off(row, q)) = hi;
+                *reinterpret_cast<u32x4*>(smem + act_off(row, x0ch + q)) = lo;
+                *reinterpret_cast<u32x4*>(smem + act_off(row, 2 * x0ch + q)) = hi;
+                *reinterpret_cast<u32x4*>(smem + act_off(row, 3 * x0ch + q)) = lo;
+                if (g.skip > 0) *reinterpret_cast<u32x4*>(sx0 + x0_rel(row, q)) = hi;
+            }
+        } else {
 #pragma unroll
         for (int q0 = 0; q0 < CPT; q0 += 8) {
             u32x4 v[8];
@@ -143,13 +167,15 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                     ldg16(g.X0b + std::min<int64_t>(p0 + row, g.P - 1) * g.K0p + ch * 8);
             }
         }
+        }
 
         bf16* hpend = nullptr;  // H (and D) of the previous layer: copied out during this k-loop
         bf16* dpend = nullptr;
-        for (int i = 1; i < g.L; ++i) {
+        for (int i = first; i < g.L; ++i) {
             const bool skip = i == g.skip;
             const bf16* wsrc = wstream(i);
-            const int nks = nmain + (skip ? ntail : 0);
+            const int nks = nks_of(i);
+            const int nkm = i == 0 ? nk0 : nmain;  // k-steps over the image
             float* sb = sbias + (i & 1) * TW;  // slot (i-1)&1 may still be read by the previous epilogue
             sb[tid] = ka->bias[i][tid];
             f32x16 acc[2][NJ];
@@ -169,7 +195,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
 #pragma unroll 1
-            for (int ks0 = 0; ks0 < nmain; ks0 += TPD) {
+            for (int ks0 = 0; ks0 < nkm; ks0 += TPD) {
 #pragma unroll
                 for (int d = 0; d < TPD; ++d) {
                     const int ks = ks0 + d;
@@ -229,12 +255,13 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             // the next layer's (or the next tile's layer-1) first k-steps load during the epilogue
             const bool last = i == g.L - 1;
             if (!last) prime(i + 1);
-            else if (tile + (int)gridDim.x < ntiles) prime(1);
+            else if (tile + (int)gridDim.x < ntiles) prime(first);
 
             __syncthreads();  // every wave is done reading the images of layer i
             bf16* Hs = ka->Hs[i];
             bf16* Ds = ka->Ds[i];
-            const float* rb = skip ? g.rb_skip : nullptr;
+            const float* rb = i == 0 ? g.rb0 : (skip ? g.rb_skip : nullptr);
+            const float w0 = i == 0 ? 30.f : 1.f;  // SIREN w0 of fc_net.0 (×1 elsewhere: exact)
             // kpass 0: cos into the image (TMt = 128 when saving: it leaves between two
             // barriers); 1: sin into the image; 2: sin into the image and cos into the D image
             auto epilogue = [&](auto kpass) {
@@ -261,8 +288,10 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                             float y[4], c[4];
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
-                                if (pass == 2) fast_sincos(v[e], &y[e], &c[e]);
-                                else y[e] = pass ? fast_sin(v[e]) : fast_cos(v[e]);
+                                const float x = w0 * v[e];
+                                if (pass == 2) fast_sincos(x, &y[e], &c[e]);
+                                else y[e] = pass ? fast_sin(x) : w0 * fast_cos(x);
+                                if (pass == 2) c[e] *= w0;
                             }
                             *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
                             if (pass == 2) *reinterpret_cast<u32x2*>(smem + IMG + o) = u32x2{pack2(c[0], c[1]), pack2(c[2], c[3])};
@@ -303,6 +332,13 @@ bool trunk_bf16_supported(int W, int L, int skip, int K0p) {
     return W == TW && L >= 2 && L <= kTrunkMaxL && K0p <= 64 && K0p % 16 == 0 && skip < L;
 }
 
+static int trunk_tile(bool save) { return g_trunk_tile ? g_trunk_tile : (save ? 64 : 128); }
+
+bool trunk_l0_supported(int K0p, bool save) {
+    const int tpd = trunk_tile(save) == 64 ? TrunkGeo<64>::TPD : TrunkGeo<128>::TPD;
+    return K0p % 4 == 0 && (K0p / 4) % tpd == 0;  // layer 0's k-loop in whole prefetch rounds
+}
+
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes) {
     SPN_ARG(a.P >= 0 && a.S > 0, "trunk_bf16: bad sizes");
     SPN_ARG(trunk_bf16_supported(TW, a.L, a.skip, a.K0p), "trunk_bf16: unsupported shape L=%d skip=%d K0p=%d", a.L,
@@ -312,7 +348,9 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     SPN_ARG(a.P < (1ll << 31) / TW, "trunk_bf16: too many points (%lld)", (long long)a.P);
     bool save = false;
     for (int i = 1; i < a.L; ++i) save |= a.Ds[i] != nullptr;
-    const int tm = g_trunk_tile ? g_trunk_tile : (save ? 64 : 128);
+    const int tm = trunk_tile(save);
+    SPN_ARG(!a.X0 || (a.Wf[0] && trunk_l0_supported(a.K0p, save)), "trunk_bf16: layer 0 unsupported for K0p=%d",
+            a.K0p);
     TrunkArgs ad = a;
     ad.dbg = g_trunk_dbg;
     const int ntiles = cdiv(a.P, tm);

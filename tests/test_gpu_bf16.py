@@ -1,8 +1,10 @@
 """bf16 MLP (SPNeRF(precision="bf16"), cfg.dtype = 1) vs the fp32 reference — needs an MI355X.
 
 The bf16 path is BASELINE.json config 3's arithmetic: activations and GEMM operands in bf16
-(8-bit mantissa, unit roundoff 2^-9), fp32 accumulation, fp32 layer 0 / heads / compositing /
-parameters / gradients — the counterpart of the reference's fp16 AMP training (main.py:334-336).
+(8-bit mantissa, unit roundoff 2^-9), fp32 accumulation, fp32 heads / compositing / parameters /
+gradients — the counterpart of the reference's fp16 AMP training (main.py:334-336).  fc_net.0
+runs on bf16 hi/lo planes, (x_hi + x_lo)·(w_hi + w_lo) with fp32 accumulation (≈2^-17 relative
+per product: the near-fp32 input precision SURVEY §8 hard part 1 asks for, at bf16 MFMA rates).
 It cannot meet the 1e-4 fp32 bar by construction, so it is held to mixed-precision tolerances
 against the SAME reference fixtures the fp32 path matches to 1e-4:
   * outputs: norm-relative error  ||bf16 - ref|| / ||ref|| <= OUT_TOL per key;

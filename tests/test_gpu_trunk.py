@@ -6,7 +6,9 @@ products, the same epilogue), so renders and gradients must agree bit for bit (m
 do); the bf16 path itself is held to the reference by tests/test_gpu_bf16.py.  Covered: the guided-sampling
 pass 1 (no saved activations, sigma only), pass 2 and the solar pass (saved H / D feeding the
 backward), the skip layer's PE columns and per-ray semantic rows, point counts that are not a
-multiple of the 128-point tile, and PE off (K0p = 32).
+multiple of the 128-point tile, and PE off (K0p = 32).  fc_net.0 runs on bf16 hi/lo planes
+(l0_split): inside the fused launch when nothing is saved (the point network below; also when
+saving with trunk_l0=2), as a separate GEMM otherwise, with the same planes and k-order.
 """
 import numpy as np
 import pytest
@@ -73,6 +75,17 @@ def test_fused_trunk_matches_layerwise(dims, n_rays, guided, sc):
         assert e <= TOL, (n, e)
     print(f"fused vs layer-by-layer: bitwise={same} worst grad rel err {worst:.2e}")
     assert same
+
+
+def test_fused_trunk_with_layer0_when_saving_bitwise_vs_layerwise():
+    """trunk_l0=2: fc_net.0 inside the fused launch also when activations are saved (64-point
+    tiles, D = w0·cos(w0·z) of layer 0 from the trunk's epilogue); the default keeps it a
+    separate GEMM there."""
+    _lib.set_option("trunk_l0", 2)
+    try:
+        test_fused_trunk_matches_layerwise(ModelDims(width=512, sem=True), 257, True, 0.1)
+    finally:
+        _lib.set_option("trunk_l0", 1)
 
 
 def test_fused_trunk_point_network_bitwise_vs_layerwise():
