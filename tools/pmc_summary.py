@@ -24,7 +24,7 @@ for d in sorted(data):
     W = c.get("SQ_WAVES", 1)
     wc = c.get("SQ_WAVE_CYCLES", 1)
     gui = c.get("GRBM_GUI_ACTIVE", 1) / 8  # summed over the 8 XCDs
-    print(f"{short:24s} grid={grid:8d} dur={dur / 1e3:7.1f}us cyc/wave={4 * wc / W:.0f} valu/wave={c.get('SQ_INSTS_VALU', 0) / W:.0f} "
+    print(f"{short:24s} grid={grid:8d} dur={dur / 1e3:7.1f}us clk={gui / dur:.2f}GHz cyc/wave={4 * wc / W:.0f} valu/wave={c.get('SQ_INSTS_VALU', 0) / W:.0f} "
           f"lds/wave={c.get('SQ_INSTS_LDS', 0) / W:.0f} mfma/wave={c.get('SQ_INSTS_MFMA', 0) / W:.0f}")
     print(f"    waitAny {c.get('SQ_WAIT_ANY', 0) / wc:.2f} waitInst {c.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} "
           f"(lds {c.get('SQ_WAIT_INST_LDS', 0) / wc:.2f}) active {c.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f} "
