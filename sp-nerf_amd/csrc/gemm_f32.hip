@@ -261,7 +261,10 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
 // Epilogue: a wave stages 32 rows x 64 columns at a time in its own LDS slice; a lane owns 8
 // consecutive columns of rows (lane >> 3) + 8 q4, so every access is a 256-B (fp32) or 128-B
 // (bf16) row segment; all global loads of a piece are issued before its stores.
-template <int BM, int BN, int WGM, int WGN>
+// P2: operand loads run two K-steps ahead in two register sets, and step k+1's LDS stores sit
+// between the two halves of step k's MFMAs instead of before the barrier (loads one step ahead
+// would make those stores wait on HBM mid-step).
+template <int BM, int BN, int WGM, int WGN, bool P2 = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntiles) {
     constexpr int T = 64 * WGM * WGN;
     constexpr int MI = BM / WGM / 32, NJ = BN / WGN / 32;
@@ -303,11 +306,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
 
     f32x16 acc[MI][NJ];
     const int wr = wid / WGN, wc = wid % WGN, r32 = lane & 31, h = lane >> 5;
-    auto compute = [&](int stg) {
+    // k-groups [lo, hi) of a K-step (8 k each)
+    auto compute_kg = [&](int stg, auto klo, auto khi) {
+        constexpr int lo = decltype(klo)::value, hi = decltype(khi)::value;
         const float* sA = smem + stg * (BM + BN) * LK + (wr * MI * 32 + r32) * LK + 4 * h;
         const float* sB = smem + stg * (BM + BN) * LK + BM * LK + (wc * NJ * 32 + r32) * LK + 4 * h;
 #pragma unroll
-        for (int kg = 0; kg < KS / 8; ++kg) {
+        for (int kg = lo; kg < hi; ++kg) {
             f32x4 a[MI], b[NJ];
 #pragma unroll
             for (int i = 0; i < MI; ++i) a[i] = ld4(sA + i * 32 * LK + kg * 8);
@@ -322,6 +327,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
         }
     };
+    auto compute = [&](int stg) {
+        compute_kg(stg, std::integral_constant<int, 0>{}, std::integral_constant<int, KS / 8>{});
+    };
 
     constexpr int SLD = 68;
     static_assert(WGM * WGN * 32 * SLD <= 2 * (BM + BN) * LK, "epilogue staging fits in the LDS");
@@ -329,10 +337,22 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
     const int nk = g.K / KS;
     const bool out16 = g.C16 != nullptr;
 
-    Regs r0;
+    Regs r0, r1;
     gload(r0, t, 0);
     sstore(r0, 0);
+    if constexpr (P2) gload(r1, t, min(1, nk - 1) * KS);
     __syncthreads();
+    // P2 step kt: stage kt & 1 holds step kt, rn holds step kt+1, rl receives step kt+2
+    auto step2 = [&](int kt, Regs& rn, Regs& rl) {
+        gload(rl, t, min(kt + 2, nk - 1) * KS);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_kg(kt & 1, std::integral_constant<int, 0>{}, std::integral_constant<int, KS / 16>{});
+        __builtin_amdgcn_sched_barrier(0);
+        sstore(rn, (kt + 1) & 1);  // stage (kt+1) & 1 was last read in step kt-1 (before the barrier)
+        __builtin_amdgcn_sched_barrier(0);
+        compute_kg(kt & 1, std::integral_constant<int, KS / 16>{}, std::integral_constant<int, KS / 8>{});
+        __syncthreads();
+    };
     while (true) {
         const int bm = (t / nN) * BM, bn = (t % nN) * BN;
 #pragma unroll
@@ -341,13 +361,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
             for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        for (int kt = 0; kt < nk; ++kt) {
-            gload(r0, t, min(kt + 1, nk - 1) * KS);  // past the last step: re-read it (L2 hit)
-            __builtin_amdgcn_sched_barrier(0);         // issue the loads before the MFMAs
-            compute(kt & 1);
-            __builtin_amdgcn_sched_barrier(0);         // LDS writes (and their vmcnt waits) after
-            sstore(r0, (kt + 1) & 1);
-            __syncthreads();
+        if constexpr (P2) {
+            // whole pairs (a conditional second step makes the register sets merge at the
+            // back edge, with a wait on the in-flight loads), then an odd last step
+            int kt = 0;
+            for (; kt + 1 < nk; kt += 2) {
+                step2(kt, r1, r0);
+                step2(kt + 1, r0, r1);
+            }
+            if (kt < nk) step2(kt, r1, r0);  // block-uniform
+        } else {
+            for (int kt = 0; kt < nk; ++kt) {
+                gload(r0, t, min(kt + 1, nk - 1) * KS);  // past the last step: re-read it (L2 hit)
+                __builtin_amdgcn_sched_barrier(0);         // issue the loads before the MFMAs
+                compute(kt & 1);
+                __builtin_amdgcn_sched_barrier(0);         // LDS writes (and their vmcnt waits) after
+                sstore(r0, (kt + 1) & 1);
+                __syncthreads();
+            }
         }
         const int tn = t + G;
         const bool more = tn < ntiles;
@@ -451,6 +482,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         if (!more) break;  // block-uniform
         __syncthreads();   // every wave is done with its staging slice
         sstore(r0, 0);
+        if constexpr (P2) gload(r1, tn, min(1, nk - 1) * KS);
         __syncthreads();
         t = tn;
     }
@@ -672,7 +704,7 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __res
     }
 }
 
-int g_nt_variant = 5;  // 256x128 persistent (k_gemm_nt_w): C2 11.2 -> 10.4 ms/step over variant 2
+int g_nt_variant = 6;  // 256x128 persistent, loads 2 K-steps ahead (k_gemm_nt_w<..., true>): C2 10.30 -> 10.15 ms/step over 5
 
 int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
@@ -692,10 +724,11 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
                         (!a.Dmul || a.ld_dmul % 4 == 0) && (!a.rowbias || a.ld_rb % 4 == 0);
         if (!ok) v = 2;
     }
-    if (v == 4 || v == 5) {
+    if (v >= 4 && v <= 6) {
         const int bm = 256, bn = v == 4 ? 256 : 128;
         const int nt = cdiv(a.M, bm) * cdiv(a.N, bn);
         if (v == 4) hipLaunchKernelGGL((k_gemm_nt_w<256, 256, 2, 4>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else if (v == 6) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, true>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
     } else if (v == 1 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 1>), dim3(nb), dim3(256), 0, s, a);
     else if (v == 2) hipLaunchKernelGGL((k_gemm_nt<32, 2>), dim3(nb), dim3(256), 0, s, a);
