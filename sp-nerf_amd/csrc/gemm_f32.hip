@@ -261,18 +261,25 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
 // Epilogue: a wave stages 32 rows x 64 columns at a time in its own LDS slice; a lane owns 8
 // consecutive columns of rows (lane >> 3) + 8 q4, so every access is a 256-B (fp32) or 128-B
 // (bf16) row segment; all global loads of a piece are issued before its stores.
-// P2: operand loads run two K-steps ahead in two register sets, and step k+1's LDS stores sit
-// between the two halves of step k's MFMAs instead of before the barrier (loads one step ahead
-// would make those stores wait on HBM mid-step).
-template <int BM, int BN, int WGM, int WGN, bool P2 = false>
+// PIPE 1 (P2): operand loads run two K-steps ahead in two register sets, and step k+1's LDS
+// stores sit between the two halves of step k's MFMAs instead of before the barrier (loads one
+// step ahead would make those stores wait on HBM mid-step).
+// PIPE 2: LDS-DMA (global_load_lds_dwordx4) into three unpadded stages, two K-steps in flight,
+// one counted vmcnt + raw barrier per step and no register staging; 128-B rows with 16-B chunks
+// XOR-swizzled by (row >> 1) & 7 (the DMA writes lane-linearly, so the swizzle goes on the
+// source address) keep the fragment ds_read_b128s conflict-free.
+template <int BM, int BN, int WGM, int WGN, int PIPE = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntiles) {
+    constexpr bool P2 = PIPE == 1;
     constexpr int T = 64 * WGM * WGN;
     constexpr int MI = BM / WGM / 32, NJ = BN / WGN / 32;
     constexpr int KS = 32, LK = KS + 4;
     constexpr int RP = T / 8;                  // rows per loader pass (8 float4 chunks per row)
     constexpr int PA = BM / RP, PB = BN / RP;  // loader passes per operand
     static_assert(BM % RP == 0 && BN % RP == 0 && NJ % 2 == 0, "tile geometry");
-    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LK];
+    constexpr int STGF = (BM + BN) * KS;       // floats per DMA stage (PIPE 2)
+    constexpr int SMEM = PIPE == 2 ? 3 * STGF : 2 * (BM + BN) * LK;
+    __shared__ __attribute__((aligned(16))) float smem[SMEM];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nN = (g.N + BN - 1) / BN;
     const int G = gridDim.x;
@@ -330,18 +337,67 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
     auto compute = [&](int stg) {
         compute_kg(stg, std::integral_constant<int, 0>{}, std::integral_constant<int, KS / 8>{});
     };
+    // PIPE 2: one K-step from DMA stage s (rows of 32 floats, chunk c of row r at c ^ ((r>>1)&7))
+    const int swz = (r32 >> 1) & 7;
+    auto compute_g = [&](int s) {
+        const float* sA = smem + s * STGF + (wr * MI * 32 + r32) * KS;
+        const float* sB = smem + s * STGF + (BM + wc * NJ * 32 + r32) * KS;
+#pragma unroll
+        for (int kg = 0; kg < KS / 8; ++kg) {
+            const int off = ((2 * kg + h) ^ swz) * 4;
+            f32x4 a[MI], b[NJ];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) a[i] = ld4(sA + i * 32 * KS + off);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b[j] = ld4(sB + j * 32 * KS + off);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s4], b[j][s4], acc[i][j], 0, 0, 0);
+        }
+    };
+    // PIPE 2: DMA K-step k0 of a tile into stage s; wave w's i-th instruction fills rows
+    // 8q .. 8q+7 (q = i·(T/64) + w), lane l row 8q + l/8, LDS chunk l%8
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+    auto gissue = [&](int tile, int k0, int s) {
+        const int bm = (tile / nN) * BM, bn = (tile % nN) * BN;
+        const bool seg2 = k0 >= K1;
+        const float* pa = seg2 ? g.A2 + (k0 - K1) : g.A + k0;
+        const int lda = seg2 ? lda2 : lda1;
+        constexpr int NI = (BM + BN) * 8 / T;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int q = i * (T / 64) + wid;
+            const int row = q * 8 + (lane >> 3);
+            const int gc = ((lane & 7) ^ ((row >> 1) & 7)) * 4;
+            const float* src = i < BM * 8 / T ? pa + (int64_t)min(bm + row, g.M - 1) * lda + gc
+                                              : g.B + (int64_t)min(bn + row - BM, g.N - 1) * g.ldb + k0 + gc;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(smem + s * STGF + q * 256), 16, 0, 0);
+        }
+    };
 
     constexpr int SLD = 68;
-    static_assert(WGM * WGN * 32 * SLD <= 2 * (BM + BN) * LK, "epilogue staging fits in the LDS");
-    float* stage = smem + wid * (32 * SLD);
+    static_assert(WGM * WGN * 32 * SLD <= SMEM, "epilogue staging fits in the LDS");
+    // PIPE 2 stages the epilogue at the top of the LDS, clear of DMA stage 0
+    static_assert(PIPE != 2 || WGM * WGN * 32 * SLD <= SMEM - STGF, "epilogue staging clear of stage 0");
+    float* stage = smem + (PIPE == 2 ? SMEM - WGM * WGN * 32 * SLD : 0) + wid * (32 * SLD);
     const int nk = g.K / KS;
     const bool out16 = g.C16 != nullptr;
 
     Regs r0, r1;
-    gload(r0, t, 0);
-    sstore(r0, 0);
-    if constexpr (P2) gload(r1, t, min(1, nk - 1) * KS);
-    __syncthreads();
+    if constexpr (PIPE == 2) {
+        gissue(t, 0, 0);
+        gissue(t, min(1, nk - 1) * KS, 1);
+    } else {
+        gload(r0, t, 0);
+        sstore(r0, 0);
+        if constexpr (P2) gload(r1, t, min(1, nk - 1) * KS);
+        __syncthreads();
+    }
     // P2 step kt: stage kt & 1 holds step kt, rn holds step kt+1, rl receives step kt+2
     auto step2 = [&](int kt, Regs& rn, Regs& rl) {
         gload(rl, t, min(kt + 2, nk - 1) * KS);
@@ -361,7 +417,20 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
             for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        if constexpr (P2) {
+        if constexpr (PIPE == 2) {
+            constexpr int NI = (BM + BN) * 8 / T;  // DMA instructions per thread per K-step
+            static_assert(NI == 6, "vmcnt below counts 6 DMAs per K-step");
+            for (int kt = 0; kt < nk; ++kt) {
+                // step kt has landed when at most step kt+1's DMAs are outstanding; the barrier
+                // makes every wave's DMA visible and retires step kt-1's readers of stage (kt+2)%3
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                gissue(t, min(kt + 2, nk - 1) * KS, (kt + 2) % 3);  // past the end: re-reads, unused
+                compute_g(kt % 3);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land in the staging area
+            __builtin_amdgcn_s_barrier();
+        } else if constexpr (P2) {
             // whole pairs (a conditional second step makes the register sets merge at the
             // back edge, with a wait on the in-flight loads), then an odd last step
             int kt = 0;
@@ -382,7 +451,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         }
         const int tn = t + G;
         const bool more = tn < ntiles;
-        gload(r0, more ? tn : t, 0);  // the next tile's first K-step loads during the epilogue
+        if constexpr (PIPE != 2) gload(r0, more ? tn : t, 0);  // the next tile's first K-step loads during the epilogue
 
         // epilogue lane geometry from an opaque lane id (recomputed per tile, not held live
         // across the main loop)
@@ -481,9 +550,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         }
         if (!more) break;  // block-uniform
         __syncthreads();   // every wave is done with its staging slice
-        sstore(r0, 0);
-        if constexpr (P2) gload(r1, tn, min(1, nk - 1) * KS);
-        __syncthreads();
+        if constexpr (PIPE == 2) {
+            gissue(tn, 0, 0);
+            gissue(tn, min(1, nk - 1) * KS, 1);
+        } else {
+            sstore(r0, 0);
+            if constexpr (P2) gload(r1, tn, min(1, nk - 1) * KS);
+            __syncthreads();
+        }
         t = tn;
     }
 }
@@ -704,7 +778,10 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __res
     }
 }
 
-int g_nt_variant = 6;  // 256x128 persistent, loads 2 K-steps ahead (k_gemm_nt_w<..., true>): C2 10.30 -> 10.15 ms/step over 5
+// 7: 256x128 persistent, LDS-DMA stages 2 K-steps ahead (k_gemm_nt_w<..., 2>); 6: register
+// loads 2 K-steps ahead; 5: 1 step ahead.  C2: 10.30 (5) -> 10.17 (6) -> 10.15 ms/step (7);
+// s_setprio(1) around the MFMA groups measured 0.5% slower.
+int g_nt_variant = 7;
 
 int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
@@ -724,11 +801,12 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
                         (!a.Dmul || a.ld_dmul % 4 == 0) && (!a.rowbias || a.ld_rb % 4 == 0);
         if (!ok) v = 2;
     }
-    if (v >= 4 && v <= 6) {
+    if (v >= 4 && v <= 7) {
         const int bm = 256, bn = v == 4 ? 256 : 128;
         const int nt = cdiv(a.M, bm) * cdiv(a.N, bn);
         if (v == 4) hipLaunchKernelGGL((k_gemm_nt_w<256, 256, 2, 4>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
-        else if (v == 6) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, true>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else if (v == 6) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 1>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else if (v == 7) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
     } else if (v == 1 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 1>), dim3(nb), dim3(256), 0, s, a);
     else if (v == 2) hipLaunchKernelGGL((k_gemm_nt<32, 2>), dim3(nb), dim3(256), 0, s, a);
