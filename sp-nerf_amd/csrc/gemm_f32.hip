@@ -685,28 +685,56 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
 // with `transpose`, dst[c][r] instead.  256 threads = 64 columns x 4 split phases, the four
 // phase partials combined in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void k_reduce_slabs(ReduceArgs g) {
-    __shared__ float part[4][65];
+    // a block: one row, 256 columns (float4 quads), the splits in 4 phases (waves); per column
+    // the phases add their splits in order and combine as (p0 + p1) + (p2 + p3)
+    __shared__ f32x4 part[4][64];
     const int r = blockIdx.y;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + tx;
+    const int c = (blockIdx.x * 64 + tx) * 4;  // first column of this thread's quad
     const int n = g.row0 + r;
-    const bool bias_col = c == g.ncols && g.dst_b;
-    float v = 0.f;
-    if (c < g.ncols) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (c + 3 < g.ncols) {
+        // 4 splits' quads in flight per thread (the sums stay in split order)
         const float* src = g.slab + (int64_t)n * g.ld_slab + c;
-        for (int k = ty; k < g.splits; k += 4) v += src[(int64_t)k * g.slab_stride];
-    } else if (bias_col) {
-        for (int k = ty; k < g.splits; k += 4) v += g.slab_b[(int64_t)k * g.N + n];
+        const int64_t st = g.slab_stride;
+        int k = ty;
+        for (; k + 12 < g.splits; k += 16) {
+            const f32x4 x0 = ld4(src + k * st), x1 = ld4(src + (k + 4) * st), x2 = ld4(src + (k + 8) * st),
+                        x3 = ld4(src + (k + 12) * st);
+            v += x0;
+            v += x1;
+            v += x2;
+            v += x3;
+        }
+        for (; k < g.splits; k += 4) v += ld4(src + k * st);
+    } else if (c <= g.ncols) {  // the ragged last quad and the bias column
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int cc = c + e;
+            float a = 0.f;
+            if (cc < g.ncols) {
+                const float* src = g.slab + (int64_t)n * g.ld_slab + cc;
+                for (int k = ty; k < g.splits; k += 4) a += src[(int64_t)k * g.slab_stride];
+            } else if (cc == g.ncols && g.dst_b) {
+                for (int k = ty; k < g.splits; k += 4) a += g.slab_b[(int64_t)k * g.N + n];
+            }
+            v[e] = a;
+        }
     }
     part[ty][tx] = v;
     __syncthreads();
-    if (ty == 0 && (c < g.ncols || bias_col)) {
-        const float s = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
-        if (bias_col) {
-            g.dst_b[r] = g.accumulate ? g.dst_b[r] + s : s;
-        } else {
-            float* d = g.transpose ? g.dst + (int64_t)c * g.ld_dst + r : g.dst + (int64_t)r * g.ld_dst + c;
-            *d = g.accumulate ? *d + s : s;
+    if (ty == 0 && c <= g.ncols) {
+        const f32x4 s4 = (part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int cc = c + e;
+            const float s = s4[e];
+            if (cc < g.ncols) {
+                float* d = g.transpose ? g.dst + (int64_t)cc * g.ld_dst + r : g.dst + (int64_t)r * g.ld_dst + cc;
+                *d = g.accumulate ? *d + s : s;
+            } else if (cc == g.ncols && g.dst_b) {
+                g.dst_b[r] = g.accumulate ? g.dst_b[r] + s : s;
+            }
         }
     }
 }
@@ -874,7 +902,7 @@ int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s, int variant) {
 int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s) {
     if (a.nrows <= 0) return SPNERF_OK;
     const int cols = a.ncols + 1;
-    hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(cols, 64), a.nrows), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(cols, 256), a.nrows), dim3(256), 0, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
