@@ -339,24 +339,32 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
     };
     // PIPE 2: one K-step from DMA stage s (rows of 32 floats, chunk c of row r at c ^ ((r>>1)&7))
     const int swz = (r32 >> 1) & 7;
+    // fragments double-buffered across k-groups: group kg+1's ds_reads are issued ahead of group
+    // kg's MFMAs (with one set, every group started with an exposed LDS latency)
     auto compute_g = [&](int s) {
         const float* sA = smem + s * STGF + (wr * MI * 32 + r32) * KS;
         const float* sB = smem + s * STGF + (BM + wc * NJ * 32 + r32) * KS;
+        f32x4 a[2][MI], b[2][NJ];
+        auto frag = [&](int kg, f32x4* fa, f32x4* fb) {
+            const int off = ((2 * kg + h) ^ swz) * 4;
+#pragma unroll
+            for (int i = 0; i < MI; ++i) fa[i] = ld4(sA + i * 32 * KS + off);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) fb[j] = ld4(sB + j * 32 * KS + off);
+        };
+        frag(0, a[0], b[0]);
 #pragma unroll
         for (int kg = 0; kg < KS / 8; ++kg) {
-            const int off = ((2 * kg + h) ^ swz) * 4;
-            f32x4 a[MI], b[NJ];
-#pragma unroll
-            for (int i = 0; i < MI; ++i) a[i] = ld4(sA + i * 32 * KS + off);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) b[j] = ld4(sB + j * 32 * KS + off);
+            const int cur = kg & 1;
+            if (kg + 1 < KS / 8) frag(kg + 1, a[cur ^ 1], b[cur ^ 1]);
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
                     for (int j = 0; j < NJ; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s4], b[j][s4], acc[i][j], 0, 0, 0);
+                        acc[i][j] =
+                            __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i][s4], b[cur][j][s4], acc[i][j], 0, 0, 0);
         }
     };
     // PIPE 2: DMA K-step k0 of a tile into stage s; wave w's i-th instruction fills rows
