@@ -268,17 +268,22 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
 // one counted vmcnt + raw barrier per step and no register staging; 128-B rows with 16-B chunks
 // XOR-swizzled by (row >> 1) & 7 (the DMA writes lane-linearly, so the swizzle goes on the
 // source address) keep the fragment ds_read_b128s conflict-free.
+// PIPE 3: PIPE 2 with K-steps of 16 (64-B rows, chunks swizzled by (row >> 2) & 3) for 4-wave
+// blocks, two per CU (72 KB of LDS each): one block's epilogue overlaps the other's MFMAs.
 template <int BM, int BN, int WGM, int WGN, int PIPE = 0>
-__global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntiles) {
+__global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_nt_w(NTArgs g,
+                                                                                                    int ntiles) {
     constexpr bool P2 = PIPE == 1;
+    constexpr bool DMA = PIPE >= 2;
     constexpr int T = 64 * WGM * WGN;
     constexpr int MI = BM / WGM / 32, NJ = BN / WGN / 32;
-    constexpr int KS = 32, LK = KS + 4;
+    constexpr int KS = PIPE == 3 ? 16 : 32, LK = KS + 4;
+    constexpr int CH = KS / 4, SH = KS == 32 ? 1 : 2;  // 16-B chunks per DMA row, swizzle row shift
     constexpr int RP = T / 8;                  // rows per loader pass (8 float4 chunks per row)
     constexpr int PA = BM / RP, PB = BN / RP;  // loader passes per operand
     static_assert(BM % RP == 0 && BN % RP == 0 && NJ % 2 == 0, "tile geometry");
     constexpr int STGF = (BM + BN) * KS;       // floats per DMA stage (PIPE 2)
-    constexpr int SMEM = PIPE == 2 ? 3 * STGF : 2 * (BM + BN) * LK;
+    constexpr int SMEM = DMA ? 3 * STGF : 2 * (BM + BN) * LK;
     __shared__ __attribute__((aligned(16))) float smem[SMEM];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nN = (g.N + BN - 1) / BN;
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         compute_kg(stg, std::integral_constant<int, 0>{}, std::integral_constant<int, KS / 8>{});
     };
     // PIPE 2: one K-step from DMA stage s (rows of 32 floats, chunk c of row r at c ^ ((r>>1)&7))
-    const int swz = (r32 >> 1) & 7;
+    const int swz = (r32 >> SH) & (CH - 1);
     // fragments double-buffered across k-groups: group kg+1's ds_reads are issued ahead of group
     // kg's MFMAs (with one set, every group started with an exposed LDS latency)
     auto compute_g = [&](int s) {
@@ -376,13 +381,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         const bool seg2 = k0 >= K1;
         const float* pa = seg2 ? g.A2 + (k0 - K1) : g.A + k0;
         const int lda = seg2 ? lda2 : lda1;
-        constexpr int NI = (BM + BN) * 8 / T;
+        constexpr int NI = (BM + BN) * CH / T;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int q = i * (T / 64) + wid;
-            const int row = q * 8 + (lane >> 3);
-            const int gc = ((lane & 7) ^ ((row >> 1) & 7)) * 4;
-            const float* src = i < BM * 8 / T ? pa + (int64_t)min(bm + row, g.M - 1) * lda + gc
+            const int row = q * (64 / CH) + lane / CH;
+            const int gc = ((lane % CH) ^ ((row >> SH) & (CH - 1))) * 4;
+            const float* src = i < BM * CH / T ? pa + (int64_t)min(bm + row, g.M - 1) * lda + gc
                                               : g.B + (int64_t)min(bn + row - BM, g.N - 1) * g.ldb + k0 + gc;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(smem + s * STGF + q * 256), 16, 0, 0);
         }
@@ -391,13 +396,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
     constexpr int SLD = 68;
     static_assert(WGM * WGN * 32 * SLD <= SMEM, "epilogue staging fits in the LDS");
     // PIPE 2 stages the epilogue at the top of the LDS, clear of DMA stage 0
-    static_assert(PIPE != 2 || WGM * WGN * 32 * SLD <= SMEM - STGF, "epilogue staging clear of stage 0");
-    float* stage = smem + (PIPE == 2 ? SMEM - WGM * WGN * 32 * SLD : 0) + wid * (32 * SLD);
+    static_assert(!DMA || WGM * WGN * 32 * SLD <= SMEM - STGF, "epilogue staging clear of stage 0");
+    float* stage = smem + (DMA ? SMEM - WGM * WGN * 32 * SLD : 0) + wid * (32 * SLD);
     const int nk = g.K / KS;
     const bool out16 = g.C16 != nullptr;
 
     Regs r0, r1;
-    if constexpr (PIPE == 2) {
+    if constexpr (DMA) {
         gissue(t, 0, 0);
         gissue(t, min(1, nk - 1) * KS, 1);
     } else {
@@ -425,8 +430,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
             for (int j = 0; j < NJ; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        if constexpr (PIPE == 2) {
-            constexpr int NI = (BM + BN) * 8 / T;  // DMA instructions per thread per K-step
+        if constexpr (DMA) {
+            constexpr int NI = (BM + BN) * CH / T;  // DMA instructions per thread per K-step
             static_assert(NI == 6, "vmcnt below counts 6 DMAs per K-step");
             for (int kt = 0; kt < nk; ++kt) {
                 // step kt has landed when at most step kt+1's DMAs are outstanding; the barrier
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         }
         const int tn = t + G;
         const bool more = tn < ntiles;
-        if constexpr (PIPE != 2) gload(r0, more ? tn : t, 0);  // the next tile's first K-step loads during the epilogue
+        if constexpr (!DMA) gload(r0, more ? tn : t, 0);  // the next tile's first K-step loads during the epilogue
 
         // epilogue lane geometry from an opaque lane id (recomputed per tile, not held live
         // across the main loop)
@@ -558,7 +563,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_w(NTArgs g, int ntil
         }
         if (!more) break;  // block-uniform
         __syncthreads();   // every wave is done with its staging slice
-        if constexpr (PIPE == 2) {
+        if constexpr (DMA) {
             gissue(tn, 0, 0);
             gissue(tn, min(1, nk - 1) * KS, 1);
         } else {
@@ -814,10 +819,11 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __res
     }
 }
 
-// 7: 256x128 persistent, LDS-DMA stages 2 K-steps ahead (k_gemm_nt_w<..., 2>); 6: register
-// loads 2 K-steps ahead; 5: 1 step ahead.  C2: 10.30 (5) -> 10.17 (6) -> 10.15 ms/step (7);
-// s_setprio(1) around the MFMA groups measured 0.5% slower.
-int g_nt_variant = 7;
+// 8: 256x128 tiles on 4-wave blocks, two per CU, LDS-DMA K-steps of 16 (k_gemm_nt_w<.., 2, 2, 3>);
+// 7: the same DMA pipeline on one 8-wave block per CU; 6: register loads 2 K-steps ahead; 5: 1
+// step ahead.  C2: 10.30 (5) -> 10.17 (6) -> 10.04 (7, + reduce) -> 9.89 ms/step (8); s_setprio(1)
+// around the MFMA groups measured 0.5% slower.
+int g_nt_variant = 8;
 
 int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
@@ -837,12 +843,13 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
                         (!a.Dmul || a.ld_dmul % 4 == 0) && (!a.rowbias || a.ld_rb % 4 == 0);
         if (!ok) v = 2;
     }
-    if (v >= 4 && v <= 7) {
+    if (v >= 4 && v <= 8) {
         const int bm = 256, bn = v == 4 ? 256 : 128;
         const int nt = cdiv(a.M, bm) * cdiv(a.N, bn);
         if (v == 4) hipLaunchKernelGGL((k_gemm_nt_w<256, 256, 2, 4>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else if (v == 6) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 1>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else if (v == 7) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else if (v == 8) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 2, 2, 3>), dim3(std::min(nt, 512)), dim3(256), 0, s, a, nt);
         else hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
     } else if (v == 1 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 1>), dim3(nb), dim3(256), 0, s, a);
     else if (v == 2) hipLaunchKernelGGL((k_gemm_nt<32, 2>), dim3(nb), dim3(256), 0, s, a);

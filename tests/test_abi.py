@@ -125,7 +125,7 @@ def test_kernel_options_roundtrip_and_reject_unknown_names():
         old = _lib.get_option(name)
         _lib.set_option(name, old)
         assert _lib.get_option(name) == old
-    assert _lib.get_option("fused_trunk") == 1 and _lib.get_option("nt_f32_variant") == 7
+    assert _lib.get_option("fused_trunk") == 1 and _lib.get_option("nt_f32_variant") == 8
     assert L.spnerf_set_option(b"no_such_option", 1) < 0
     assert b"unknown option" in L.spnerf_last_error()
     with pytest.raises(_lib.SpnerfError):

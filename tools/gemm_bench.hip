@@ -69,7 +69,7 @@ int main(int argc, char** argv) {
         gemm_nt(f, 0, 0);
         CK(hipMemcpy(ref.data(), C, ref.size() * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(refD.data(), D, ref.size() * 4, hipMemcpyDeviceToHost));
-        for (int v = 1; v < 8; ++v) {
+        for (int v = 1; v < 9; ++v) {
             CK(hipMemset(C, 0, ref.size() * 4));
             CK(hipMemset(D, 0, ref.size() * 4));
             gemm_nt(f, 0, v);
@@ -83,12 +83,12 @@ int main(int argc, char** argv) {
             printf("variant %d max|diff| vs variant 0: C %.3g D %.3g\n", v, md, mdd);
         }
     }
-    for (int v = 0; v < 8; ++v) {
+    for (int v = 0; v < 9; ++v) {
         char nm[64];
         snprintf(nm, 64, "nt plain variant %d", v);
         report(nm, time_it([&] { gemm_nt(g, 0, v); }));
     }
-    for (int v = 0; v < 8; ++v) {
+    for (int v = 0; v < 9; ++v) {
         NTArgs f = g;
         f.bias = bias; f.act = 1; f.w0 = 1.f; f.Dout = D; f.ld_dout = N;
         char nm[64];
@@ -110,7 +110,7 @@ int main(int argc, char** argv) {
     const int sp = tn_splits(M, N, K);
     report("tn (dW) 1 stage", time_it([&] { gemm_tn(t, sp, 0, 0); }));
     report("tn (dW) 2 stages", time_it([&] { gemm_tn(t, sp, 0, 1); }));
-    for (int v = 0; v < 8; ++v) {
+    for (int v = 0; v < 9; ++v) {
         NTArgs bb = b;
         char nm[64];
         snprintf(nm, 64, "nt bwd Dmul variant %d", v);
