@@ -110,6 +110,21 @@ int main(int argc, char** argv) {
     const int sp = tn_splits(M, N, K);
     report("tn (dW) 1 stage", time_it([&] { gemm_tn(t, sp, 0, 0); }));
     report("tn (dW) 2 stages", time_it([&] { gemm_tn(t, sp, 0, 1); }));
+    report("tn (dW) 2 stages, 2 ahead", time_it([&] { gemm_tn(t, sp, 0, 2); }));
+    {  // slabs of variants 0 and 2 vs variant 1 (same k-order: bit-identical)
+        const size_t ns = (size_t)sp * N * K;
+        std::vector<float> ref(ns), got(ns);
+        gemm_tn(t, sp, 0, 1);
+        CK(hipMemcpy(ref.data(), slab, ns * 4, hipMemcpyDeviceToHost));
+        for (int v : {0, 2}) {
+            CK(hipMemset(slab, 0, ns * 4));
+            gemm_tn(t, sp, 0, v);
+            CK(hipMemcpy(got.data(), slab, ns * 4, hipMemcpyDeviceToHost));
+            double md = 0;
+            for (size_t i = 0; i < ns; ++i) md = std::max(md, (double)std::fabs(ref[i] - got[i]));
+            printf("tn variant %d max|diff| vs variant 1: %.3g\n", v, md);
+        }
+    }
     for (int v = 0; v < 9; ++v) {
         NTArgs bb = b;
         char nm[64];
