@@ -39,7 +39,7 @@ from spnerf_amd.scene import synthetic_scene  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec
 BF16_MFMA_PEAK_TFLOPS = 2516.6    # dense bf16 = 16 x the f32 MFMA rate (MI355X_MICROARCH.md "Peak BF16", ~2.5 PF)
 HBM_PEAK_GBS = 8000.0
-GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt_w (fp32 MFMA, 256x128 persistent tiles)", FP32_MFMA_PEAK_TFLOPS),
+GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt_w (fp32 MFMA, 256x128 persistent tiles, 2 blocks/CU, LDS-DMA)", FP32_MFMA_PEAK_TFLOPS),
                 "gemm_tn_f32": ("k_gemm_tn (fp32 MFMA, weight gradients)", FP32_MFMA_PEAK_TFLOPS),
                 "gemm_nt_bf16": ("k_gemm_nt_bf16w (bf16 MFMA, 256x256 persistent tiles)", BF16_MFMA_PEAK_TFLOPS),
                 "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA, weight gradients)", BF16_MFMA_PEAK_TFLOPS),
