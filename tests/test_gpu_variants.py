@@ -1,0 +1,58 @@
+"""fp32 GEMM kernel variants through a whole training render — needs an MI355X.
+
+Every fp32 NT variant (`nt_f32_variant` 5 … 8: register staging one / two K-steps ahead, LDS-DMA
+on one 8-wave block or on two 4-wave blocks per CU) and TN variant (`tn_f32_variant` 0 … 2)
+accumulates each output in the same k-order, so a C2-shaped render (W = 512, semantic and sun
+heads on, guided pass) and its parameter gradients must come out bit for bit the same as with
+the defaults; the defaults themselves are held to the reference by tests/test_gpu_parity.py.
+"""
+import pytest
+import torch
+
+import golden_util as gu
+import spnerf_amd
+from spnerf_amd import _lib
+from oracle.weights import ModelDims
+from test_gpu_parity import DEV, gu_rays, make_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _render(opts):
+    old = {k: _lib.get_option(k) for k in opts}
+    for k, v in opts.items():
+        _lib.set_option(k, v)
+    try:
+        args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+                                        sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+        n = 300  # 300 · 64 points: ragged last tiles for every tiling
+        rays = torch.tensor(gu_rays(n, 21), device=DEV)
+        g = torch.Generator(device="cpu").manual_seed(4)
+        kw = dict(valid_depth=(torch.rand(n, generator=g) < 0.7).long().to(DEV),
+                  target_depths=torch.stack([rays[:, 7] * 0.5, torch.ones(n, device=DEV)], 1),
+                  target_std=torch.full((n,), 0.01, device=DEV))
+        sem = torch.randint(0, 3, (n,), generator=g).to(DEV)
+        model = make_model(ModelDims(width=512, sem=True), 6, "fp32")
+        torch.manual_seed(7)
+        res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="train", **kw)
+        loss = sum((v.float() ** 2).mean() for k, v in sorted(res.items()) if v.requires_grad)
+        loss.backward()
+        torch.cuda.synchronize()
+        return ({k: v.detach().cpu() for k, v in res.items()},
+                {k: p.grad.detach().cpu() for k, p in model.named_parameters() if p.grad is not None})
+    finally:
+        for k, v in old.items():
+            _lib.set_option(k, v)
+
+
+@pytest.mark.parametrize("opts", [{"nt_f32_variant": v} for v in (5, 6, 7, 8)] +
+                         [{"tn_f32_variant": v} for v in (0, 1, 2)])
+def test_fp32_gemm_variants_bitwise_equal(opts):
+    r0, g0 = _render({})
+    r1, g1 = _render(opts)
+    assert sorted(r0) == sorted(r1) and sorted(g0) == sorted(g1)
+    for k in r0:
+        assert torch.isfinite(r0[k]).all(), k
+        assert torch.equal(r0[k], r1[k]), (opts, k)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), (opts, k)
