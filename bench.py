@@ -306,6 +306,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--torch-adam", action="store_true", help="torch.optim.Adam(fused=True) instead of spnerf_amd.optim.Adam")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="replay render+loss+backward as a HIP graph (default)")
@@ -330,10 +331,10 @@ def main():
     model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"],
                               precision=c["precision"]).to(dev)
     params = list(model.parameters())
-    try:
+    if a.torch_adam:
         opt = torch.optim.Adam(params, lr=5e-4, fused=True)
-    except (RuntimeError, TypeError):
-        opt = torch.optim.Adam(params, lr=5e-4, foreach=True)
+    else:  # the library's one-launch Adam (torch's fused multi-tensor step took ~100 us at C2)
+        opt = spnerf_amd.optim.Adam(params, lr=5e-4)
     args = make_args(c)
     B = c["batch"]
     sampler = dp.SharedSeedSampler(R["rays"].shape[0], B * world, rank, world, seed=0, device=dev)

@@ -142,6 +142,13 @@ int32_t spnerf_rpc_rays(const double* rpc, double downscale, double min_alt, dou
 int32_t spnerf_set_option(const char* name, int32_t value);
 int32_t spnerf_get_option(const char* name, int32_t* value);
 
+/* ---- optimizer step (reference main.py: torch.optim.Adam; no reference kernel) ----------
+ * One Adam step over n fp32 tensors (device pointers; exp_avg / exp_avg_sq zero-initialised by
+ * the caller before step 1), torch's arithmetic with bias corrections for `step` (>= 1). */
+int32_t spnerf_adam_step(int32_t n, void* const* params, const void* const* grads, void* const* exp_avg,
+                         void* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2,
+                         double eps, int32_t step, void* stream);
+
 /* ---- in-library kernel timing (HIP events on the launch stream) ------------------------- */
 int32_t spnerf_prof_enable(int32_t on);
 int32_t spnerf_prof_reset(void);

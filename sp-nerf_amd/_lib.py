@@ -58,6 +58,8 @@ SIGNATURES = {
                                   c_void_p]),
     "spnerf_set_option": (c_int32, [c_char_p, c_int32]),
     "spnerf_get_option": (c_int32, [c_char_p, POINTER(c_int32)]),
+    "spnerf_adam_step": (c_int32, [c_int32, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
+                                   POINTER(c_int64), c_double, c_double, c_double, c_double, c_int32, c_void_p]),
     "spnerf_prof_enable": (c_int32, [c_int32]),
     "spnerf_prof_reset": (c_int32, []),
     "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
