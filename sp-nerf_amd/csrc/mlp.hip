@@ -513,6 +513,117 @@ __global__ __launch_bounds__(256) void k_heads_bwd(HeadsBwdArgs<T> a, PackedOffs
     }
 }
 
+// k_heads_bwd with the latency structure of k_heads_fwd_v: the d_out row, the hsave row and
+// the D rows of point p + nw load into a second register set while point p computes (two sets
+// in turn), the d_out / hsave values come from one coalesced load each (lane c holds column c,
+// read back with readlane), the head weights sit in VGPRs / LDS.  Same arithmetic per element
+// as k_heads_bwd (bit-identical).  H ≤ 256·NH.
+template <typename T, int NH>
+__global__ __launch_bounds__(256) void k_heads_bwd_v(HeadsBwdArgs<T> a, PackedOffs k) {
+    extern __shared__ float wsem[];  // [C][H] semantic weights (mode 0, semantic model)
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const Dims& d = a.d;
+    const float* Pk = a.packed;
+    const int H = d.H;
+    const bool sun_on = a.mode != 1, full = a.mode == 0, beta = full && d.beta, sem = full && d.sem;
+    if (sem) {
+        for (int i = threadIdx.x; i < d.C * H; i += 256) wsem[i] = Pk[k.Wm2 + i];
+        __syncthreads();
+    }
+    int ch[NH];
+    bool vh[NH];
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        vh[i] = 4 * lane + 256 * i < H;
+        ch[i] = vh[i] ? 4 * lane + 256 * i : 0;
+    }
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 w4[NH], wr[3][NH], wb[NH];
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        w4[i] = vh[i] && sun_on ? ld4(Pk + k.ws4 + ch[i]) : z4;
+        for (int c = 0; c < 3; ++c) wr[c][i] = vh[i] && full ? ld4(Pk + k.Wr2 + c * H + ch[i]) : z4;
+        wb[i] = vh[i] && beta ? ld4(Pk + k.wb2 + ch[i]) : z4;
+    }
+    struct Rows {
+        float g, h;  // lane c: d_out[c] (c < NO), hsave[c] (c < 8)
+        typename RawOf<T>::type s3[NH], qr[NH], qb[NH], gm[NH];
+    };
+    auto load = [&](int64_t p, Rows& r) {
+        r.g = a.d_out[p * d.NO + min(lane, d.NO - 1)];
+        r.h = a.hsave[p * 8 + (lane & 7)];
+        if (sun_on) {
+#pragma unroll
+            for (int i = 0; i < NH; ++i) r.s3[i] = ld_raw(a.DS3 + p * H + ch[i]);
+        }
+        if (full) {
+#pragma unroll
+            for (int i = 0; i < NH; ++i) {
+                r.qr[i] = ld_raw(a.DQ + p * d.NQ + H + ch[i]);
+                if (beta) r.qb[i] = ld_raw(a.DQ + p * d.NQ + 2 * H + ch[i]);
+                if (sem) r.gm[i] = ld_raw(a.DG + p * d.NG + d.W + ch[i]);
+            }
+        }
+    };
+    auto col = [](float v, int c) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), c)); };
+    auto body = [&](int64_t p, const Rows& cur, Rows& nxt) {
+        load(std::min(p + nw, a.P - 1), nxt);
+        const float dsig = softplus_grad(col(cur.g, 3), col(cur.h, 0));
+        float dys = 0.f, dy[3] = {0.f, 0.f, 0.f}, db = 0.f;
+        if (sun_on) {
+            const float s = col(cur.h, 4);
+            dys = col(cur.g, 4) * (1.f - s) * s;
+        }
+        if (full) {
+            for (int c = 0; c < 3; ++c) {
+                const float s = col(cur.h, 1 + c);
+                dy[c] = col(cur.g, c) * 1.002f * (1.f - s) * s;
+            }
+            if (d.beta) db = softplus_grad(col(cur.g, 8), col(cur.h, 5));
+        }
+        // hpre row [dσ, drgb3, dsun, dβ, dsem C]: lane c; the semantic gradients are d_out's
+        // columns sem_col + c - 6, shifted across lanes
+        const float gs = __shfl(cur.g, min(d.sem_col + lane - 6 + 64, 63 + 64) - 64, 64);
+        if (lane < d.HP) {
+            float v = 0.f;
+            if (lane == 0) v = dsig;
+            else if (lane <= 3) v = dy[lane - 1];
+            else if (lane == 4) v = dys;
+            else if (lane == 5) v = db;
+            else if (full) v = gs;
+            a.hpre[p * d.HP + lane] = v;
+        }
+        if (!sun_on) return;
+#pragma unroll
+        for (int i = 0; i < NH; ++i)
+            if (vh[i]) st4(a.dS3 + p * H + ch[i], (dys * w4[i]) * raw_f32(cur.s3[i]));
+        if (!full) return;
+#pragma unroll
+        for (int i = 0; i < NH; ++i) {
+            if (!vh[i]) continue;
+            st4(a.dZQ + p * d.NQ + H + ch[i], (dy[0] * wr[0][i] + dy[1] * wr[1][i] + dy[2] * wr[2][i]) * raw_f32(cur.qr[i]));
+            if (d.beta) st4(a.dZQ + p * d.NQ + 2 * H + ch[i], (db * wb[i]) * raw_f32(cur.qb[i]));
+            if (d.sem) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < d.C; ++j)
+                    acc += col(cur.g, d.sem_col + j) * *reinterpret_cast<const f32x4*>(wsem + j * H + ch[i]);
+                st4(a.dZG + p * d.NG + d.W + ch[i], acc * raw_f32(cur.gm[i]));
+            }
+        }
+    };
+    int64_t p = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+    if (p >= a.P) return;
+    Rows ra, rb;
+    load(p, ra);
+    for (;;) {
+        body(p, ra, rb);
+        if ((p += nw) >= a.P) break;
+        body(p, rb, ra);
+        if ((p += nw) >= a.P) break;
+    }
+}
+
 // out[ray][n] = Σ_{s<S} in[(ray*S + s)*ld + c0 + n]
 template <typename T>
 __global__ void k_ray_rowsum(const T* __restrict__ in, int ld, int c0, int N, int S, float* __restrict__ out,
@@ -1120,8 +1231,12 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
                           P, mode};
         const double eb = BF ? 2.0 : 4.0;
         ProfScope prof("heads_bwd", s, 2.0 * P * 4 * H, 4.0 * P * (d.NO + d.HP) + eb * P * 6 * H);
-        hipLaunchKernelGGL(k_heads_bwd<T>, dim3((unsigned)std::min<int64_t>(cdiv(P, 4), 8192)), dim3(256), 0, s, a,
-                           (PackedOffs)c.k);
+        const unsigned grid = (unsigned)std::min<int64_t>(cdiv(P, 4), 8192);
+        const int nh = g_heads_variant == 0 ? 0 : cdiv(H, 256);
+        const size_t lds = mode == 0 && d.sem ? sizeof(float) * d.C * H : 0;
+        if (nh == 1) hipLaunchKernelGGL((k_heads_bwd_v<T, 1>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k);
+        else if (nh == 2) hipLaunchKernelGGL((k_heads_bwd_v<T, 2>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k);
+        else hipLaunchKernelGGL(k_heads_bwd<T>, dim3(grid), dim3(256), 0, s, a, (PackedOffs)c.k);
         SPN_HIP(hipGetLastError());
     }
     // 2. narrow-head weights: reductions over points
