@@ -142,7 +142,7 @@ int32_t spnerf_rpc_rays(const double* rpc, double downscale, double min_alt, dou
 int32_t spnerf_set_option(const char* name, int32_t value);
 int32_t spnerf_get_option(const char* name, int32_t* value);
 
-/* ---- optimizer step (reference main.py: torch.optim.Adam; no reference kernel) ----------
+/* ---- optimizer step (reference main.py:97: torch.optim.Adam; no reference kernel) -------
  * One Adam step over n fp32 tensors (device pointers; exp_avg / exp_avg_sq zero-initialised by
  * the caller before step 1), torch's arithmetic with bias corrections for `step` (>= 1). */
 int32_t spnerf_adam_step(int32_t n, void* const* params, const void* const* grads, void* const* exp_avg,

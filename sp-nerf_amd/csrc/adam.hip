@@ -1,5 +1,5 @@
 // Adam over a list of fp32 parameter tensors in one launch (the optimizer step of the training
-// loop, reference main.py: torch.optim.Adam(lr) with the default betas / eps, no weight decay).
+// loop, reference main.py:97: torch.optim.Adam(parameters, lr, weight_decay=0), default betas / eps).
 // torch's fused multi-tensor Adam took ~100 us per C2 step for 2.7 M parameters (0.75 TB/s):
 // here every block owns 4096 consecutive elements of one tensor (found by a binary search over
 // the per-tensor block prefix held in the kernel arguments), each thread 4 x float4.
