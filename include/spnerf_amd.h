@@ -134,7 +134,7 @@ int32_t spnerf_rpc_rays(const double* rpc, double downscale, double min_alt, dou
 /* ---- kernel selection (no reference counterpart: A/B switches for tests and benches) ----
  *      "fused_trunk" (1 = bf16 trunk layers 1..L-1 in one persistent LDS-resident launch,
  *      the default; 0 = layer by layer), "nt_f32_variant", "tn_f32_variant",
- *      "nt_bf16_variant" (GEMM tilings), "heads_variant" (1 = prefetching
+ *      "nt_bf16_variant", "tn_bf16_variant" (GEMM tilings), "heads_variant" (1 = prefetching
  *      output heads, forward and backward, the default; 0 = one point at a time), "l0_split" (bf16 MLP: 1 = fc_net.0
  *      on bf16 hi/lo planes, the default; 0 = fp32 MFMA), "trunk_l0" (with l0_split: 1 = fc_net.0
  *      inside the fused trunk launch when nothing is saved, the default; 2 = always; 0 = never).

@@ -39,7 +39,11 @@ struct TN16Args {
 // variant: prefetch depth in K-steps (1 or 2); <= 0 = library default (g_nt16_variant)
 extern int g_nt16_variant;
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);
-int tn_splits_bf16(int P, int N, int K);
+// variant: 1 = 128x128 tiles, 2 = 256x256 tiles where N, K are multiples of 256, 3 = the same
+// tiles fed by LDS-DMA (when P % 32 == 0 as well);
+// <= 0 = library default (g_tn16_variant)
+extern int g_tn16_variant;
+int tn_splits_bf16(int P, int N, int K, int variant = -1);
 int32_t gemm_tn_bf16(const TN16Args& a, int splits, hipStream_t s);
 
 }  // namespace spn

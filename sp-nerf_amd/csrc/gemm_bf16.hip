@@ -585,10 +585,311 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
     }
 }
 
+// Wide TN: 256 (A features) x 256 (B features) per block, 8 waves of 128x64 (4x2 32x32
+// accumulators, 128 AGPRs), one block per CU.  Per 64-point step a block stages 2 x 32 KB and
+// runs 8 x 32 MFMAs: half the L2 bytes per FLOP of the 128x128 kernel above, whose two
+// co-resident blocks need ≈39 TB/s of L2 at MFMA peak (more than the ≈34.5 TB/s the XCDs give),
+// and 1.5 transposed LDS reads per MFMA instead of 2.  Each operand tile is staged as two
+// [64][128] halves in the tn_off image, so the conflict-free read pattern is the one above.
+// Selected (g_tn16_variant = 2) for N, K multiples of 256; other shapes use k_gemm_tn_bf16.
+constexpr int TW = 256;
+__global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 2 * 64 * 256];  // [stage][A|B][half]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nK = (g.K + TW - 1) / TW;
+    const int ntiles = cdiv(g.N, TW) * nK;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);  // split-major, as k_gemm_tn_bf16
+    const int split = w / ntiles, t = w % ntiles;
+    const int n0 = (t / nK) * TW, k0 = (t % nK) * TW;
+    const int p_beg = split * g.p_per_split;
+    const int p_end = min(g.P, p_beg + g.p_per_split);
+    const int ch = tid & 31, lrow = tid >> 5;  // loader: 8 features (chunk ch of 32), rows lrow + 16 i
+    const bool do_bias = g.slab_b != nullptr && k0 == 0;
+
+    u32x4 ra[4], rb[4];
+    float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int nc = min(n0 + 8 * ch, g.N - 8);
+    const int kc = min(k0 + 8 * ch, g.K - 8);
+    const bf16* pb = kc < g.K1 ? g.B + kc : g.B2 + (kc - g.K1);
+    const int ldb = kc < g.K1 ? g.ldb : g.ldb2;
+    const int lda = g.lda;
+    const int soff = (ch >> 4) * 64 * 256;  // half of the tile this thread's chunk lands in
+    int p_ld = 0;
+    auto gload = [&](int p0) {
+        p_ld = p0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pc = min(p0 + lrow + 16 * i, p_end - 1);
+            ra[i] = ldg16(g.A + (int64_t)pc * lda + nc);
+            rb[i] = ldg16(pb + (int64_t)pc * ldb);
+        }
+    };
+    auto sstore = [&](int stg) {
+        char* sA = smem + stg * 4 * 64 * 256 + soff;
+        char* sB = sA + 2 * 64 * 256;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool pin = p_ld + lrow + 16 * i < p_end;
+            const u32x4 v = pin ? ra[i] : z;
+            if (do_bias) {
+                float f[8];
+                unpack8(v, f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bs[e] += f[e];
+            }
+            const int o = tn_off(lrow + 16 * i, ch & 15);
+            *reinterpret_cast<u32x4*>(sA + o) = v;
+            *reinterpret_cast<u32x4*>(sB + o) = pin ? rb[i] : z;
+        }
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int wa = wid >> 2, wb = wid & 3, h = lane >> 5, grp = (lane >> 4) & 1;
+    const int q = (lane & 15) >> 2, pp = lane & 3;
+    auto trd = [&](const char* base, int r0, int col) -> s16x4 {
+        const int o = tn_off(r0 + q, (col >> 3) + (pp >> 1)) + 8 * (pp & 1);
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o));
+    };
+    auto operand = [&](const char* base, int r0, int col) -> bf16x8 {
+        const s16x4 lo = trd(base, r0, col), hi = trd(base, r0 + 4, col);
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    auto compute = [&](int stg) {
+        const char* sA = smem + stg * 4 * 64 * 256 + wa * 64 * 256;                  // half wa of A
+        const char* sB = smem + stg * 4 * 64 * 256 + (2 + (wb >> 1)) * 64 * 256;     // half wb/2 of B
+        const int cb = (wb & 1) * 64;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int r0 = 16 * ks + 8 * h;
+            bf16x8 a[4], b[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = operand(sB, r0, cb + 32 * j + 16 * grp);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = operand(sA, r0, 32 * i + 16 * grp);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    if (p_beg < p_end) {  // block-uniform
+        const int ns = (p_end - p_beg + 63) / 64;
+        gload(p_beg);
+        sstore(0);
+        __syncthreads();
+        for (int st = 0; st < ns; ++st) {
+            gload(p_beg + 64 * (st + 1));
+            __builtin_amdgcn_sched_barrier(0);
+            compute(st & 1);
+            __builtin_amdgcn_sched_barrier(0);
+            sstore((st + 1) & 1);
+            __syncthreads();
+        }
+    }
+
+    float* slab = g.slab + (int64_t)split * g.slab_stride;
+    const int r32 = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int k = k0 + wb * 64 + j * 32 + r32;
+        if (k >= g.K) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + wa * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (n < g.N) slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
+            }
+    }
+    if (do_bias) {  // block-uniform; the 16 row phases of every chunk combined in a fixed order
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);  // [16 phases][256 features]
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[lrow * 256 + 8 * ch + e] = bs[e];
+        __syncthreads();
+        if (tid < 256 && n0 + tid < g.N) {
+            float s = 0.f;
+            for (int ph = 0; ph < 16; ++ph) s += red[ph * 256 + tid];
+            g.slab_b[(int64_t)split * g.N + n0 + tid] = s;
+        }
+    }
+}
+
+// Wide TN fed by LDS-DMA (g_tn16_variant = 3): the tiling of k_gemm_tn_bf16w, but 32-point
+// steps land by global_load_lds_dwordx4 straight into four 32 KB stages, three steps in flight
+// (the register-staged kernel has one step in flight and waits a full HBM latency per step).
+// A wave instruction fills 4 rows x 256 B of one half image; lane l lands at chunk position
+// l % 16 of row l / 16, so it loads the logical chunk (l % 16) ^ swizzle(row) — the tn_off image
+// is built by permuting source addresses.  DMA cannot zero rows, so the host uses this kernel
+// only when every split holds whole 32-point steps (P % 32 == 0).  Bias sums are read back from
+// the landed stage (k0 == 0 blocks only).
+constexpr int TD_STEP = 32, TD_STAGES = 4, TD_STG = 4 * TD_STEP * 256;  // bytes per stage
+__global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
+    __shared__ __attribute__((aligned(16))) char smem[TD_STAGES * TD_STG];  // [stage][A0|A1|B0|B1]
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nK = (g.K + TW - 1) / TW;
+    const int ntiles = cdiv(g.N, TW) * nK;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = w / ntiles, t = w % ntiles;
+    const int n0 = (t / nK) * TW, k0 = (t % nK) * TW;
+    const int p_beg = split * g.p_per_split;
+    const int p_end = min(g.P, p_beg + g.p_per_split);
+    const bool do_bias = g.slab_b != nullptr && k0 == 0;
+    const int ns = p_end > p_beg ? (p_end - p_beg) / TD_STEP : 0;  // whole steps (host-checked)
+
+    // this lane's 4 DMA sources (instructions q = wid + 8 i: i < 2 → A, else B), advanced by
+    // TD_STEP rows per step
+    const bf16* src[4];
+    int ld[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = wid + 8 * i, X = q >> 4, hf = (q >> 3) & 1, rg = q & 7;
+        const int row = rg * 4 + (lane >> 4);
+        const int chl = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const int f = (X ? k0 : n0) + hf * 128 + 8 * chl;
+        if (X == 0) {
+            src[i] = g.A + (int64_t)row * g.lda + min(f, g.N - 8);
+            ld[i] = g.lda;
+        } else {
+            const int kc = min(f, g.K - 8);
+            const bool s2 = kc >= g.K1;
+            ld[i] = s2 ? g.ldb2 : g.ldb;
+            src[i] = (s2 ? g.B2 + (kc - g.K1) : g.B + kc) + (int64_t)row * ld[i];
+        }
+    }
+    auto issue = [&](int st, int stg) {
+        const int64_t p0 = p_beg + (int64_t)TD_STEP * st;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = wid + 8 * i;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src[i] + p0 * ld[i]),
+                                             (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int wa = wid >> 2, wb = wid & 3, h = lane >> 5, grp = (lane >> 4) & 1;
+    const int q4 = (lane & 15) >> 2, pp = lane & 3;
+    auto trd = [&](const char* base, int r0, int col) -> s16x4 {
+        const int o = tn_off(r0 + q4, (col >> 3) + (pp >> 1)) + 8 * (pp & 1);
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o));
+    };
+    auto operand = [&](const char* base, int r0, int col) -> bf16x8 {
+        const s16x4 lo = trd(base, r0, col), hi = trd(base, r0 + 4, col);
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    constexpr int HALF = TD_STEP * 256;
+    auto compute = [&](int stg) {
+        const char* sA = smem + stg * TD_STG + wa * HALF;
+        const char* sB = smem + stg * TD_STG + (2 + (wb >> 1)) * HALF;
+        const int cb = (wb & 1) * 64;
+#pragma unroll
+        for (int ks = 0; ks < TD_STEP / 16; ++ks) {
+            const int r0 = 16 * ks + 8 * h;
+            bf16x8 a[4], b[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = operand(sB, r0, cb + 32 * j + 16 * grp);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = operand(sA, r0, 32 * i + 16 * grp);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    // bias: thread (chunk ch of 32, row phase lrow of 16) sums rows lrow, lrow + 16 of each step
+    const int ch = tid & 31, lrow = tid >> 5;
+    float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto bias_rows = [&](int stg) {
+        const char* sA = smem + stg * TD_STG + (ch >> 4) * HALF;
+#pragma unroll
+        for (int i = 0; i < TD_STEP / 16; ++i) {
+            float f[8];
+            unpack8(*reinterpret_cast<const u32x4*>(sA + tn_off(lrow + 16 * i, ch & 15)), f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bs[e] += f[e];
+        }
+    };
+
+    if (ns > 0) {  // block-uniform
+        issue(0, 0);
+        issue(min(1, ns - 1), 1);  // past the end: re-reads of the last step, never consumed
+        issue(min(2, ns - 1), 2);
+        for (int st = 0; st < ns; ++st) {
+            // step st has landed when at most steps st+1, st+2 (4 DMAs each) are outstanding; the
+            // barrier publishes every wave's DMAs and retires step st-1's reads of stage (st+3)%4
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES);
+            compute(st % TD_STAGES);
+            if (do_bias) bias_rows(st % TD_STAGES);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
+        __builtin_amdgcn_s_barrier();
+    }
+
+    float* slab = g.slab + (int64_t)split * g.slab_stride;
+    const int r32 = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int k = k0 + wb * 64 + j * 32 + r32;
+        if (k >= g.K) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + wa * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (n < g.N) slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
+            }
+    }
+    if (do_bias) {
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);  // [16 phases][256 features]
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[lrow * 256 + 8 * ch + e] = bs[e];
+        __syncthreads();
+        if (tid < 256 && n0 + tid < g.N) {
+            float s = 0.f;
+            for (int ph = 0; ph < 16; ++ph) s += red[ph * 256 + tid];
+            g.slab_b[(int64_t)split * g.N + n0 + tid] = s;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
 int g_nt16_variant = 5;
+int g_tn16_variant = 2;
+
+static bool tn_wide(int N, int K, int variant) {
+    const int v = variant > 0 ? variant : g_tn16_variant;
+    return (v == 2 || v == 3) && N % TW == 0 && K % TW == 0;
+}
 
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt_bf16: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
@@ -629,9 +930,10 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     return SPNERF_OK;
 }
 
-int tn_splits_bf16(int P, int N, int K) {
-    const int tiles = cdiv(N, HB) * cdiv(K, HB);
-    int splits = cdiv(512, tiles);
+int tn_splits_bf16(int P, int N, int K, int variant) {
+    const bool wide = tn_wide(N, K, variant);
+    const int tiles = wide ? cdiv(N, TW) * cdiv(K, TW) : cdiv(N, HB) * cdiv(K, HB);
+    int splits = cdiv(wide ? 256 : 512, tiles);  // one wide block per CU; two 128x128 blocks
     if (splits > 64) splits = 64;
     const int max_splits = cdiv(P, 1024);
     if (splits > max_splits) splits = max_splits;
@@ -647,10 +949,19 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     int pps = cdiv(a.P, splits);
     pps = (pps + 63) / 64 * 64;
     a.p_per_split = pps < 64 ? 64 : pps;
-    const int nb = cdiv(a.N, HB) * cdiv(a.K, HB);
     ProfScope prof("gemm_tn_bf16", s, 2.0 * a.P * a.N * a.K,
                    2.0 * (double)a.P * (a.N + a.K) + 4.0 * splits * (double)a.N * a.K);
-    hipLaunchKernelGGL(k_gemm_tn_bf16, dim3(nb * splits), dim3(256), 0, s, a);
+    if (tn_wide(a.N, a.K, -1)) {
+        const int nb = cdiv(a.N, TW) * cdiv(a.K, TW);
+        const int v = g_tn16_variant;
+        if (v == 3 && a.P % TD_STEP == 0)  // DMA needs whole 32-point steps (p_per_split is a multiple of 64)
+            hipLaunchKernelGGL(k_gemm_tn_bf16d, dim3(nb * splits), dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_gemm_tn_bf16w, dim3(nb * splits), dim3(512), 0, s, a);
+    } else {
+        const int nb = cdiv(a.N, HB) * cdiv(a.K, HB);
+        hipLaunchKernelGGL(k_gemm_tn_bf16, dim3(nb * splits), dim3(256), 0, s, a);
+    }
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -1395,6 +1395,7 @@ static int* option_slot(const char* name) {
     if (n == "nt_f32_variant") return &g_nt_variant;
     if (n == "tn_f32_variant") return &g_tn_variant;
     if (n == "nt_bf16_variant") return &g_nt16_variant;
+    if (n == "tn_bf16_variant") return &g_tn16_variant;
     if (n == "heads_variant") return &g_heads_variant;
     if (n == "l0_split") return &g_l0_split;
     if (n == "trunk_l0") return &g_trunk_l0;

@@ -56,3 +56,48 @@ def test_fp32_gemm_variants_bitwise_equal(opts):
         assert torch.equal(r0[k], r1[k]), (opts, k)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), (opts, k)
+
+
+def _render_bf16(opts):
+    old = {k: _lib.get_option(k) for k in opts}
+    for k, v in opts.items():
+        _lib.set_option(k, v)
+    try:
+        args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+                                        sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+        n = 300
+        rays = torch.tensor(gu_rays(n, 22), device=DEV)
+        g = torch.Generator(device="cpu").manual_seed(5)
+        kw = dict(valid_depth=(torch.rand(n, generator=g) < 0.7).long().to(DEV),
+                  target_depths=torch.stack([rays[:, 7] * 0.5, torch.ones(n, device=DEV)], 1),
+                  target_std=torch.full((n,), 0.01, device=DEV))
+        sem = torch.randint(0, 3, (n,), generator=g).to(DEV)
+        model = make_model(ModelDims(width=512, sem=True), 6, "bf16")
+        torch.manual_seed(7)
+        res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="train", **kw)
+        loss = sum((v.float() ** 2).mean() for k, v in sorted(res.items()) if v.requires_grad)
+        loss.backward()
+        torch.cuda.synchronize()
+        return ({k: v.detach().cpu() for k, v in res.items()},
+                {k: p.grad.detach().cpu() for k, p in model.named_parameters() if p.grad is not None})
+    finally:
+        for k, v in old.items():
+            _lib.set_option(k, v)
+
+
+@pytest.mark.parametrize("variant", [2, 3])
+def test_bf16_tn_tilings_agree(variant):
+    """bf16 weight gradients: the 256x256 TN tilings (tn_bf16_variant 2: register-staged, 3:
+    LDS-DMA; one block per CU) against the 128x128 one (1).  They split the points differently, so the fp32 slab sums round
+    differently: renders must be bit-identical (the TN GEMMs only feed gradients) and every
+    gradient within 1e-4 of its largest entry — fp32 summation-order noise, far below the bf16
+    operand rounding both share."""
+    r1, g1 = _render_bf16({"tn_bf16_variant": 1})
+    r2, g2 = _render_bf16({"tn_bf16_variant": variant})
+    for k in r1:
+        assert torch.equal(r1[k], r2[k]), k
+    assert sorted(g1) == sorted(g2)
+    for k in g1:
+        assert torch.isfinite(g2[k]).all(), k
+        scale = g1[k].abs().max().item()
+        assert (g1[k] - g2[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k

@@ -179,6 +179,21 @@ static void check_tn(int P, int N, int K, int K1, bool timing) {
 int main(int argc, char** argv) {
     const int P = argc > 1 ? atoi(argv[1]) : 131072;
     if (argc > 2) g_iters = atoi(argv[2]);
+    if (argc > 3 && !strcmp(argv[3], "tn")) {  // TN tilings only: checks, then timings per variant
+        const int vs = argc > 4 ? atoi(argv[4]) : 0;  // 0 = all
+        for (int v = 1; v <= 3; ++v) {
+            if (vs && v != vs) continue;
+            g_tn16_variant = v;
+            printf("tn_bf16_variant %d\n", v);
+            check_tn(4100, 512, 512, 512, false);
+            check_tn(4096 + 96, 512, 768, 512, false);
+            check_tn(8192, 768, 512, 512, false);
+            check_tn(P, 512, 512, 512, true);
+            check_tn(P, 768, 512, 512, true);
+        }
+        printf("%s\n", fails ? "SOME CHECKS FAILED" : "all checks ok");
+        return fails ? 1 : 0;
+    }
     // edge shapes (MLP at W=64 / nomap / skip layer)
     check_nt(1000, 64, 64, 64, true, false);
     check_nt(1000, 64, 128, 64, true, false);
