@@ -933,7 +933,9 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
 int tn_splits_bf16(int P, int N, int K, int variant) {
     const bool wide = tn_wide(N, K, variant);
     const int tiles = wide ? cdiv(N, TW) * cdiv(K, TW) : cdiv(N, HB) * cdiv(K, HB);
-    int splits = cdiv(wide ? 256 : 512, tiles);  // one wide block per CU; two 128x128 blocks
+    // one wide block per CU, two 128x128 ones: as many splits as fill the 256 CUs WITHOUT a
+    // second round (N = 768, K = 512 rounded up to 258 wide blocks: 221 us, two rounds)
+    int splits = (wide ? 256 : 512) / tiles;
     if (splits > 64) splits = 64;
     const int max_splits = cdiv(P, 1024);
     if (splits > max_splits) splits = max_splits;
