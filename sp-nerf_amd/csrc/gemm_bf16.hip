@@ -888,7 +888,11 @@ int g_tn16_variant = 2;
 
 static bool tn_wide(int N, int K, int variant) {
     const int v = variant > 0 ? variant : g_tn16_variant;
-    return (v == 2 || v == 3) && N % TW == 0 && K % TW == 0;
+    // fewer than 4 wide tiles cannot fill the chip within the 64-split cap (N = K = 256: 64
+    // blocks, 76 us against 40 us for 256 blocks of the 128x128 kernel).  A skip-layer K (512 +
+    // K0p) stays on the 128x128 kernel too: a wide part + narrow tail re-reads dZ for the tail
+    // and needs 64 splits (K = 576: 143 + 18 us reduction against 152 + 7)
+    return (v == 2 || v == 3) && N % TW == 0 && K % TW == 0 && (N / TW) * (K / TW) >= 4;
 }
 
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {

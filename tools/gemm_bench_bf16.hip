@@ -188,8 +188,12 @@ int main(int argc, char** argv) {
             check_tn(4100, 512, 512, 512, false);
             check_tn(4096 + 96, 512, 768, 512, false);
             check_tn(8192, 768, 512, 512, false);
+            check_tn(4100, 512, 584, 520, false);  // wide + tail, the tail straddling B / B2
+            check_tn(4100, 512, 800, 640, false);  // wide + tail, the tail in B2
             check_tn(P, 512, 512, 512, true);
             check_tn(P, 768, 512, 512, true);
+            check_tn(P, 256, 256, 256, true);
+            check_tn(P, 512, 576, 512, true);
         }
         printf("%s\n", fails ? "SOME CHECKS FAILED" : "all checks ok");
         return fails ? 1 : 0;
