@@ -791,12 +791,18 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 
     const int wa = wid >> 2, wb = wid & 3, h = lane >> 5, grp = (lane >> 4) & 1;
     const int q4 = (lane & 15) >> 2, pp = lane & 3;
+    // The transposed LDS reads are inline asm here: through the builtin, the compiler cannot tell
+    // them from the in-flight DMA's LDS writes and drains vmcnt(0) before every step's first read
+    // (no DMA would ever be in flight across the MFMAs).  Their results are therefore invisible to
+    // its lgkmcnt tracking: one explicit wait, tied to every value it guards, precedes the MFMAs.
     auto trd = [&](const char* base, int r0, int col) -> s16x4 {
         const int o = tn_off(r0 + q4, (col >> 3) + (pp >> 1)) + 8 * (pp & 1);
-        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o));
+        const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(base + o);
+        s16x4 v;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+        return v;
     };
-    auto operand = [&](const char* base, int r0, int col) -> bf16x8 {
-        const s16x4 lo = trd(base, r0, col), hi = trd(base, r0 + 4, col);
+    auto join = [](s16x4 lo, s16x4 hi) -> bf16x8 {
         typedef short s16x8 __attribute__((ext_vector_type(8)));
         const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         return __builtin_bit_cast(bf16x8, v);
@@ -809,11 +815,27 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 #pragma unroll
         for (int ks = 0; ks < TD_STEP / 16; ++ks) {
             const int r0 = 16 * ks + 8 * h;
+            s16x4 al[4], ah[4], bl[2], bh[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                bl[j] = trd(sB, r0, cb + 32 * j + 16 * grp);
+                bh[j] = trd(sB, r0 + 4, cb + 32 * j + 16 * grp);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                al[i] = trd(sA, r0, 32 * i + 16 * grp);
+                ah[i] = trd(sA, r0 + 4, 32 * i + 16 * grp);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(ah[0]), "+v"(ah[1]),
+                           "+v"(ah[2]), "+v"(ah[3]), "+v"(bl[0]), "+v"(bl[1]), "+v"(bh[0]), "+v"(bh[1])
+                         :
+                         : "memory");
             bf16x8 a[4], b[2];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = operand(sB, r0, cb + 32 * j + 16 * grp);
+            for (int j = 0; j < 2; ++j) b[j] = join(bl[j], bh[j]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = operand(sA, r0, 32 * i + 16 * grp);
+            for (int i = 0; i < 4; ++i) a[i] = join(al[i], ah[i]);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
