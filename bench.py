@@ -207,6 +207,30 @@ def measured_traffic(config, kernel_class):
         return None, None
 
 
+
+def roofline_of(dom, nt, traffic=None, traffic_src=None):
+    """Roofline of the dominant kernel class: the bound is the one its algorithmic intensity
+    (FLOP per algorithmic HBM byte, both counted per launch by the library) sits under — MFMA
+    when it is above the ridge peak_flops / 8 TB/s (fp32: 19.7 FLOP/B, bf16: 315), HBM below it
+    (the bf16 GEMMs at K = 512: ≈127 FLOP/B for a sine layer, reading 2 B and writing 4 B per
+    output).  Both fractions are reported; ``frac`` is the binding one."""
+    dom_name, peak = GEMM_CLASSES[dom]
+    secs = nt["ms"] * 1e-3
+    tflops = nt["flop"] / secs / 1e12 if secs else 0.0
+    gbs = nt["bytes"] / secs / 1e9 if secs else 0.0
+    ridge = peak * 1e3 / HBM_PEAK_GBS  # FLOP per byte
+    intensity = nt["flop"] / nt["bytes"] if nt["bytes"] else float("inf")
+    r = {"kernel": f"{dom} ({dom_name})", "intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge,
+         "mfma_frac": tflops / peak, "hbm_frac": gbs / HBM_PEAK_GBS}
+    if intensity >= ridge:
+        r.update(bound="mfma", achieved=tflops, peak=peak, unit="TFLOP/s", frac=tflops / peak)
+    else:
+        r.update(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=gbs / HBM_PEAK_GBS)
+    r.update(traffic=traffic, traffic_unit="HBM bytes per launch", traffic_source=traffic_src,
+             algorithmic_bytes_per_launch=nt["bytes"] / max(1, nt["launches"]),
+             avg_launch_us=1e3 * nt["ms"] / max(1, nt["launches"]))
+    return r
+
 def gemm_totals(steps):
     """All MFMA GEMM launches of the timed steps: counted FLOP / summed kernel time, against the
     peak of each launch's dtype (time-weighted) — the MLP's MFMA utilisation."""
@@ -272,8 +296,6 @@ def run_inference(a, c, rank, world, dev):
     elapsed = float(elapsed.item())
     dom = max(GEMM_CLASSES, key=lambda k: _lib.prof_read(k)["ms"])
     nt = _lib.prof_read(dom)
-    dom_name, peak = GEMM_CLASSES[dom]
-    achieved = nt["flop"] / (nt["ms"] * 1e-3) / 1e12 if nt["ms"] else 0.0
     total = world * B * c["n_samples"] * a.steps
     value = total / elapsed
     out = {
@@ -284,9 +306,7 @@ def run_inference(a, c, rank, world, dev):
         "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": c["n_samples"],
                    "parallelism": f"ray-shard{world}", "image_rays": h * w},
         "image_seconds_projected": h * w * c["n_samples"] / value,
-        "roofline": {"bound": "mfma", "kernel": f"{dom} ({dom_name})", "achieved": achieved, "peak": peak,
-                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                     "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
+        "roofline": roofline_of(dom, nt),
         "mlp_gemms": gemm_totals(a.steps),
         "finite": bool(torch.isfinite(res["rgb_coarse"]).all()),
     }
@@ -462,8 +482,6 @@ def main():
     # dominant kernel = the GEMM class with the most time in the timed steps
     dom = max(GEMM_CLASSES, key=lambda k: _lib.prof_read(k)["ms"])
     nt = _lib.prof_read(dom)
-    dom_name, peak = GEMM_CLASSES[dom]
-    achieved = nt["flop"] / (nt["ms"] * 1e-3) / 1e12 if nt["ms"] else 0.0
     traffic, traffic_src = measured_traffic(a.config, dom)
     total = world * B * s_final * a.steps
     out = {
@@ -481,11 +499,7 @@ def main():
         "data": "synthetic targets on real JAX_269 RPC camera rays (JAX_214 proxy, resident in HBM), seeded-random SPNeRF init",
         "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": s_final,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"{dom} ({dom_name})", "achieved": achieved,
-                     "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                     "traffic": traffic, "traffic_unit": "HBM bytes per launch", "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": nt["bytes"] / max(1, nt["launches"]),
-                     "avg_launch_us": 1e3 * nt["ms"] / max(1, nt["launches"])},
+        "roofline": roofline_of(dom, nt, traffic, traffic_src),
         "mlp_gemms": gemm_totals(prof_steps),
         "kernels": kernels,
         "final_loss": final_loss,
