@@ -132,5 +132,21 @@ int main(int argc, char** argv) {
         report(nm, time_it([&] { gemm_nt(bb, 0, v); }));
     }
     printf("tn splits=%d\n", sp);
+    {  // point-split sweep of the default TN variant (timing only)
+        float *big, *big_b;
+        CK(hipMalloc(&big, (size_t)256 * N * K * 4));
+        CK(hipMalloc(&big_b, (size_t)256 * N * 4));
+        TNArgs ts = t;
+        ts.slab = big;
+        ts.slab_b = big_b;
+        for (int s2 : {16, 32, 64, 128, 256}) {
+            if (s2 * 256 > M) continue;
+            char nm[64];
+            snprintf(nm, 64, "tn variant 2, %d splits", s2);
+            report(nm, time_it([&] { gemm_tn(ts, s2, 0, 2); }));
+        }
+        CK(hipFree(big));
+        CK(hipFree(big_b));
+    }
     return 0;
 }
