@@ -1,20 +1,26 @@
 #!/usr/bin/env python3
 """SP-NeRF train-step throughput on MI355X (ray-samples/s), BASELINE.json metric.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c5|...] [--no-cpu-baseline]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+``--gpus N`` without torchrun's environment starts the N ranks itself (a torch.distributed.run
+child process, launched before anything touches the GPU); under torchrun, WORLD_SIZE must
+equal ``--gpus``, and asking for more GPUs than the node has is an error, not a 1-GPU run.
 
 One step = sample a batch of rays from the HBM-resident synthetic scene (shared-seed sampler,
 every rank its slice), render_rays (stratified [+ guided] sampling, MLP, compositing
 [+ solar pass]) on the HIP kernels, the reference losses, backward, ONE RCCL all-reduce of the
-flat gradient bucket (N > 1), Adam.  Per-GPU batch is fixed (weak scaling).
+flat gradient bucket (N > 1), Adam.
 
-The default workload is BASELINE.json configs[1] (C2: JAX_214 shape at img_downscale=4,
-1024 rays x 64 samples, coarse only, fp32).  ``roofline`` reports the dominant kernel
-(the fp32 MFMA GEMM) from HIP events recorded by the library around each of its launches
-during the timed steps; ``cpu_baseline`` times the repo's PyTorch-CPU oracle (the reference
-algorithm restated, parity-pinned) on the host cores for a bounded sample of the workload.
+The default workload is BASELINE.json configs[3] (C4: the training workload the 1/2/4/8-GPU
+metric is quoted on — C3's README-recipe flags with the bf16 MLP at a GLOBAL batch of 4096 rays
+per step, split over the ranks: strong scaling).  At N=1 the same 4096-ray step runs on one
+GPU.  C2 (configs[1], fp32) is reported beside it as ``secondary`` at N=1.  ``roofline``
+reports the dominant kernel from HIP events recorded by the library around each of its
+launches; ``cpu_baseline`` times the repo's PyTorch-CPU oracle (the reference algorithm
+restated, parity-pinned) on the host cores for a bounded sample of the workload.
 """
 from __future__ import annotations
 
@@ -53,6 +59,13 @@ CONFIGS = {
                         "samples, solar pass, depth + semantic (C=3) heads, W=512, bf16 MLP (fp32 accumulate / params)",
                img_downscale=1.0, batch=1024, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True,
                precision="bf16"),
+    # BASELINE.json configs[3]: the 1/2/4/8-GPU training workload.  The 4096-ray batch is
+    # GLOBAL (split over the ranks: 4096 / N rays each), so this line scales strongly.
+    "c4": dict(workload="C4: JAX_214-shape scene (3 JAX_269 RPC cameras), img_downscale=1, global batch 4096 rays x "
+                        "(64 + 64 guided) samples split over the ranks, solar pass, depth + semantic (C=3) heads, W=512, "
+                        "bf16 MLP (fp32 accumulate / params), one RCCL gradient all-reduce per step",
+               img_downscale=1.0, global_batch=4096, n_samples=64, sem=True, guided=True, sc_lambda=0.1, depth=True,
+               precision="bf16"),
     "c5": dict(workload="C5: whole-image inference render (no grad) of a synthetic 4k RPC camera: JAX_269_006 RPC at x5 "
                         "(4065 x 3965 = 16.1M rays), 128 stratified samples/ray, semantic head on (C=3), W=512, bf16 MLP; "
                         "rays sharded by image rows across ranks, each step renders the next 32768-ray chunk of the shard",
@@ -70,21 +83,47 @@ def make_args(c):
                                  chunk=5120, noise_std=0.0)
 
 
-def cpu_baseline(c, seconds: float):
+def host_cpus():
+    """CPUs this process may actually run on: the affinity mask, capped by the cgroup CPU quota
+    (on the GPU box os.cpu_count() reports the whole machine while the job gets a share of it)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(c, seconds: float, batch: int):
     """The parity-pinned CPU restatement (oracle/ref_cpu.py) of the same train step on the host
-    cores: 256-ray batches of the same workload, timed for ~``seconds``."""
+    cores: batches of the GPU step's size (``batch`` rays) of the same workload, repeated until
+    ~``seconds`` have passed (at least one timed step), after one small warm-up step."""
     import numpy as np
     from oracle import ref_cpu
     from oracle.weights import ModelDims, make_weights
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = host_cpus()
     torch.set_num_threads(threads)
     dims = ModelDims(width=512, sem=c["sem"])
     p = ref_cpu.to_params(make_weights(dims, 0), requires_grad=True)
     opt = torch.optim.Adam(list(p.values()), lr=5e-4)
     scene = synthetic_scene(c["img_downscale"] if not c.get("inference") else 4.0, seed=1, device="cuda").to("cpu")
     args = make_args(c)
-    B = 256
+    B = 64
     g = torch.Generator().manual_seed(0)
     s_final = c["n_samples"] * (2 if c["guided"] else 1)
 
@@ -103,7 +142,8 @@ def cpu_baseline(c, seconds: float):
         loss.backward()
         opt.step()
 
-    one()
+    one()                      # warm-up at 64 rays (pages in the CPU kernels)
+    B = batch
     n, t0 = 0, time.perf_counter()
     while True:
         one()
@@ -113,7 +153,9 @@ def cpu_baseline(c, seconds: float):
     dt = time.perf_counter() - t0
     what = "inference renders" if c.get("inference") else "train steps"
     return {"value": B * s_final * n / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} {what} of {B} rays x {s_final} samples (oracle/ref_cpu.py, torch CPU, {threads} threads)"}
+            "host_cpus_reported": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"{n} {what} of {B} rays x {s_final} samples, the GPU step's batch (oracle/ref_cpu.py, torch "
+                      f"CPU, fp32, {threads} threads = the CPUs this job may use)"}
 
 
 def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int = 3, dev="cuda:0"):
@@ -311,7 +353,7 @@ def run_inference(a, c, rank, world, dev):
         "finite": bool(torch.isfinite(res["rgb_coarse"]).all()),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or 1024)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -319,32 +361,86 @@ def run_inference(a, c, rank, world, dev):
         dist.destroy_process_group()
 
 
-def main():
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a) -> int:
+    """``--gpus N`` outside torchrun: start the N ranks as a torch.distributed.run CHILD process
+    (nothing here has touched the GPU — device_count() does not initialise HIP) and return its
+    exit code.  More GPUs than the node has is an error, never a silent 1-GPU run."""
+    import subprocess
+    have = torch.cuda.device_count()
+    if not a.share_device and have < a.gpus:
+        print(f"bench: --gpus {a.gpus} but this node has {have} GPU(s)", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line reported beside the default C4 at N=1")
     ap.add_argument("--torch-adam", action="store_true", help="torch.optim.Adam(fused=True) instead of spnerf_amd.optim.Adam")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-batch", type=int, default=0, help="rays per CPU-baseline step (default: the GPU step's batch)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="replay render+loss+backward as a HIP graph (default)")
     ap.add_argument("--eager", dest="graph", action="store_false", help="launch every kernel from Python")
     ap.add_argument("--prof-steps", type=int, default=3, help="eager steps timed per kernel in graph mode")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="library kernel switch (spnerf_set_option), e.g. fused_trunk=0, nt_f32_variant=4")
-    a = ap.parse_args()
+    ap.add_argument("--share-device", action="store_true",
+                    help="(rehearsal on a 1-GPU box) every rank on cuda:0 over gloo instead of RCCL")
+    return ap.parse_args(argv)
+
+
+def main():
+    a = parse_args()
+    if a.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if "RANK" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    rank, local, world = dp.env_rank()
+    if world != a.gpus:
+        raise SystemExit(f"bench: launched with WORLD_SIZE={world} but --gpus {a.gpus}")
     for o in a.option:
         name, value = o.split("=")
         _lib.set_option(name, int(value))
-
-    rank, local, world = dp.init_from_env("nccl")
-    torch.cuda.set_device(local)
+    local = 0 if a.share_device else local
+    torch.cuda.set_device(local)                  # before the process group: RCCL binds this device
     dev = torch.device("cuda", local)
+    dp.init_from_env("gloo" if a.share_device else "nccl", device=dev)
     c = CONFIGS[a.config]
     if c.get("inference"):
         return run_inference(a, c, rank, world, dev)
+    out = run_train(a, a.config, rank, world, dev)
+    if rank == 0 and world == 1 and a.config == "c4" and not a.no_secondary:
+        # configs[1] (C2, fp32) beside the headline, same process and GPU, no CPU leg
+        sec = run_train(a, "c2", rank, world, dev, secondary=True)
+        out["secondary"] = {"c2": {k: sec[k] for k in ("value", "unit", "ms_per_step", "dtype", "config", "roofline")}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_train(a, config, rank, world, dev, secondary=False):
+    """One training workload: warm-up, HIP-graph capture, ``a.steps`` timed steps (barrier +
+    synchronize on both sides, max over ranks), per-kernel timings; returns the JSON record."""
+    c = CONFIGS[config]
     scene = synthetic_scene(c["img_downscale"], seed=0, device=dev)
     R = {k: getattr(scene, k) for k in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")}
     torch.manual_seed(0)
@@ -356,7 +452,10 @@ def main():
     else:  # the library's one-launch Adam (torch's fused multi-tensor step took ~100 us at C2)
         opt = spnerf_amd.optim.Adam(params, lr=5e-4)
     args = make_args(c)
-    B = c["batch"]
+    strong = "global_batch" in c
+    if strong and c["global_batch"] % world:
+        raise SystemExit(f"bench: global batch {c['global_batch']} does not split over {world} ranks")
+    B = c["global_batch"] // world if strong else c["batch"]
     sampler = dp.SharedSeedSampler(R["rays"].shape[0], B * world, rank, world, seed=0, device=dev)
     sloss = SNerfLoss(lambda_sc=c["sc_lambda"])
     dloss = DepthLoss(lambda_ds=1.0) if c["depth"] else None
@@ -390,7 +489,7 @@ def main():
             sl = semloss(res, sem)[0]
             loss = loss + (dp.shard_ce(sl, sem, R["sems"][gidx], world) if world > 1 else sl)
         loss.backward()
-        return loss
+        return loss.detach()   # no autograd graph outlives the step (captured nodes would pin their stream)
 
     def finish():
         dp.allreduce_grads(params, world)   # one RCCL all-reduce of the flat gradient (N > 1)
@@ -482,7 +581,7 @@ def main():
     # dominant kernel = the GEMM class with the most time in the timed steps
     dom = max(GEMM_CLASSES, key=lambda k: _lib.prof_read(k)["ms"])
     nt = _lib.prof_read(dom)
-    traffic, traffic_src = measured_traffic(a.config, dom)
+    traffic, traffic_src = measured_traffic(config, dom)
     total = world * B * s_final * a.steps
     out = {
         "metric": "ray-samples/sec (train step)",
@@ -493,12 +592,12 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": 1e3 * elapsed / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": c["precision"],
         "data": "synthetic targets on real JAX_269 RPC camera rays (JAX_214 proxy, resident in HBM), seeded-random SPNeRF init",
-        "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": s_final,
-                   "parallelism": f"dp{world}"},
+        "config": {"workload": c["workload"], "global_batch": B * world, "rays_per_rank": B,
+                   "samples_per_ray": s_final, "parallelism": f"dp{world}"},
         "roofline": roofline_of(dom, nt, traffic, traffic_src),
         "mlp_gemms": gemm_totals(prof_steps),
         "kernels": kernels,
@@ -506,15 +605,12 @@ def main():
         "execution": ("hip graph of render+loss+backward per step, eager all-reduce + fused Adam; kernel timings "
                       f"from {prof_steps} eager steps right after the timed region") if a.graph else "eager",
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
-        if a.config == "c2":
+    del graph
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not secondary:
+        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or B)
+        if config == "c2":
             out["psnr_parity"] = psnr_parity(dev=dev)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":

@@ -25,10 +25,13 @@ def env_rank():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
 
-def init_from_env(backend: str = "nccl"):
+def init_from_env(backend: str = "nccl", device=None):
+    """Join the process group torchrun describes in the environment.  Call it AFTER
+    ``torch.cuda.set_device``; with RCCL the rank's device is bound eagerly (``device_id``)."""
     rank, local, world = env_rank()
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        kw = {"device_id": torch.device(device)} if (backend == "nccl" and device is not None) else {}
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, local, world
 
 
@@ -60,18 +63,22 @@ class SharedSeedSampler:
 
 
 def allreduce_grads(params, world: int, group=None):
-    """One flat all-reduce (SUM then /world) of every gradient; params without grad get zeros."""
+    """One flat all-reduce (SUM then /world) of every gradient.
+
+    Parameters without a gradient stay without one (Adam skips them, as on one GPU).  Which
+    parameters have gradients depends only on the model configuration and the render flags, so
+    the set is the same on every rank and the flat buffers line up."""
     if world <= 1:
         return
-    grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
+    have = [p for p in params if p.grad is not None]
+    if not have:
+        return
+    grads = [p.grad for p in have]
     flat = torch._utils._flatten_dense_tensors(grads)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     flat.div_(world)
-    for p, g in zip(params, torch._utils._unflatten_dense_tensors(flat, grads)):
-        if p.grad is None:
-            p.grad = g
-        else:
-            p.grad.copy_(g)
+    for p, g in zip(have, torch._utils._unflatten_dense_tensors(flat, grads)):
+        p.grad.copy_(g)
 
 
 def ce_scale(local_labels: torch.Tensor, global_labels: torch.Tensor, world: int) -> torch.Tensor:

@@ -47,9 +47,9 @@ def sample_pdf(bins, weights, N_importance, det=False, eps=1e-5):
     else:
         u = current_random_source().rand((B, N_importance), bins.device)
     out = torch.empty(B, N_importance, device=bins.device)
-    _lib.check(_lib.lib().spnerf_sample_pdf(B, nb, _lib.ptr(bins.contiguous().float()), _lib.ptr(weights.contiguous().float()),
-                                            N_importance, _lib.ptr(u.contiguous().float()), float(eps), _lib.ptr(out),
-                                            _lib.stream_of(bins)), "sample_pdf")
+    b, w, uu = bins.contiguous().float(), weights.contiguous().float(), u.contiguous().float()
+    _lib.check(_lib.lib().spnerf_sample_pdf(B, nb, _lib.ptr(b), _lib.ptr(w), N_importance, _lib.ptr(uu), float(eps),
+                                            _lib.ptr(out), _lib.stream_of(bins)), "sample_pdf")
     return out
 
 
@@ -59,21 +59,30 @@ def _bounds(near, far, device):
     return nf.contiguous()
 
 
+def _window_samples(low, high, u, near, far):
+    """Gaussian-binned window sampling at given uniforms u (B, N) (k_sample_pdf, window mode)."""
+    B, N = u.shape
+    lo = low.contiguous().float()          # converted tensors stay bound across the library call
+    hi = high.contiguous().float()
+    uu = u.contiguous().float()
+    nf = _bounds(near, far, lo.device)
+    out = torch.empty(B, N, device=lo.device)
+    _lib.check(_lib.lib().spnerf_sample_3sigma(B, N, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(nf), _lib.ptr(uu), _lib.ptr(out),
+                                               _lib.stream_of(lo)), "sample_3sigma")
+    return out
+
+
+def _uniforms(B, N, det, dev):
+    if det:
+        return torch.linspace(0, 1, N, device=dev).expand(B, N).contiguous()
+    return current_random_source().rand((B, N), dev)
+
+
 def sample_3sigma(low_3sigma, high_3sigma, N, det, near, far, device=None):
     """rendering.py:58-73: Gaussian-weighted bins over [low, high] clamped to [near, far]."""
     _lib.require_device(low_3sigma, high_3sigma)
-    dev = low_3sigma.device
     B = low_3sigma.shape[0]
-    if det:
-        u = torch.linspace(0, 1, N, device=dev).expand(B, N).contiguous()
-    else:
-        u = current_random_source().rand((B, N), dev)
-    out = torch.empty(B, N, device=dev)
-    _lib.check(_lib.lib().spnerf_sample_3sigma(B, N, _lib.ptr(low_3sigma.contiguous().float()),
-                                               _lib.ptr(high_3sigma.contiguous().float()), _lib.ptr(_bounds(near, far, dev)),
-                                               _lib.ptr(u.contiguous().float()), _lib.ptr(out), _lib.stream_of(low_3sigma)),
-               "sample_3sigma")
-    return out
+    return _window_samples(low_3sigma, high_3sigma, _uniforms(B, N, det, low_3sigma.device), near, far)
 
 
 def compute_samples_around_depth(res, N_samples, z_vals, perturb, near, far, device=None):
@@ -102,8 +111,9 @@ def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std, 
     z_unsort = torch.empty(B, 2 * n, device=dev)
     if clamp_nf is None:
         clamp_nf = rays[0, 6:8]                                               # first ray: rendering.py:95,113
-    _lib.check(_lib.lib().spnerf_sample_guided(B, n, _lib.ptr(z_vals), _lib.ptr(res["depth"].contiguous()),
-                                               _lib.ptr(res["weights"].contiguous()), _lib.ptr(clamp_nf), _lib.ptr(valid),
+    depth, weights = res["depth"].contiguous(), res["weights"].contiguous()
+    _lib.check(_lib.lib().spnerf_sample_guided(B, n, _lib.ptr(z_vals), _lib.ptr(depth),
+                                               _lib.ptr(weights), _lib.ptr(clamp_nf), _lib.ptr(valid),
                                                _lib.ptr(tdep), td_stride, _lib.ptr(tstd), _lib.ptr(u_pred), _lib.ptr(u_gt),
                                                _lib.ptr(z_sorted), _lib.ptr(z_unsort), _lib.stream_of(z_vals)),
                "sample_guided")
@@ -112,15 +122,26 @@ def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std, 
 
 def GenerateGuidedSamples(res, z_vals, N_samples, perturb, near, far, mode='test', valid_depth=None, target_depths=None,
                           target_std=None, device=None, margin=0, stdscale=1):
-    """rendering.py:92-116 (``margin`` / ``stdscale`` are unused there too).  The clamp bounds
-    are near[0,0] / far[0,0] — the first ray of the chunk, as in the reference."""
-    B = z_vals.shape[0]
-    rays_like = torch.zeros(B, 11, device=z_vals.device)
-    rays_like[0, 6] = near[0, 0]
-    rays_like[0, 7] = far[0, 0]
-    z_sorted, z_unsort = _guided(res, z_vals.contiguous().float(), N_samples, rays_like, mode, valid_depth, target_depths,
-                                 target_std)
-    return z_unsort[:, N_samples:]   # sorted guided samples (sorting does not change the set)
+    """rendering.py:92-116 (``margin`` / ``stdscale`` are unused there too).  Samples come back
+    in DRAW order, like the reference (render_rays sorts them afterwards, :165); the clamp bounds
+    are near[0,0] / far[0,0] — the first ray of the chunk.  On rays with a depth prior (train)
+    the window is the GT depth ± 3 target_std (:106-114).  render_rays itself uses the fused
+    ``spnerf_sample_guided`` kernel, which also sorts and merges."""
+    n0, f0 = near[0, 0], far[0, 0]
+    z2 = compute_samples_around_depth(res, N_samples, z_vals, perturb, n0, f0, device=device)
+    if mode == 'train':
+        assert valid_depth is not None, 'valid_depth missing in training batch!'
+        dev = z_vals.device
+        valid = valid_depth.reshape(-1).to(device=dev, dtype=torch.int64)
+        if perturb == 0.:
+            u = _uniforms(valid.shape[0], N_samples, True, dev)
+        else:   # one row of u per ray (rows of rays without a prior are unused)
+            u = current_random_source().gt_uniform(valid, N_samples, dev)
+        td = target_depths[:, 0].to(dev, torch.float32)
+        ts = target_std.reshape(-1).to(dev, torch.float32)
+        gt = _window_samples(td - 3. * ts, td + 3. * ts, u, n0, f0)
+        z2 = torch.where((valid > 0).unsqueeze(-1), gt, z2)
+    return z2
 
 
 def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth=None, target_depths=None,

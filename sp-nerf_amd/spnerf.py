@@ -129,6 +129,7 @@ class SPNeRF(torch.nn.Module):
         self._cfg = None
         self._order = None
         self._packed = None
+        self._pack_pool = []
 
     # ---------------------------------------------------------------- library plumbing
     def cfg(self) -> _lib.ModelCfg:
@@ -169,25 +170,45 @@ class SPNeRF(torch.nn.Module):
         named = dict(self.named_parameters())
         return [named[n] for n in self._order]
 
-    def packed_weights(self) -> torch.Tensor:
+    def packed_weights(self, own: bool = False) -> torch.Tensor:
         """Kernel-layout copy of the weights, re-packed on every call (one ≈10 µs kernel).
 
         Change detection is not possible: ``torch.optim.Adam(fused=True)`` updates parameters
         in place without bumping ``_version``, so a version-keyed cache trains on stale weights.
         Re-packing unconditionally is also what a captured HIP graph of a training step needs
-        (every replay re-packs the parameters the optimizer updated)."""
+        (every replay re-packs the parameters the optimizer updated).
+
+        ``own=True`` (a forward that saves for backward) packs into a buffer of its own, taken
+        from a free list and handed back by ``release_packed`` after the backward: the backward
+        then uses the weights of ITS forward even if the parameters change and another forward
+        re-packs in between (autograd semantics).  Padding is zero from allocation and never
+        written, so recycled buffers need no clearing."""
         params = self.canonical_parameters()
         _lib.require_device(params[0])
-        if self._packed is None or self._packed.device != params[0].device:
+        dev = params[0].device
+        if self._packed is not None and self._packed.device != dev:
+            self._packed, self._pack_pool = None, []
+        if own:
+            buf = self._pack_pool.pop() if self._pack_pool else None
+        else:
+            buf = self._packed
+        if buf is None:
             nbytes = _lib.lib().spnerf_packed_bytes(ctypes.byref(self.cfg()))
-            self._packed = torch.zeros(nbytes // 4, dtype=torch.float32, device=params[0].device)
+            buf = torch.zeros(nbytes // 4, dtype=torch.float32, device=dev)
+            if not own:
+                self._packed = buf
         for p in params:
             if not p.is_contiguous() or p.dtype != torch.float32:
                 raise _lib.SpnerfError("parameters must be contiguous float32")
         arr = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
-        _lib.check(_lib.lib().spnerf_pack_params(ctypes.byref(self.cfg()), arr, _lib.ptr(self._packed),
-                                                 _lib.stream_of(self._packed)), "pack_params")
-        return self._packed
+        _lib.check(_lib.lib().spnerf_pack_params(ctypes.byref(self.cfg()), arr, _lib.ptr(buf), _lib.stream_of(buf)),
+                   "pack_params")
+        return buf
+
+    def release_packed(self, buf: torch.Tensor) -> None:
+        """Return a buffer from ``packed_weights(own=True)`` once its backward has run."""
+        if buf is not None and buf is not self._packed and len(self._pack_pool) < 4:
+            self._pack_pool.append(buf)
 
     def invalidate_packed(self) -> None:
         """Kept for callers that prepared a graph capture with it: packing is unconditional."""
@@ -197,11 +218,11 @@ class SPNeRF(torch.nn.Module):
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
         self.precision = precision
-        self._cfg, self._packed = None, None
+        self._cfg, self._packed, self._pack_pool = None, None, []
         return self
 
     def _apply(self, fn, *args, **kwargs):
-        self._packed = None
+        self._packed, self._pack_pool = None, []
         return super()._apply(fn, *args, **kwargs)
 
     # ---------------------------------------------------------------- reference forward API
@@ -240,7 +261,7 @@ class _MLP(torch.autograd.Function):
             _lib.check(-1, "workspace_bytes")
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
         out = torch.empty(B * S, model.number_of_outputs, dtype=torch.float32, device=dev)
-        packed = model.packed_weights()
+        packed = model.packed_weights(own=need_grad)
         _lib.check(L.spnerf_mlp_forward(ctypes.byref(cfg), _lib.ptr(packed), _lib.ptr(rays), rays.stride(0), dir_offset,
                                         B, S, _lib.ptr(z), _lib.ptr(labels), _lib.ptr(temb), flags, _lib.ptr(ws),
                                         _lib.ptr(out), _lib.stream_of(rays)), "mlp_forward")
@@ -259,10 +280,15 @@ class _MLP(torch.autograd.Function):
         total = sum(p.numel() for p in params)
         grad = torch.empty(total, dtype=torch.float32, device=rays.device)
         gt = torch.empty_like(temb) if (temb is not None and ctx.needs_input_grad[5]) else None
+        if ctx.ws is None:
+            raise RuntimeError("SPNeRF MLP backward called twice on the same forward (its activations are freed)")
+        d_out = d_out.contiguous()
         _lib.check(_lib.lib().spnerf_mlp_backward(ctypes.byref(model.cfg()), _lib.ptr(ctx.packed), _lib.ptr(rays),
                                                   rays.stride(0), B, S, _lib.ptr(labels), _lib.ptr(temb), ctx.flags,
-                                                  _lib.ptr(ctx.ws), _lib.ptr(d_out.contiguous()), _lib.ptr(grad),
+                                                  _lib.ptr(ctx.ws), _lib.ptr(d_out), _lib.ptr(grad),
                                                   _lib.ptr(gt), _lib.stream_of(rays)), "mlp_backward")
+        model.release_packed(ctx.packed)
+        ctx.packed = None
         grads, off = [], 0
         for p in params:
             grads.append(grad[off:off + p.numel()].view_as(p))
@@ -338,12 +364,13 @@ class _Composite(torch.autograd.Function):
         out, z, noise = ctx.saved_tensors
         noise_std, sem_col, n_sem, f = ctx.cfg
         B, S = z.shape
-        c = lambda g: None if g is None else g.contiguous()
+        # contiguous copies stay bound to names until the library call has been issued
+        g_rgb, g_depth, g_w, g_T, g_sem = (None if g is None else g.contiguous() for g in (g_rgb, g_depth, g_w, g_T, g_sem))
         d_out = torch.empty_like(out)
         _lib.check(_lib.lib().spnerf_composite_backward(B, S, _lib.ptr(z), _lib.ptr(out), out.shape[1], _lib.ptr(noise),
-                                                        noise_std, sem_col, n_sem, f, _lib.ptr(c(g_rgb)),
-                                                        _lib.ptr(c(g_depth)), _lib.ptr(c(g_w)), _lib.ptr(c(g_T)),
-                                                        _lib.ptr(c(g_sem)), _lib.ptr(d_out), _lib.stream_of(out)),
+                                                        noise_std, sem_col, n_sem, f, _lib.ptr(g_rgb),
+                                                        _lib.ptr(g_depth), _lib.ptr(g_w), _lib.ptr(g_T),
+                                                        _lib.ptr(g_sem), _lib.ptr(d_out), _lib.stream_of(out)),
                    "composite_backward")
         return d_out, None, None, None, None, None, None
 

@@ -34,34 +34,9 @@ sys.path.insert(0, REPO)
 from oracle.weights import ModelDims, make_weights  # noqa: E402
 
 
-# ------------------------------------------------------------------ helpers shared with the tests
-
-def synthetic_rays(n: int, seed: int, far_scale: float = 0.21) -> np.ndarray:
-    """JAX_269-like normalised rays (n, 11): origins inside the unit scene box, unit
-    directions within ~6 deg of the local down vector at Jacksonville (lat 30.3, lon
-    -81.7) expressed in ECEF, near = 0, far ≈ 28 m / 141.2 m, sun_d = (0, 1, 0)
-    (JAX_269 JSONs carry sun_elevation = sun_azimuth = 0, satellite_scene.py:449-473)."""
-    rng = np.random.default_rng(seed)
-    down = np.array([-0.124, 0.855, -0.505])
-    down /= np.linalg.norm(down)
-    o = rng.uniform(-0.8, 0.8, size=(n, 3))
-    d = down + rng.normal(scale=0.05, size=(n, 3))
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    far = far_scale * rng.uniform(0.95, 1.1, size=n)
-    rays = np.zeros((n, 11), np.float64)
-    rays[:, 0:3], rays[:, 3:6], rays[:, 7] = o, d, far
-    rays[:, 9] = 1.0
-    return rays.astype(np.float32)
-
-
-def projection_weights(shapes: dict, seed: int = 1234) -> dict:
-    rng = np.random.default_rng(seed)
-    return {k: rng.standard_normal(shapes[k]).astype(np.float32) for k in sorted(shapes)}
-
-
-def param_projections(names_shapes: list, seed: int = 4321) -> dict:
-    rng = np.random.default_rng(seed)
-    return {n: rng.standard_normal(s).astype(np.float32) for n, s in names_shapes}
+# helpers shared with the tests live in tests/golden_util.py (the GPU tests never load this file)
+sys.path.insert(0, os.path.dirname(HERE))
+from golden_util import param_projections, projection_weights, synthetic_rays  # noqa: E402
 
 
 # ------------------------------------------------------------------ reference driver
@@ -118,13 +93,13 @@ def make_args(**kw):
 
 def run_case(ref_spnerf, ref_rendering, name: str, dims: ModelDims, args, n_rays: int, mode: str,
              full_grads: bool, seed: int = 0, with_depth: bool = False, torch_seed: int = 0,
-             t_vocab: int = 30):
+             t_vocab: int = 30, rays_np=None):
     torch.manual_seed(torch_seed)
     model = build_model(ref_spnerf, dims, seed)
     models = {"coarse": model}
     if args.n_importance > 0:   # second network, weights from seed + 100
         models["fine"] = build_model(ref_spnerf, dims, seed + 100)
-    rays = torch.tensor(synthetic_rays(n_rays, seed=100 + seed))
+    rays = torch.tensor(synthetic_rays(n_rays, seed=100 + seed) if rays_np is None else rays_np[:n_rays])
     rng = np.random.default_rng(7 + seed)
     sem = ts = None
     extra = {}
@@ -246,6 +221,64 @@ def unit_composite(ref_spnerf):
     print("unit_composite written")
 
 
+def dropins(ref_spnerf, ref_rendering):
+    """The public drop-ins outside render_rays, through the reference itself:
+    inference() on explicit sample positions (spnerf.py:63-159, noise on, sem on),
+    compute_samples_around_depth (rendering.py:76-89) and GenerateGuidedSamples in test and
+    train mode (:92-116; its output is in DRAW order, render_rays sorts afterwards at :165),
+    and load_model(args) (models/__init__.py:4-16) after torch.manual_seed(9)."""
+    from models import load_model
+    dims = ModelDims(width=64, sem=True)
+    torch.manual_seed(0)
+    model = build_model(ref_spnerf, dims, 12)
+    B, S = 24, 32
+    rays = torch.tensor(synthetic_rays(B, seed=120))
+    rng = np.random.default_rng(13)
+    far = rays[:, 7:8]
+    z = torch.tensor(np.sort(rng.uniform(0, 1, (B, S)), -1).astype(np.float32)) * far
+    xyz = rays[:, None, 0:3] + rays[:, None, 3:6] * z[..., None]
+    sem = torch.tensor(rng.choice([0, 1, 2, -100], size=B).astype(np.int64))
+    args = make_args(n_samples=S, noise_std=0.2)
+    with Recorder() as rec:
+        res = ref_spnerf.inference(model, args, xyz, z, sun_d=rays[:, 8:11], semantics=sem)
+    outs = {k: v for k, v in res.items() if torch.is_tensor(v)}
+    R = projection_weights({k: tuple(v.shape) for k, v in outs.items() if v.requires_grad})
+    sum((outs[k] * torch.tensor(R[k])).sum() for k in sorted(R)).backward()
+    data = {"rays": rays.numpy(), "z": z.numpy(), "xyz": xyz.numpy(), "in_semantics": sem.numpy(),
+            "noise_std": np.array(0.2), "rng00_randn": rec.draws[0][1].numpy()}
+    data.update({"out_" + k: v.detach().numpy() for k, v in outs.items()})
+    data.update({"grad_" + n: p.grad.numpy() for n, p in model.named_parameters()})
+    # guided sampling around the rendered depth, clamped to the first ray's [near, far]
+    rd = {"depth": res["depth"].detach(), "weights": res["weights"].detach()}
+    near, far2 = rays[:, 6:7], rays[:, 7:8]
+    with Recorder() as rc:
+        zc = ref_rendering.compute_samples_around_depth(rd, S, z, 1.0, near[0, 0], far2[0, 0])
+    data.update(csad_u=rc.draws[0][1].numpy(), csad_out=zc.numpy())
+    with Recorder() as rt:
+        zt = ref_rendering.GenerateGuidedSamples(rd, z, S, 1.0, near, far2, mode="test")
+    data.update(ggs_test_u=rt.draws[0][1].numpy(), ggs_test_out=zt.numpy())
+    valid = (rng.uniform(size=B) < 0.6).astype(np.int64)
+    td = np.stack([(far[:, 0].numpy() * rng.uniform(0.3, 0.7, B)), rng.uniform(0.2, 1, B)], 1).astype(np.float32)
+    tstd = ((1 - rng.uniform(0, 1, B)) * 0.05 + 1e-4).astype(np.float32)
+    with Recorder() as rr:
+        ztr = ref_rendering.GenerateGuidedSamples(rd, z, S, 1.0, near, far2, mode="train", valid_depth=torch.tensor(valid),
+                                                  target_depths=torch.tensor(td), target_std=torch.tensor(tstd))
+    data.update(ggs_train_u0=rr.draws[0][1].numpy(), ggs_train_u1=rr.draws[1][1].numpy(), ggs_train_out=ztr.numpy(),
+                in_valid_depth=valid, in_target_depths=td, in_target_std=tstd)
+    # load_model(args): the reference's factory and initialisation
+    margs = types.SimpleNamespace(model="sp-nerf", num_sem_classes=3, s_embedding_factor=1, fc_layers=8, fc_units=64,
+                                  mapping=True, t_embbeding_tau=4, beta=True, sem=True)
+    torch.manual_seed(9)
+    lm = load_model(margs)
+    Q = param_projections([(n, tuple(p.shape)) for n, p in lm.named_parameters()])
+    for n, p in lm.named_parameters():
+        data[f"load_model|{n}|sum"] = np.array(p.detach().double().sum().item())
+        data[f"load_model|{n}|proj"] = np.array((p.detach().double() * torch.tensor(Q[n]).double()).sum().item())
+    data["load_model|number_of_outputs"] = np.array(lm.number_of_outputs)
+    np.savez_compressed(os.path.join(HERE, "dropins_w64.npz"), **data)
+    print("dropins_w64 written")
+
+
 def init_weights(ref_spnerf):
     """SPNeRF(...) built after torch.manual_seed(7): the reference's own initialisation, for the
     seeded-init equivalence test of the drop-in module (stored as per-parameter sums and
@@ -264,7 +297,7 @@ def init_weights(ref_spnerf):
     print("init_seed7 written")
 
 
-def rpc_rays(ref: str):
+def rpc_rays(ref: str) -> dict:
     """Rays of JAX_269 views through the reference's own datasets/satellite_scene.py get_rays
     (:21-68, with modules/utils.py geodetic_to_ecef :80-100), normalize_rays (:415-425) and
     get_sun_dirs (:449-473).  Its I/O-only imports (rasterio, rpcm, torchvision, cv2, …) are
@@ -320,6 +353,7 @@ def rpc_rays(ref: str):
     out["sun_60_140"] = ss.SatelliteSceneDataset.get_sun_dirs(holder, 60.0, 140.0, 2).numpy()
     np.savez_compressed(os.path.join(HERE, "rpc_rays.npz"), **out)
     print("rpc_rays written", {k: v.shape for k, v in out.items() if k.endswith("rays")})
+    return out
 
 
 def main():
@@ -328,8 +362,11 @@ def main():
     a = ap.parse_args()
     torch.set_num_threads(8)
     ref_spnerf, ref_rendering = load_reference(a.ref)
-    # config 1: 256 rays x 64 samples, coarse, mapping, W=512, no sem/guided/sc
-    run_case(ref_spnerf, ref_rendering, "c1_w512", ModelDims(width=512), make_args(), 256, "test", full_grads=False)
+    real = rpc_rays(a.ref)
+    # config 1: the 16x16 crop of JAX_269_006 (rows/cols 400-415; rays through the reference's
+    # get_rays / normalize_rays / get_sun_dirs), 256 rays x 64 samples, coarse, mapping, W=512
+    run_case(ref_spnerf, ref_rendering, "c1_w512", ModelDims(width=512), make_args(), 256, "test", full_grads=False,
+             rays_np=real["006_crop|rays"])
     # small full-gradient case of the same path
     run_case(ref_spnerf, ref_rendering, "c1_w64", ModelDims(width=64), make_args(), 64, "train", full_grads=True, seed=1)
     # README recipe path (config 3 flags): guided + solar correction + semantics, train mode with depth priors
@@ -353,10 +390,13 @@ def main():
     # no positional encoding (mapping off), n_samples=32
     run_case(ref_spnerf, ref_rendering, "nomap_w64", ModelDims(width=64, mapping=False),
              make_args(n_samples=32), 40, "test", full_grads=True, seed=6)
+    # config 5 flags: 128 stratified samples/ray, semantic head on (C=3), W=512, test mode
+    run_case(ref_spnerf, ref_rendering, "c5_w512", ModelDims(width=512, sem=True), make_args(n_samples=128), 64, "test",
+             full_grads=False, seed=10)
     unit_sampling(ref_rendering)
     unit_composite(ref_spnerf)
     init_weights(ref_spnerf)
-    rpc_rays(a.ref)
+    dropins(ref_spnerf, ref_rendering)
 
 
 if __name__ == "__main__":

@@ -10,7 +10,7 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 CASES = ["c1_w512", "c1_w64", "c3_w64", "c3_w512", "c3_test_w64", "beta_w64", "nomap_w64", "fine_w64",
-         "fine_sc_guided_w64"]
+         "fine_sc_guided_w64", "c5_w512"]
 
 
 def load(name: str) -> dict:
@@ -50,6 +50,24 @@ class Replay:
         assert k == kind and tuple(arr.shape) == tuple(shape), (self.used, k, kind, arr.shape, shape)
         self.used += 1
         return self.to_tensor(arr)
+
+
+def synthetic_rays(n: int, seed: int, far_scale: float = 0.21) -> np.ndarray:
+    """JAX_269-like normalised rays (n, 11): origins inside the unit scene box, unit
+    directions within ~6 deg of the local down vector at Jacksonville (lat 30.3, lon
+    -81.7) expressed in ECEF, near = 0, far ≈ 28 m / 141.2 m, sun_d = (0, 1, 0)
+    (JAX_269 JSONs carry sun_elevation = sun_azimuth = 0, satellite_scene.py:449-473)."""
+    rng = np.random.default_rng(seed)
+    down = np.array([-0.124, 0.855, -0.505])
+    down /= np.linalg.norm(down)
+    o = rng.uniform(-0.8, 0.8, size=(n, 3))
+    d = down + rng.normal(scale=0.05, size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    far = far_scale * rng.uniform(0.95, 1.1, size=n)
+    rays = np.zeros((n, 11), np.float64)
+    rays[:, 0:3], rays[:, 3:6], rays[:, 7] = o, d, far
+    rays[:, 9] = 1.0
+    return rays.astype(np.float32)
 
 
 def projection_weights(shapes: dict, seed: int = 1234) -> dict:

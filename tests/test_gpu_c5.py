@@ -1,0 +1,110 @@
+"""Config 5 (BASELINE.json configs[4]): whole-image inference — 128 stratified samples per ray,
+semantic head on (C=3), W=512, bf16 MLP, no grad — on the HIP path (needs an MI355X).
+
+* against the reference: fixture c5_w512 (64 rays of the C5 flags rendered by the reference's
+  own render_rays, tests/golden/gen_golden.py) through render_rays(mode="test") under
+  torch.no_grad(), i.e. the fused inference trunk; fp32 at the 1e-4 bar, bf16 at the
+  mixed-precision bound of test_gpu_bf16 (OUT_TOL, norm-relative);
+* at full chunk size (32 768 rays x 128 samples = 4.2 M points, the bench's per-step chunk of
+  the synthetic 4k RPC camera): size-independent properties, and bf16 against the fp32 HIP
+  path (which is parity-pinned) on the same rays and draws.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+import spnerf_amd
+from spnerf_amd import ReplayRandom, random_source
+from test_gpu_bf16 import OUT_TOL
+from test_gpu_parity import DEV, make_model
+
+pytestmark = pytest.mark.gpu
+
+
+def render_fixture(precision):
+    data = gu.load("c5_w512")
+    meta = data["meta"]
+    dims, args = gu.dims_of(meta), gu.args_of(meta)
+    assert args.n_samples == 128 and dims.sem and dims.width == 512 and meta["mode"] == "test"
+    model = make_model(dims, meta["seed"], precision)
+    with torch.no_grad(), random_source(ReplayRandom(gu.draws_of(data))) as src:
+        res = spnerf_amd.render_rays({"coarse": model}, args, torch.tensor(data["rays"], device=DEV), None,
+                                     semantics=torch.tensor(data["in_semantics"], device=DEV), mode="test")
+    assert src.used == len(src.draws)
+    return data, res
+
+
+def test_c5_fixture_fp32_inference_matches_reference():
+    data, res = render_fixture("fp32")
+    keys = sorted(k[4:] for k in data if k.startswith("out_"))
+    assert sorted(res) == keys
+    for k in keys:
+        gu.assert_close(k, res[k].cpu().numpy(), data["out_" + k], rtol=1e-4, atol_frac=1e-5)
+
+
+def test_c5_fixture_bf16_inference_close_to_reference():
+    data, res = render_fixture("bf16")
+    errs = {}
+    for k in sorted(k[4:] for k in data if k.startswith("out_")):
+        got = res[k].cpu().numpy()
+        assert np.isfinite(got).all(), k
+        errs[k] = gu.rel_err(got, data["out_" + k])
+    print({k: f"{v:.2e}" for k, v in errs.items()})
+    assert max(errs.values()) < OUT_TOL, errs
+    gu.assert_close("z_vals", res["z_vals_coarse"].cpu().numpy(), data["out_z_vals_coarse"], rtol=1e-6, atol_frac=1e-7)
+
+
+class FixedU:
+    """Stratified jitter from a given table; no σ noise (noise_std = 0)."""
+
+    def __init__(self, u):
+        self.u = u
+
+    def rand(self, shape, device):
+        assert tuple(shape) == tuple(self.u.shape)
+        return self.u
+
+    def noise(self, shape, device, noise_std):
+        assert noise_std == 0
+        return None
+
+
+def test_c5_full_chunk_properties_and_bf16_vs_fp32():
+    from spnerf_amd.satellite import image_rays, load_cameras
+    cams = load_cameras()
+    meta = cams["images"]["JAX_269_006_RGB"]
+    ds = 0.2                                             # the x5 synthetic 4k camera of bench.py c5
+    w = int(meta["width"] // ds)
+    rays = image_rays(meta, ds, cams["scene_loc"], crop=(1600, 0, 32768 // w + 1, w), device=DEV)[:32768]
+    B, S = rays.shape[0], 128
+    assert B == 32768
+    g = torch.Generator(device="cpu").manual_seed(0)
+    sem = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    u = torch.rand(B, S, generator=g).to(DEV)
+    args = gu.args_of({"args": dict(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                                    sc_lambda=0.0, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+    from oracle.weights import ModelDims
+    dims = ModelDims(width=512, sem=True)
+    out = {}
+    for prec in ("fp32", "bf16"):
+        model = make_model(dims, 4, prec)
+        with torch.no_grad(), random_source(FixedU(u)):
+            out[prec] = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="test")
+    r = out["bf16"]
+    for k, v in r.items():
+        assert torch.isfinite(v).all(), k
+    z = r["z_vals_coarse"]
+    assert torch.equal(z, out["fp32"]["z_vals_coarse"])
+    assert bool((z[:, 1:] >= z[:, :-1]).all()) and bool((z >= rays[:, 6:7]).all()) and bool((z <= rays[:, 7:8]).all())
+    wts, T = r["weights_coarse"], r["transparency_coarse"]
+    assert bool((wts >= 0).all()) and bool((wts.sum(-1) <= 1 + 1e-5).all())
+    assert bool((T[:, 1:] <= T[:, :-1] + 1e-7).all()) and bool((T[:, 0] == 1).all())
+    # depth is a convex-ish combination of the sample depths: within [0, far]
+    assert bool((r["depth_coarse"] >= 0).all()) and bool((r["depth_coarse"] <= rays[:, 7] * (1 + 1e-5) + 1e-7).all())
+    rgb = r["rgb_coarse"]
+    assert bool(((rgb >= 0) & (rgb <= 1)).all())
+    for k in ("rgb_coarse", "depth_coarse", "sem_logits_coarse", "weights_coarse"):
+        e = gu.rel_err(r[k].cpu().numpy(), out["fp32"][k].cpu().numpy())
+        print(k, f"{e:.2e}")
+        assert e < OUT_TOL, (k, e)

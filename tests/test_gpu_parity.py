@@ -167,11 +167,7 @@ def c2_batch(n_rays=1024, n=64, seed=0):
 
 
 def gu_rays(n, seed):
-    import importlib.util, os
-    spec = importlib.util.spec_from_file_location("gen_golden", os.path.join(gu.GOLDEN, "gen_golden.py"))
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod.synthetic_rays(n, seed)
+    return gu.synthetic_rays(n, seed)
 
 
 def test_config2_batch_matches_oracle():

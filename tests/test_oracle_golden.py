@@ -87,3 +87,57 @@ def test_oracle_composite_unit():
     R = gu.projection_weights({k: tuple(v.shape) for k, v in res.items()})
     sum((res[k] * torch.tensor(R[k])).sum() for k in sorted(R)).backward()
     gu.assert_close("grad_raw", raw.grad.numpy().reshape(d["grad_raw"].shape), d["grad_raw"], rtol=1e-5, atol_frac=1e-7)
+
+
+def load_npz(name):
+    with np.load(f"{gu.GOLDEN}/{name}.npz", allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def test_oracle_dropins():
+    """inference() on explicit positions, compute_samples_around_depth and GenerateGuidedSamples
+    (test + train, draw order) against the reference's own outputs (fixture dropins_w64)."""
+    from oracle.weights import ModelDims
+    d = load_npz("dropins_w64")
+    dims = ModelDims(width=64, sem=True)
+    p = ref_cpu.to_params(make_weights(dims, 12), requires_grad=True)
+    rays, z = torch.tensor(d["rays"]), torch.tensor(d["z"])
+    res = ref_cpu.inference(p, dims, 0.2, torch.tensor(d["xyz"]), z, rays[:, 8:11],
+                            gu.Replay([("randn", d["rng00_randn"])], torch.tensor), labels=torch.tensor(d["in_semantics"]))
+    for k in ("rgb", "depth", "weights", "transparency", "albedo", "sun", "sky", "sem_logits"):
+        gu.assert_close(k, res[k].detach().numpy(), d["out_" + k], rtol=2e-5, atol_frac=1e-6)
+    R = gu.projection_weights({k: tuple(v.shape) for k, v in res.items() if v.requires_grad})
+    sum((res[k] * torch.tensor(R[k])).sum() for k in sorted(R)).backward()
+    for n, t in p.items():
+        gu.assert_close("grad " + n, t.grad.numpy(), d["grad_" + n], rtol=1e-4, atol_frac=1e-5)
+    rd = {"depth": torch.tensor(d["out_depth"]), "weights": torch.tensor(d["out_weights"])}
+    nf = rays[0, 6], rays[0, 7]
+    zt = ref_cpu.guided_depths(rd, z, z.shape[1], *nf, gu.Replay([("rand", d["ggs_test_u"])], torch.tensor), False)
+    gu.assert_close("GenerateGuidedSamples test", zt.numpy(), d["ggs_test_out"], rtol=1e-5, atol_frac=1e-6)
+    ztr = ref_cpu.guided_depths(rd, z, z.shape[1], *nf,
+                                gu.Replay([("rand", d["ggs_train_u0"]), ("rand", d["ggs_train_u1"])], torch.tensor), True,
+                                torch.tensor(d["in_valid_depth"]), torch.tensor(d["in_target_depths"]),
+                                torch.tensor(d["in_target_std"]))
+    gu.assert_close("GenerateGuidedSamples train", ztr.numpy(), d["ggs_train_out"], rtol=1e-5, atol_frac=1e-6)
+
+
+def test_load_model_init_matches_reference():
+    """spnerf_amd.load_model(args) after torch.manual_seed(9) builds the reference's parameters
+    (models/__init__.py:4-16: same factory arguments, same RNG-consuming init order)."""
+    import types
+    import spnerf_amd
+    d = load_npz("dropins_w64")
+    args = types.SimpleNamespace(model="sp-nerf", num_sem_classes=3, s_embedding_factor=1, fc_layers=8, fc_units=64,
+                                 mapping=True, t_embbeding_tau=4, beta=True, sem=True)
+    torch.manual_seed(9)
+    m = spnerf_amd.load_model(args)
+    assert m.number_of_outputs == int(d["load_model|number_of_outputs"])
+    named = list(m.named_parameters())
+    assert {n for n, _ in named} == {k.split("|")[1] for k in d if k.endswith("|sum")}
+    Q = gu.param_projections([(n, tuple(t.shape)) for n, t in named])
+    for n, t in named:
+        np.testing.assert_allclose(float(t.detach().double().sum()), float(d[f"load_model|{n}|sum"]), rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(float((t.detach().double() * torch.tensor(Q[n]).double()).sum()),
+                                   float(d[f"load_model|{n}|proj"]), rtol=1e-9, atol=1e-9)
+    with pytest.raises(ValueError):
+        spnerf_amd.load_model(types.SimpleNamespace(**dict(vars(args), model="nerf")))
