@@ -401,6 +401,7 @@ def parse_args(argv=None):
     ap.add_argument("--prof-steps", type=int, default=3, help="eager steps timed per kernel in graph mode")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="library kernel switch (spnerf_set_option), e.g. fused_trunk=0, nt_f32_variant=4")
+    ap.add_argument("--global-batch", type=int, default=0, help="override the config's global batch (rays per step)")
     ap.add_argument("--share-device", action="store_true",
                     help="(rehearsal on a 1-GPU box) every rank on cuda:0 over gloo instead of RCCL")
     return ap.parse_args(argv)
@@ -440,7 +441,11 @@ def main():
 def run_train(a, config, rank, world, dev, secondary=False):
     """One training workload: warm-up, HIP-graph capture, ``a.steps`` timed steps (barrier +
     synchronize on both sides, max over ranks), per-kernel timings; returns the JSON record."""
-    c = CONFIGS[config]
+    c = dict(CONFIGS[config])
+    if a.global_batch and not secondary:
+        c.pop("batch", None)
+        c["global_batch"] = a.global_batch
+        c["workload"] += f" [global batch overridden: {a.global_batch} rays]"
     scene = synthetic_scene(c["img_downscale"], seed=0, device=dev)
     R = {k: getattr(scene, k) for k in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")}
     torch.manual_seed(0)

@@ -46,6 +46,7 @@ typedef struct spnerf_model_cfg {
 #define SPNERF_MLP_SAVE 1        /* keep activations for spnerf_mlp_backward (training)      */
 #define SPNERF_MLP_SIGMA_ONLY 2  /* trunk + sigma head only (pass 1 of guided sampling)      */
 #define SPNERF_MLP_SUN_ONLY 4    /* sigma + sun-visibility heads (solar-correction pass)     */
+#define SPNERF_MLP_ACCUMULATE 8  /* backward: add into grad_flat instead of overwriting it   */
 
 /* composite flags */
 #define SPNERF_COMP_WEIGHTS_ONLY 1  /* weights, transparency, depth only (no rgb / sem)      */
@@ -74,8 +75,9 @@ int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed,
                            int64_t n_rays, int32_t n_samples, const float* z,
                            const int64_t* labels, const float* t_emb, int32_t flags,
                            void* workspace, float* out, void* stream);
-/* Gradients of sum(d_out * out) w.r.t. every parameter, written (overwritten) into
- * `grad_flat` (canonical order, torch shapes, contiguous) and w.r.t. t_emb (n_rays, t_dim). */
+/* Gradients of sum(d_out * out) w.r.t. every parameter, written (overwritten, or added with
+ * SPNERF_MLP_ACCUMULATE in `flags`) into `grad_flat` (canonical order, torch shapes,
+ * contiguous) and w.r.t. t_emb (n_rays, t_dim, overwritten). */
 int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed,
                             const float* rays, int32_t ray_stride, int64_t n_rays, int32_t n_samples,
                             const int64_t* labels, const float* t_emb, int32_t flags,

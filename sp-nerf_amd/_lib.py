@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "libspnerf_amd.so")
 SPNERF_MLP_SAVE = 1
 SPNERF_MLP_SIGMA_ONLY = 2
 SPNERF_MLP_SUN_ONLY = 4
+SPNERF_MLP_ACCUMULATE = 8
 SPNERF_COMP_WEIGHTS_ONLY = 1
 
 

@@ -36,17 +36,52 @@ struct PackPiece {
     int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;
     int64_t dst;
 };
-constexpr int kMaxPieces = 24;
+constexpr int kMaxPieces = 64;
+constexpr int kPackTR = 32, kPackTC = 64;  // a block re-lays one 32 x 64 tile of a piece
 struct PackArgs {
     PackPiece p[kMaxPieces];
+    int tile0[kMaxPieces + 1];  // prefix of the pieces' tile counts (block ranges)
+    int n;
     float* packed;
 };
 
-__global__ void k_pack(PackArgs a) {
-    const PackPiece pc = a.p[blockIdx.y];
-    const int64_t n = (int64_t)pc.rows * pc.cols;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int r = (int)(i / pc.cols), c = (int)(i % pc.cols);
+// One launch for up to kMaxPieces pieces: block b re-lays tile (b - tile0[piece]) of its piece,
+// 8 elements per thread.  Transposed pieces (fp32 or bf16) go through an LDS tile so both the
+// read (rows of the source) and the write (rows of the transpose) are coalesced.
+__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+    __shared__ float tileT[kPackTC][kPackTR + 1];
+    const int b = blockIdx.x;
+    int pi = 0;
+    while (pi + 1 < a.n && a.tile0[pi + 1] <= b) ++pi;  // block-uniform
+    const PackPiece pc = a.p[pi];
+    const int t = b - a.tile0[pi];
+    const int tcols = (pc.cols + kPackTC - 1) / kPackTC;
+    const int r0 = (t / tcols) * kPackTR, c0 = (t % tcols) * kPackTC;
+    const int tid = threadIdx.x;
+    if (pc.transpose && pc.bf <= 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int rr = (tid >> 6) + 4 * e, cc = tid & 63;
+            const int r = r0 + rr, c = c0 + cc;
+            tileT[cc][rr] = (r < pc.rows && c < pc.cols) ? pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int rr = tid & 31, cc = (tid >> 5) + 8 * e;
+            const int r = r0 + rr, c = c0 + cc;
+            if (r < pc.rows && c < pc.cols) {
+                const int64_t o = pc.dst + (int64_t)c * pc.dst_ld + r;
+                if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)tileT[cc][rr];
+                else a.packed[o] = tileT[cc][rr];
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int r = r0 + (tid >> 6) + 4 * e, c = c0 + (tid & 63);
+        if (r >= pc.rows || c >= pc.cols) continue;
         const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
         if (pc.bf >= 3) {
             bf16* dst = reinterpret_cast<bf16*>(a.packed) + pc.dst;
@@ -740,7 +775,8 @@ __global__ __launch_bounds__(256) void k_ray_bwd(RayBwdArgs a) {
 // (nn.Embedding padding_idx, spnerf.py:191-194).
 // One block per (class, j): rays strided over 256 threads, then a fixed-order tree in LDS.
 __global__ __launch_bounds__(256) void k_class_sum(int64_t B, const float* __restrict__ gemb, int sd,
-                                                   const int64_t* __restrict__ labels, int C, float* __restrict__ out) {
+                                                   const int64_t* __restrict__ labels, int C, float* __restrict__ out,
+                                                   int accumulate) {
     __shared__ float red[256];
     const int c = blockIdx.x / sd, j = blockIdx.x % sd;
     float s = 0.f;
@@ -753,7 +789,7 @@ __global__ __launch_bounds__(256) void k_class_sum(int64_t B, const float* __res
         if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+    if (threadIdx.x == 0) out[blockIdx.x] = accumulate ? out[blockIdx.x] + red[0] : red[0];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -764,14 +800,16 @@ static int32_t launch_pack(const std::vector<PackPiece>& pieces, float* packed, 
     for (size_t b = 0; b < pieces.size(); b += kMaxPieces) {
         PackArgs a{};
         a.packed = packed;
-        int n = 0;
-        int64_t maxe = 1;
+        int n = 0, tiles = 0;
         for (size_t i = b; i < pieces.size() && n < kMaxPieces; ++i, ++n) {
             a.p[n] = pieces[i];
-            maxe = std::max(maxe, (int64_t)pieces[i].rows * pieces[i].cols);
+            a.tile0[n] = tiles;
+            tiles += cdiv(pieces[i].rows, kPackTR) * cdiv(pieces[i].cols, kPackTC);
         }
-        const int gx = (int)std::min<int64_t>((maxe + 255) / 256, 1024);
-        hipLaunchKernelGGL(k_pack, dim3(gx, n), dim3(256), 0, s, a);
+        a.tile0[n] = tiles;
+        a.n = n;
+        ProfScope prof("pack", s, 0.0, 0.0);
+        hipLaunchKernelGGL(k_pack, dim3(tiles), dim3(256), 0, s, a);
         SPN_HIP(hipGetLastError());
     }
     return SPNERF_OK;
@@ -877,6 +915,7 @@ struct Ctx {
     const float* P;  // packed
     float* ws;       // workspace base
     int S;
+    int acc = 0;     // backward: gradient reductions add into the flat gradient
     float* at(int64_t off) const { return ws + off; }
     const float* pk(int64_t off) const { return P + off; }
     bf16* hb(int64_t off) const { return reinterpret_cast<bf16*>(ws + off); }          // bf16 workspace buffer
@@ -925,6 +964,7 @@ static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int
     for (ReduceArgs r : outs) {
         r.slab = t.slab; r.ld_slab = K; r.slab_stride = t.slab_stride; r.splits = splits; r.N = N;
         r.slab_b = t.slab_b;
+        r.accumulate = c.acc;
         SPN_TRY(reduce_slabs(r, s));
     }
     return SPNERF_OK;
@@ -952,6 +992,7 @@ static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int M
     ReduceArgs r = red(0, Ma, K, dst, ld_dst, dst_b);
     r.slab = k.slab; r.ld_slab = K; r.slab_stride = (int64_t)Mt * K; r.splits = chunks; r.N = Mt; r.slab_b = k.slab_b;
     r.transpose = transpose;
+    r.accumulate = c.acc;
     if (dst) SPN_TRY(reduce_slabs(r, s));
     if (dst_ones) {
         ReduceArgs o = r;
@@ -1329,14 +1370,15 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
                             float* grad, float* grad_t, hipStream_t s) {
     SPN_ARG(flags & SPNERF_MLP_SAVE, "backward needs a workspace written with SPNERF_MLP_SAVE");
     SPN_ARG(!(flags & SPNERF_MLP_SIGMA_ONLY), "backward of a sigma-only pass is not supported");
-    Ctx c{d, packed_layout(d), ws_layout(d, n_rays, S, flags), packed, ws, S};
+    Ctx c{d, packed_layout(d), ws_layout(d, n_rays, S, flags & ~SPNERF_MLP_ACCUMULATE), packed, ws, S};
+    c.acc = (flags & SPNERF_MLP_ACCUMULATE) ? 1 : 0;
     const int mode = (flags & SPNERF_MLP_SUN_ONLY) ? 2 : 0;
     const int64_t P = n_rays * S;
     const int W = d.W, H = d.H;
     PIdx x;
     auto specs = param_specs(d, &x);
     const int64_t total = specs.back().off + specs.back().numel();
-    SPN_TRY(zero_fill(grad, total, s));
+    if (!c.acc) SPN_TRY(zero_fill(grad, total, s));
     if (grad_t && d.beta) SPN_TRY(zero_fill(grad_t, n_rays * d.td, s));
     if (P == 0) return SPNERF_OK;
     auto gp = [&](int pi) { return grad + specs[pi].off; };
@@ -1373,7 +1415,7 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
             SPN_TRY(skinny(c, B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R4), W, W, gp(x.fcW[d.skip]) + W + d.K0,
                            ld(x.fcW[d.skip]), 1, nullptr, nullptr, s));
             hipLaunchKernelGGL(k_class_sum, dim3((d.C + 1) * d.sd), dim3(256), 0, s, n_rays, c.at(c.w.gemb), d.sd, labels,
-                               d.C, gp(x.emb));
+                               d.C, gp(x.emb), c.acc);
             SPN_HIP(hipGetLastError());
         }
     }

@@ -74,11 +74,30 @@ def allreduce_grads(params, world: int, group=None):
     if not have:
         return
     grads = [p.grad for p in have]
+    flat = _shared_flat(grads)
+    if flat is not None:   # the .grads are consecutive views of one buffer (SPNeRF's flat gradient)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        flat.div_(world)
+        return
     flat = torch._utils._flatten_dense_tensors(grads)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     flat.div_(world)
     for p, g in zip(have, torch._utils._unflatten_dense_tensors(flat, grads)):
         p.grad.copy_(g)
+
+
+def _shared_flat(grads):
+    """The buffer the gradients are consecutive views of, covering it exactly; else None."""
+    base = grads[0]._base
+    if base is None or base.dim() != 1 or not base.is_contiguous():
+        return None
+    ptr, esz = base.data_ptr(), base.element_size()
+    off = 0
+    for g in grads:
+        if g._base is not base or g.data_ptr() != ptr + esz * off or not g.is_contiguous():
+            return None
+        off += g.numel()
+    return base if off == base.numel() else None
 
 
 def ce_scale(local_labels: torch.Tensor, global_labels: torch.Tensor, world: int) -> torch.Tensor:

@@ -23,7 +23,7 @@ import torch
 
 from . import _lib
 from .rng import current_random_source
-from .spnerf import inference_rays
+from .spnerf import inference_rays, pack_for_render
 
 
 def stratified(rays: torch.Tensor, n_samples: int, u: torch.Tensor) -> torch.Tensor:
@@ -163,16 +163,17 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
     if args.beta:
         rays_t = models["t"](ts) if ts is not None else None                       # rendering.py:156
     sem = semantics if model.sem else None
+    pk = pack_for_render(model)   # every pass of this render reads the same packed weights
     if args.guidedsample:
         with torch.no_grad():   # pass 1 feeds only the detached guided depths (rendering.py:164)
-            res1 = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, mode="sigma")
+            res1 = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, mode="sigma", pack=pk)
         cnf = None if clamp_near_far is None else clamp_near_far.reshape(2).to(rays.device, torch.float32).contiguous()
         z_vals, z_unsort = _guided(res1, z_vals, N_samples, rays, mode, valid_depth, target_depths, target_std, cnf)
-        result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, z_vals_unsort=z_unsort)
+        result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, z_vals_unsort=z_unsort, pack=pk)
     else:
-        result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t)
+        result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, pack=pk)
     if args.sc_lambda > 0:                                                           # rendering.py:171-177
-        sc = inference_rays(model, args, rays, z_vals, 8, sem, rays_t, mode="sun")
+        sc = inference_rays(model, args, rays, z_vals, 8, sem, rays_t, mode="sun", pack=pk)
         result["weights_sc"] = sc["weights"]
         result["transparency_sc"] = sc["transparency"]
         result["sun_sc"] = sc["sun"]
@@ -206,9 +207,10 @@ def _fine(models, args, rays, ts, z_vals, result_, semantics, rays_t_coarse):
     if args.beta:
         rays_t = models['t'](ts) if ts else None                                    # :201, as written there
     sem = semantics if model.sem else None
-    result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t)
+    pk = pack_for_render(model)
+    result = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, pack=pk)
     if args.sc_lambda > 0:
-        result_ = inference_rays(model, args, rays, z_vals, 8, sem, rays_t)        # :207 overwrites result_
+        result_ = inference_rays(model, args, rays, z_vals, 8, sem, rays_t, pack=pk)  # :207 overwrites result_
         result["weights_sc"] = result_["weights"]
         result["transparency_sc"] = result_["transparency"]
         result["sun_sc"] = result_["sun"]

@@ -19,7 +19,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_SAVE, SPNERF_MLP_SIGMA_ONLY, SPNERF_MLP_SUN_ONLY
+from ._lib import (SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_ACCUMULATE, SPNERF_MLP_SAVE, SPNERF_MLP_SIGMA_ONLY,
+                   SPNERF_MLP_SUN_ONLY)
 from .rng import current_random_source
 
 
@@ -130,6 +131,7 @@ class SPNeRF(torch.nn.Module):
         self._order = None
         self._packed = None
         self._pack_pool = []
+        self._flat_grad = None
 
     # ---------------------------------------------------------------- library plumbing
     def cfg(self) -> _lib.ModelCfg:
@@ -210,6 +212,35 @@ class SPNeRF(torch.nn.Module):
         if buf is not None and buf is not self._packed and len(self._pack_pool) < 4:
             self._pack_pool.append(buf)
 
+    def flat_grad_target(self, params):
+        """Where the MLP backward accumulates parameter gradients directly (no per-parameter
+        autograd accumulation, no flatten for the all-reduce): the model's flat gradient buffer,
+        when every parameter's ``.grad`` is its view — or, when every ``.grad`` is None, the
+        buffer zeroed, with its views installed as the ``.grad``s.  None otherwise (the
+        gradients then go back through autograd)."""
+        fb = self._flat_grad
+        if all(p.grad is None for p in params):
+            total = sum(p.numel() for p in params)
+            dev = params[0].device
+            if fb is None or fb.numel() != total or fb.device != dev:
+                fb = torch.empty(total, dtype=torch.float32, device=dev)
+                self._flat_grad = fb
+            fb.zero_()
+            off = 0
+            for p in params:
+                p.grad = fb[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            return fb
+        if fb is None:
+            return None
+        base, off = fb.data_ptr(), 0
+        for p in params:
+            g = p.grad
+            if g is None or g.data_ptr() != base + 4 * off or g.shape != p.shape or not g.is_contiguous():
+                return None
+            off += p.numel()
+        return fb
+
     def invalidate_packed(self) -> None:
         """Kept for callers that prepared a graph capture with it: packing is unconditional."""
 
@@ -248,9 +279,30 @@ class SPNeRF(torch.nn.Module):
 # autograd functions
 # ------------------------------------------------------------------------------------------
 
+class WeightPack:
+    """One packed copy of a model's weights shared by the MLP calls of one render (all passes
+    of a render_rays call see the same parameters).  A buffer of its own (``owned``) goes back to
+    the model's free list once the last backward that reads it has run."""
+
+    def __init__(self, model, owned: bool):
+        self.model, self.owned, self.pending = model, owned, 0
+        self.buf = model.packed_weights(own=owned)
+
+    def done(self):
+        self.pending -= 1
+        if self.pending == 0 and self.owned:
+            self.model.release_packed(self.buf)
+            self.buf = None
+
+
+def pack_for_render(model) -> "WeightPack":
+    """Pack once for a whole render: own buffer when gradients may be taken."""
+    return WeightPack(model, owned=torch.is_grad_enabled())
+
+
 class _MLP(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, model, rays, dir_offset, z, labels, temb, flags, *params):
+    def forward(ctx, model, pack, rays, dir_offset, z, labels, temb, flags, *params):
         cfg = model.cfg()
         B, S = z.shape
         dev = rays.device
@@ -261,12 +313,15 @@ class _MLP(torch.autograd.Function):
             _lib.check(-1, "workspace_bytes")
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
         out = torch.empty(B * S, model.number_of_outputs, dtype=torch.float32, device=dev)
-        packed = model.packed_weights(own=need_grad)
+        if pack is None or (need_grad and not pack.owned):
+            pack = WeightPack(model, owned=need_grad)
+        packed = pack.buf
         _lib.check(L.spnerf_mlp_forward(ctypes.byref(cfg), _lib.ptr(packed), _lib.ptr(rays), rays.stride(0), dir_offset,
                                         B, S, _lib.ptr(z), _lib.ptr(labels), _lib.ptr(temb), flags, _lib.ptr(ws),
                                         _lib.ptr(out), _lib.stream_of(rays)), "mlp_forward")
         if need_grad:
-            ctx.model, ctx.flags, ctx.ws, ctx.packed = model, flags, ws, packed
+            pack.pending += 1
+            ctx.model, ctx.flags, ctx.ws, ctx.pack, ctx.packed = model, flags, ws, pack, packed
             ctx.shape = (B, S)
             ctx.save_for_backward(rays, labels, temb)
         return out
@@ -277,28 +332,35 @@ class _MLP(torch.autograd.Function):
         model = ctx.model
         params = model.canonical_parameters()
         B, S = ctx.shape
-        total = sum(p.numel() for p in params)
-        grad = torch.empty(total, dtype=torch.float32, device=rays.device)
-        gt = torch.empty_like(temb) if (temb is not None and ctx.needs_input_grad[5]) else None
+        gt = torch.empty_like(temb) if (temb is not None and ctx.needs_input_grad[6]) else None
         if ctx.ws is None:
             raise RuntimeError("SPNeRF MLP backward called twice on the same forward (its activations are freed)")
         d_out = d_out.contiguous()
+        flags = ctx.flags
+        grad = model.flat_grad_target(params)
+        direct = grad is not None
+        if direct:   # add straight into the .grad views (the library's fixed-order reductions)
+            flags |= SPNERF_MLP_ACCUMULATE
+        else:
+            grad = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=rays.device)
         _lib.check(_lib.lib().spnerf_mlp_backward(ctypes.byref(model.cfg()), _lib.ptr(ctx.packed), _lib.ptr(rays),
-                                                  rays.stride(0), B, S, _lib.ptr(labels), _lib.ptr(temb), ctx.flags,
+                                                  rays.stride(0), B, S, _lib.ptr(labels), _lib.ptr(temb), flags,
                                                   _lib.ptr(ctx.ws), _lib.ptr(d_out), _lib.ptr(grad),
                                                   _lib.ptr(gt), _lib.stream_of(rays)), "mlp_backward")
-        model.release_packed(ctx.packed)
-        ctx.packed = None
+        ctx.pack.done()
+        ctx.pack = ctx.packed = None
+        ctx.ws = None
+        if direct:
+            return (None, None, None, None, None, None, gt, None, *([None] * len(params)))
         grads, off = [], 0
         for p in params:
             grads.append(grad[off:off + p.numel()].view_as(p))
             off += p.numel()
-        ctx.ws = None
-        return (None, None, None, None, None, gt, None, *grads)
+        return (None, None, None, None, None, None, gt, None, *grads)
 
 
 def run_mlp(model: SPNeRF, rays: torch.Tensor, z: torch.Tensor, dir_offset: int, labels=None, temb=None,
-            sigma_only=False, sun_only=False) -> torch.Tensor:
+            sigma_only=False, sun_only=False, pack: Optional[WeightPack] = None) -> torch.Tensor:
     """out (B·S, number_of_outputs) for xyz = rays[:, 0:3] + rays[:, dir:dir+3] · z."""
     _lib.require_device(rays, z, labels, temb)
     rays = rays.contiguous().float()
@@ -313,18 +375,20 @@ def run_mlp(model: SPNeRF, rays: torch.Tensor, z: torch.Tensor, dir_offset: int,
         if sigma_only:
             raise _lib.SpnerfError("sigma-only passes are not differentiable (run them under torch.no_grad())")
         flags |= SPNERF_MLP_SAVE
-        return _MLP.apply(model, rays, dir_offset, z, labels, temb, flags, *params)
+        return _MLP.apply(model, pack, rays, dir_offset, z, labels, temb, flags, *params)
     # No autograd: ray chunks of at most max_points_per_call() points each write a slice of one
     # output (the reference's args.chunk loop, spnerf.py:98, with chunks sized by the library's
     # per-call limit instead of 5120 points).
     B, S = z.shape
     cb = max(1, max_points_per_call(model) // S)
+    if pack is None:
+        pack = WeightPack(model, owned=False)
     if B <= cb:
-        return _MLP.apply(model, rays, dir_offset, z, labels, temb, flags, *params)
+        return _MLP.apply(model, pack, rays, dir_offset, z, labels, temb, flags, *params)
     out = torch.empty(B * S, model.number_of_outputs, dtype=torch.float32, device=rays.device)
     for i0 in range(0, B, cb):
         i1 = min(B, i0 + cb)
-        out[i0 * S:i1 * S] = _MLP.apply(model, rays[i0:i1], dir_offset, z[i0:i1],
+        out[i0 * S:i1 * S] = _MLP.apply(model, pack, rays[i0:i1], dir_offset, z[i0:i1],
                                         None if labels is None else labels[i0:i1],
                                         None if temb is None else temb[i0:i1], flags, *params)
     return out
@@ -402,11 +466,12 @@ def _result(model, out, z, rgb, depth, w, T, sem, z_unsort=None):
 
 
 def inference_rays(model: SPNeRF, args, rays, z_vals, dir_offset=3, semantics=None, rays_t=None, z_vals_unsort=None,
-                   mode="full"):
+                   mode="full", pack: Optional[WeightPack] = None):
     """inference() over rays given by (origin, direction) + depths, without materialising xyz:
-    mode 'full' (all heads), 'sun' (σ + sun, the solar-correction pass) or 'sigma'."""
+    mode 'full' (all heads), 'sun' (σ + sun, the solar-correction pass) or 'sigma'.  ``pack``:
+    the weights packed once for a whole render (``pack_for_render``)."""
     out = run_mlp(model, rays, z_vals, dir_offset, semantics if model.sem else None, rays_t if model.beta else None,
-                  sigma_only=mode == "sigma", sun_only=mode == "sun")
+                  sigma_only=mode == "sigma", sun_only=mode == "sun", pack=pack)
     rgb, depth, w, T, sem = composite(model, out, z_vals, args.noise_std, weights_only=mode != "full")
     return _result(model, out, z_vals, rgb, depth, w, T, sem, z_vals_unsort)
 
