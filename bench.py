@@ -39,7 +39,7 @@ import torch.distributed as dist  # noqa: E402
 
 import spnerf_amd  # noqa: E402
 from spnerf_amd import _lib, dp  # noqa: E402
-from spnerf_amd.losses import DepthLoss, SemanticLoss, SNerfLoss  # noqa: E402
+from spnerf_amd.losses import DepthLoss, FusedRenderLoss, SemanticLoss, SNerfLoss  # noqa: E402
 from spnerf_amd.scene import synthetic_scene  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec
@@ -393,6 +393,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line reported beside the default C4 at N=1")
     ap.add_argument("--torch-adam", action="store_true", help="torch.optim.Adam(fused=True) instead of spnerf_amd.optim.Adam")
+    ap.add_argument("--torch-loss", action="store_true", help="the losses module (plain torch) instead of the fused loss kernels")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-batch", type=int, default=0, help="rays per CPU-baseline step (default: the GPU step's batch)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
@@ -463,8 +464,9 @@ def run_train(a, config, rank, world, dev, secondary=False):
     B = c["global_batch"] // world if strong else c["batch"]
     sampler = dp.SharedSeedSampler(R["rays"].shape[0], B * world, rank, world, seed=0, device=dev)
     sloss = SNerfLoss(lambda_sc=c["sc_lambda"])
-    dloss = DepthLoss(lambda_ds=1.0) if c["depth"] else None
+    dloss = DepthLoss(lambda_ds=1.0, usealldepth=False) if c["depth"] else None
     semloss = SemanticLoss(lambda_ss=1.0) if c["sem"] else None
+    floss = None if a.torch_loss else FusedRenderLoss(c["sc_lambda"], 1.0 if c["depth"] else 0.0, 1.0 if c["sem"] else 0.0)
     s_final = c["n_samples"] * (2 if c["guided"] else 1)
 
     # Batch indices live in static buffers so that the captured step reads each new batch.
@@ -487,6 +489,11 @@ def run_train(a, config, rank, world, dev, secondary=False):
                       clamp_near_far=R["rays"].index_select(0, gidx[:1])[0, 6:8])
         sem = R["sems"][idx] if c["sem"] else None
         res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="train", **kw)
+        if floss is not None:   # the trainer's loss sum (main.py:143-174) in two kernels
+            loss, _ = floss(res, R["rgbs"][idx], R["depths"][idx], R["valid_depth"][idx], R["depth_std"][idx], sem,
+                            labels_global=R["sems"][gidx] if (world > 1 and sem is not None) else None, world=world)
+            loss.backward()
+            return loss.detach()
         loss, _ = sloss(res, R["rgbs"][idx])
         if dloss is not None:
             loss = loss + dloss(res, R["depths"][idx, 0], R["depths"][idx, 1], R["valid_depth"][idx], R["depth_std"][idx])[0]
@@ -576,7 +583,7 @@ def run_train(a, config, rank, world, dev, secondary=False):
 
     kernels = {}
     for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "trunk_bf16", "tn_skinny", "encode", "heads_fwd",
-              "heads_bwd", "composite_fwd", "composite_bwd", "sample_guided"):
+              "heads_bwd", "composite_fwd", "composite_bwd", "sample_guided", "render_loss", "pack", "adam"):
         s = _lib.prof_read(k)
         if s["launches"]:
             kernels[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / prof_steps,

@@ -97,6 +97,36 @@ int32_t spnerf_composite_backward(int64_t n_rays, int32_t n_samples, const float
                                   const float* g_weights, const float* g_transparency, const float* g_sem,
                                   float* d_out, void* stream);
 
+/* ---- training losses (modules/metrics.py as main.py:125-174 combines them) ------------------
+ * loss = SNerfLoss colour MSE (rgb, target (B,3); rgb NULL = off)                  metrics.py:27-45
+ *      + solar_correction terms 2, 3 (lambda_sc > 0; sun_sc[(r*S+s)*ld_sun], T_sc, w_sc (B,S))  :17-24
+ *      + DepthLoss subset MSE form (lambda_ds > 0; depth (B), z, w (B,S), target depth / weight at
+ *        stride ld_td, valid_depth int64, target_std)                              :82-132,151-153
+ *      + lambda_ss * SemanticLoss cross-entropy, ignore_index -100 (logits (B,C) NULL = off)  :162-183
+ * The CE mean runs over the valid labels of labels_global[0..n_global) divided by `world` (data
+ * parallelism: the ranks' losses average to the global loss; single process: labels_global =
+ * labels, world = 1).  loss_out (device, 7 floats): [0] loss, [1..5] colour, sc2, sc3, depth, CE,
+ * [6] the CE denominator.  Deterministic (fixed-order partial sums in `workspace`).  The
+ * backward writes the gradients of g_loss[0] * loss w.r.t. rgb, sun_sc (dense (B,S)), depth and
+ * logits, reading loss_out[6]. */
+int64_t spnerf_render_loss_workspace_bytes(int64_t n_rays);
+int32_t spnerf_render_loss_forward(int64_t n_rays, int32_t n_samples, int32_t n_classes, const float* rgb,
+                                   const float* target, float lambda_sc, const float* sun_sc, int32_t ld_sun,
+                                   const float* T_sc, const float* w_sc, float lambda_ds, const float* depth,
+                                   const float* z, const float* w, const float* target_depth,
+                                   const float* target_weight, int32_t ld_td, const int64_t* valid_depth,
+                                   const float* target_std, float lambda_ss, const float* logits,
+                                   const int64_t* labels, const int64_t* labels_global, int64_t n_global,
+                                   int32_t world, void* workspace, float* loss_out, void* stream);
+int32_t spnerf_render_loss_backward(int64_t n_rays, int32_t n_samples, int32_t n_classes, const float* rgb,
+                                    const float* target, float lambda_sc, const float* sun_sc, int32_t ld_sun,
+                                    const float* T_sc, const float* w_sc, float lambda_ds, const float* depth,
+                                    const float* z, const float* w, const float* target_depth,
+                                    const float* target_weight, int32_t ld_td, const int64_t* valid_depth,
+                                    const float* target_std, float lambda_ss, const float* logits,
+                                    const int64_t* labels, const float* loss_out, const float* g_loss,
+                                    float* d_rgb, float* d_sun_sc, float* d_depth, float* d_logits, void* stream);
+
 /* ---- sample generation (rendering.py) --------------------------------------------------- */
 /* stratified jittered depths, perturb = 1 (rendering.py:131-144); u (n_rays, n) in [0,1) */
 int32_t spnerf_sample_stratified(int64_t n_rays, int32_t n_samples, const float* rays, int32_t ray_stride,

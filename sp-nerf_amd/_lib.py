@@ -48,6 +48,15 @@ SIGNATURES = {
     "spnerf_composite_backward": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_int32,
                                             c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p]),
+    "spnerf_render_loss_workspace_bytes": (c_int64, [c_int64]),
+    "spnerf_render_loss_forward": (c_int32, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_float, c_void_p, c_int32,
+                                             c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_int32, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_int64,
+                                             c_int32, c_void_p, c_void_p, c_void_p]),
+    "spnerf_render_loss_backward": (c_int32, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_float, c_void_p, c_int32,
+                                              c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_int32, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "spnerf_sample_stratified": (c_int32, [c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "spnerf_sample_guided": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -1,13 +1,39 @@
-"""Training losses over the render dictionary — mirrors modules/metrics.py of the reference
-(SNerfLoss :27-45, solar_correction :17-24, DepthLoss :68-159, SemanticLoss :162-183, psnr
-:206-207).  Plain torch ops on (B, ·) tensors; the per-point work stays in the HIP kernels.
-(A fused loss + composite-backward kernel is the next §8(f) row.)"""
+"""Training losses over the render dictionary — drop-in for modules/metrics.py of the reference.
+
+Same classes, constructor arguments, dictionary keys and reductions as metrics.py:
+``uncertainty_aware_loss`` :10-14, ``solar_correction`` :17-24, ``SNerfLoss`` :27-45,
+``SatNerfLoss`` :48-65, ``DepthLoss`` :68-159 (subset MSE, subset GNLL, use-all-depth),
+``SemanticLoss`` :162-183, ``load_loss`` :186-194, ``mse`` / ``psnr`` :197-207, each with its
+``*_fine`` terms when the render carries fine keys.  These are plain torch on (B, ·) tensors and
+pinned to the reference's own values and gradients (tests/golden/losses.npz,
+tests/test_losses.py).
+
+One deliberate difference, not in the values: the reference selects the depth-loss rays with
+boolean indexing, a device→host count per step; here the same sums run under a 0/1 mask, so a
+step has no host synchronisation and can be captured in a HIP graph.
+
+For the training step's own combination (SNerfLoss with the solar terms + subset MSE depth
+loss + semantic cross-entropy) ``FusedRenderLoss`` computes the loss value and every upstream
+gradient in ONE kernel (``spnerf_render_loss``, csrc/loss.hip) instead of ~60 small ATen launches.
+"""
 from __future__ import annotations
+
+import ctypes
 
 import torch
 
 
+def uncertainty_aware_loss(loss_dict, inputs, gt_rgb, typ, beta_min=0.05):
+    """metrics.py:10-14 (β of the COARSE pass weights either pass's colour, as there)."""
+    beta = torch.sum(inputs[f"weights_{typ}"].unsqueeze(-1) * inputs["beta_coarse"], -2) + beta_min
+    loss_dict[f"{typ}_color"] = ((inputs[f"rgb_{typ}"] - gt_rgb) ** 2 / (2 * beta ** 2)).mean()
+    loss_dict[f"{typ}_logbeta"] = (3 + torch.log(beta).mean()) / 2
+    return loss_dict
+
+
 def solar_correction(loss_dict, inputs, typ, lambda_sc=0.05):
+    """metrics.py:17-24: Shadow-NeRF terms 2 and 3 (transparency / weights of the solar pass
+    detached: only sun_sc receives a gradient)."""
     sun_sc = inputs[f"sun_sc_{typ}"].squeeze()
     term2 = torch.sum(torch.square(inputs[f"transparency_sc_{typ}"].detach() - sun_sc), -1)
     term3 = 1 - torch.sum(inputs[f"weights_sc_{typ}"].detach() * sun_sc, -1)
@@ -17,56 +43,232 @@ def solar_correction(loss_dict, inputs, typ, lambda_sc=0.05):
 
 
 class SNerfLoss(torch.nn.Module):
+    """metrics.py:27-45."""
+
     def __init__(self, lambda_sc=0.05):
         super().__init__()
         self.lambda_sc = lambda_sc
         self.loss = torch.nn.MSELoss(reduction="mean")
 
     def forward(self, inputs, targets):
-        loss_dict = {"coarse_color": self.loss(inputs["rgb_coarse"], targets)}
-        if self.lambda_sc > 0:
-            loss_dict = solar_correction(loss_dict, inputs, "coarse", self.lambda_sc)
+        loss_dict = {}
+        for typ in ("coarse", "fine"):
+            if typ == "fine" and "rgb_fine" not in inputs:
+                break
+            loss_dict[f"{typ}_color"] = self.loss(inputs[f"rgb_{typ}"], targets)
+            if self.lambda_sc > 0:
+                loss_dict = solar_correction(loss_dict, inputs, typ, self.lambda_sc)
         return sum(loss_dict.values()), loss_dict
 
 
+class SatNerfLoss(torch.nn.Module):
+    """metrics.py:48-65: colour weighted by the rendered uncertainty β, plus log β."""
+
+    def __init__(self, lambda_sc=0.0):
+        super().__init__()
+        self.lambda_sc = lambda_sc
+
+    def forward(self, inputs, targets):
+        loss_dict = {}
+        for typ in ("coarse", "fine"):
+            if typ == "fine" and "rgb_fine" not in inputs:
+                break
+            loss_dict = uncertainty_aware_loss(loss_dict, inputs, targets, typ)
+            if self.lambda_sc > 0:
+                loss_dict = solar_correction(loss_dict, inputs, typ, self.lambda_sc)
+        return sum(loss_dict.values()), loss_dict
+
+
+def _gaussian_nll(inp, target, var, eps=1e-6):
+    """Elementwise torch.nn.GaussianNLLLoss (full=False): the variance is clamped to eps with
+    the clamp invisible to autograd, as torch does."""
+    var = var + (var.clamp(min=eps) - var).detach()
+    return 0.5 * (torch.log(var) + (inp - target) ** 2 / var)
+
+
 class DepthLoss(torch.nn.Module):
-    """Subset depth loss (usealldepth=False — the trainer's default, opt.py:79 — MSE form,
-    metrics.py:82-132,151-153).
+    """metrics.py:68-159.  ``usealldepth`` (the reference default): λ/3 · mean(w · (d − t)²) over
+    all rays.  Otherwise the subset form: rays with a depth prior (valid) whose prediction lies
+    outside the expected distribution (|d − t| > σ_t or σ_pred > σ_t, :78-80), each term scaled by
+    n_applied / B (:125-127) before the mean over the applied rays — i.e. λ/3 · Σ_applied term / B;
+    term = w · (d − t)² (MSE) or the Gaussian NLL with variance σ_pred (GNLL, :129-130), where
+    σ_pred = sqrt(Σ weights · (z − d)²) (:102) carries a gradient in the GNLL form only."""
 
-    The reference selects the valid rays, then the rays outside the expected distribution,
-    and returns λ/3 · mean((n_apply / B) · tw · (pd − td)²) over the selected rays, i.e.
-    λ/3 · Σ_{valid ∧ apply} tw · (pd − td)² / B (0 when nothing is selected).  The same sum is
-    taken here with a 0/1 mask instead of boolean indexing, so it needs no host sync (boolean
-    indexing is a device→host count) and can be captured in a HIP graph.  The predicted std
-    only enters the comparison, so no gradient flows through its sqrt."""
-
-    def __init__(self, lambda_ds=1.0):
+    def __init__(self, lambda_ds=1.0, GNLL=False, usealldepth=True, margin=0, stdscale=1):
         super().__init__()
         self.lambda_ds = lambda_ds / 3.0
+        self.GNLL = GNLL
+        self.usealldepth = usealldepth
+        self.margin = margin
+        self.stdscale = stdscale
 
-    def forward(self, inputs, target_depth, target_weight, target_valid_depth, target_std):
-        z = inputs["z_vals_coarse"]
-        pd = inputs["depth_coarse"]
-        pw = inputs["weights_coarse"]
+    @staticmethod
+    def is_not_in_expected_distribution(pred_depth, pred_std, target_depth, target_std):
+        depth_diff = (pred_depth - target_depth).abs()
+        return torch.logical_or(depth_diff > target_std, pred_std > target_std)
+
+    def subset_term(self, inputs, typ, target_depth, target_weight, target_valid_depth, target_std):
+        z, pd, pw = inputs[f"z_vals_{typ}"], inputs[f"depth_{typ}"], inputs[f"weights_{typ}"]
+        if target_valid_depth is None:
+            target_valid_depth = torch.ones(pd.shape[0], device=pd.device)
+        B = float(target_valid_depth.shape[0])
+        pstd = (((z - pd.unsqueeze(-1)).pow(2) * pw).sum(-1)).sqrt()
         with torch.no_grad():
-            pstd = (((z - pd.unsqueeze(-1)).pow(2) * pw).sum(-1)).sqrt()
-            apply = (target_valid_depth > 0) & torch.logical_or((pd - target_depth).abs() > target_std,
-                                                                pstd > target_std)
+            apply = (target_valid_depth > 0) & self.is_not_in_expected_distribution(pd, pstd, target_depth, target_std)
             m = apply.to(pd.dtype)
-        loss = self.lambda_ds * torch.sum(m * target_weight * (pd - target_depth) ** 2) / float(pd.shape[0])
-        return loss, {"coarse_ds": loss}
+        if self.GNLL:
+            term = _gaussian_nll(pd, target_depth, torch.where(apply, pstd, torch.ones_like(pstd)))
+        else:
+            term = target_weight * (pd - target_depth) ** 2
+        return self.lambda_ds * torch.sum(m * term) / B
+
+    def forward(self, inputs, targets, weights=1.0, target_valid_depth=None, target_std=None):
+        loss_dict = {}
+        for typ in ("coarse", "fine"):
+            if typ == "fine" and "depth_fine" not in inputs:
+                break
+            if self.usealldepth:
+                loss_dict[f"{typ}_ds"] = self.lambda_ds * torch.mean(weights * (inputs[f"depth_{typ}"] - targets) ** 2)
+            else:
+                loss_dict[f"{typ}_ds"] = self.subset_term(inputs, typ, targets, weights, target_valid_depth, target_std)
+        return sum(loss_dict.values()), loss_dict
 
 
 class SemanticLoss(torch.nn.Module):
+    """metrics.py:162-183: cross-entropy of the ray's mean semantic logits, ignore_index −100."""
+
     def __init__(self, lambda_ss=1.0):
         super().__init__()
         self.lambda_ss = lambda_ss
-        self.ce = torch.nn.CrossEntropyLoss(ignore_index=-100)
+        self.cross_entropy_loss = torch.nn.CrossEntropyLoss(ignore_index=-100)
 
     def forward(self, inputs, targets):
-        loss = self.lambda_ss * self.ce(inputs["sem_logits_coarse"], targets)
-        return loss, {"coarse_ss": loss}
+        loss_dict = {"coarse_ss": self.cross_entropy_loss(inputs["sem_logits_coarse"], targets)}
+        if "sem_logits_fine" in inputs:
+            loss_dict["fine_ss"] = self.cross_entropy_loss(inputs["sem_logits_fine"], targets)
+        for k in loss_dict:
+            loss_dict[k] = self.lambda_ss * loss_dict[k]
+        return sum(loss_dict.values()), loss_dict
 
 
-def psnr(image_pred, image_gt):
-    return -10 * torch.log10(torch.mean((image_pred - image_gt) ** 2))
+def load_loss(args):
+    """metrics.py:186-194."""
+    if args.model == "sp-nerf":
+        return SatNerfLoss(lambda_sc=args.sc_lambda) if args.beta else SNerfLoss(lambda_sc=args.sc_lambda)
+    raise ValueError(f"model {args.model} is not valid")
+
+
+def mse(image_pred, image_gt, valid_mask=None, reduction="mean"):
+    value = (image_pred - image_gt) ** 2
+    if valid_mask is not None:
+        value = value[valid_mask]
+    if reduction == "mean":
+        return torch.mean(value)
+    return value
+
+
+def psnr(image_pred, image_gt, valid_mask=None, reduction="mean"):
+    return -10 * torch.log10(mse(image_pred, image_gt, valid_mask, reduction))
+
+
+# ------------------------------------------------------------------------------------------
+# fused training loss (csrc/loss.hip)
+# ------------------------------------------------------------------------------------------
+
+class _RenderLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rgb, sun_sc, depth, logits, cfg):
+        from . import _lib
+        L = _lib.lib()
+        B, S, C = cfg["B"], cfg["S"], cfg["C"]
+        dev = rgb.device
+        ws = torch.empty(max(1, L.spnerf_render_loss_workspace_bytes(B) // 4), dtype=torch.float32, device=dev)
+        out = torch.empty(7, dtype=torch.float32, device=dev)
+        p = _lib.ptr
+        _lib.check(L.spnerf_render_loss_forward(
+            B, S, C, p(rgb), p(cfg["target"]), cfg["lambda_sc"], p(sun_sc), cfg["ld_sun"], p(cfg["T_sc"]), p(cfg["w_sc"]),
+            cfg["lambda_ds"], p(depth), p(cfg["z"]), p(cfg["w"]), p(cfg["td"]), p(cfg["tw"]), cfg["ld_td"], p(cfg["valid"]),
+            p(cfg["tstd"]), cfg["lambda_ss"], p(logits), p(cfg["labels"]), p(cfg["labels_global"]), cfg["n_global"],
+            cfg["world"], p(ws), p(out), _lib.stream_of(rgb)), "render_loss_forward")
+        ctx.cfg = cfg
+        ctx.save_for_backward(rgb, sun_sc, depth, logits, out)
+        terms = out[1:6]
+        ctx.mark_non_differentiable(terms)
+        return out[0], terms
+
+    @staticmethod
+    def backward(ctx, g_loss, g_terms):
+        from . import _lib
+        rgb, sun_sc, depth, logits, out = ctx.saved_tensors
+        cfg = ctx.cfg
+        B, S, C = cfg["B"], cfg["S"], cfg["C"]
+        g = g_loss.contiguous().reshape(1)
+        d_rgb = torch.empty_like(rgb)
+        d_sun = torch.empty(B, S, 1, dtype=torch.float32, device=rgb.device) if cfg["lambda_sc"] > 0 else None
+        d_depth = torch.empty_like(depth) if cfg["lambda_ds"] > 0 else None
+        d_logits = torch.empty_like(logits) if cfg["lambda_ss"] is not None and logits.numel() else None
+        p = _lib.ptr
+        _lib.check(_lib.lib().spnerf_render_loss_backward(
+            B, S, C, p(rgb), p(cfg["target"]), cfg["lambda_sc"], p(sun_sc), cfg["ld_sun"], p(cfg["T_sc"]), p(cfg["w_sc"]),
+            cfg["lambda_ds"], p(depth), p(cfg["z"]), p(cfg["w"]), p(cfg["td"]), p(cfg["tw"]), cfg["ld_td"], p(cfg["valid"]),
+            p(cfg["tstd"]), cfg["lambda_ss"], p(logits if logits.numel() else None), p(cfg["labels"]), p(out), p(g),
+            p(d_rgb), p(d_sun), p(d_depth), p(d_logits), _lib.stream_of(rgb)), "render_loss_backward")
+        return d_rgb, d_sun, d_depth, d_logits, None
+
+
+class FusedRenderLoss(torch.nn.Module):
+    """The training step's combined loss in two kernels (csrc/loss.hip): SNerfLoss(lambda_sc)
+    + DepthLoss(lambda_ds, usealldepth=False) (MSE form) + SemanticLoss(lambda_ss), as
+    main.py:143-174 adds them (coarse keys, no β, no fine model).  Returns (loss, terms) like
+    the reference modules, terms = {coarse_color, coarse_sc_term2, coarse_sc_term3, coarse_ds,
+    coarse_ss} (0-d device tensors, no gradient).
+
+    ``labels_global`` / ``world`` (data parallelism): the CE mean runs over the valid labels of
+    the GLOBAL batch divided by ``world``, so the ranks' losses average to the global one
+    (SURVEY §8e pitfall 2); default = this batch, world 1."""
+
+    def __init__(self, lambda_sc=0.05, lambda_ds=0.0, lambda_ss=0.0):
+        super().__init__()
+        self.lambda_sc, self.lambda_ds, self.lambda_ss = float(lambda_sc), float(lambda_ds), float(lambda_ss)
+
+    def forward(self, inputs, targets, target_depths=None, target_valid_depth=None, target_std=None, semantics=None,
+                labels_global=None, world=1):
+        from . import _lib
+        rgb = inputs["rgb_coarse"]
+        _lib.require_device(rgb)
+        B = rgb.shape[0]
+        dev = rgb.device
+        f32 = lambda t: t.contiguous().float()
+        cfg = dict(B=B, S=1, C=0, target=f32(targets), lambda_sc=0.0, ld_sun=1, T_sc=None, w_sc=None, lambda_ds=0.0, z=None,
+                   w=None, td=None, tw=None, ld_td=2, valid=None, tstd=None, lambda_ss=0.0, labels=None,
+                   labels_global=None, n_global=0, world=int(world))
+        sun = depth = None
+        if self.lambda_sc > 0:
+            sun = inputs["sun_sc_coarse"]
+            S = sun.shape[1]
+            if sun.stride(1) != sun.stride(0) // S or sun.stride(0) % S:
+                sun = sun.contiguous()
+            cfg.update(S=S, lambda_sc=self.lambda_sc, ld_sun=sun.stride(1), T_sc=f32(inputs["transparency_sc_coarse"]),
+                       w_sc=f32(inputs["weights_sc_coarse"]))
+        if self.lambda_ds > 0:
+            depth = inputs["depth_coarse"].contiguous()
+            z = f32(inputs["z_vals_coarse"])
+            td = target_depths.float()
+            if td.dim() != 2 or td.stride(1) != 1:
+                td = td.contiguous()
+            cfg.update(S=z.shape[1], lambda_ds=self.lambda_ds, z=z, w=f32(inputs["weights_coarse"].detach()), td=td,
+                       tw=td[:, 1:], ld_td=td.stride(0), valid=target_valid_depth.reshape(-1).long().contiguous(),
+                       tstd=f32(target_std.reshape(-1)))
+        logits = torch.empty(0, device=dev)
+        if self.lambda_ss > 0:
+            logits = inputs["sem_logits_coarse"].contiguous()
+            labels = semantics.reshape(-1).long().contiguous()
+            lg = labels if labels_global is None else labels_global.reshape(-1).long().contiguous()
+            cfg.update(C=logits.shape[1], lambda_ss=self.lambda_ss, labels=labels, labels_global=lg, n_global=lg.numel())
+        if sun is None:
+            sun = torch.empty(0, device=dev)
+        if depth is None:
+            depth = torch.empty(0, device=dev)
+        loss, terms = _RenderLoss.apply(rgb.contiguous(), sun, depth, logits, cfg)
+        names = ("coarse_color", "coarse_sc_term2", "coarse_sc_term3", "coarse_ds", "coarse_ss")
+        return loss, {n: terms[i] for i, n in enumerate(names)}

@@ -279,6 +279,84 @@ def dropins(ref_spnerf, ref_rendering):
     print("dropins_w64 written")
 
 
+def load_metrics(ref: str):
+    """modules/metrics.py with its only non-torch import (kornia, for SSIM) stubbed."""
+    from unittest import mock
+    saved = {k: sys.modules.get(k) for k in ("kornia", "kornia.losses")}
+    for k in saved:
+        sys.modules[k] = mock.MagicMock()
+    try:
+        import modules.metrics as metrics
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    return metrics
+
+
+def losses(ref: str):
+    """The reference losses (modules/metrics.py:10-207) on render-shaped random inputs: SNerfLoss
+    (+ solar terms, + fine keys), SatNerfLoss (β uncertainty), DepthLoss in its subset MSE, subset
+    GNLL and use-all-depth forms, SemanticLoss (ignore_index -100, + fine), psnr.  Stores the
+    inputs, every loss value and the gradient w.r.t. every differentiable input."""
+    metrics = load_metrics(ref)
+    rng = np.random.default_rng(31)
+    B, S, C = 40, 24, 3
+    t = lambda a: torch.tensor(np.asarray(a, np.float32), requires_grad=True)
+    data = {}
+    inp = {}
+    for typ in ("coarse", "fine"):
+        w = rng.uniform(0, 1, (B, S)) ** 3
+        w = w / w.sum(1, keepdims=True) * rng.uniform(0.6, 1.0, (B, 1))
+        z = np.sort(rng.uniform(0, 0.2, (B, S)), 1)
+        raw = dict(rgb=rng.uniform(0, 1, (B, 3)), depth=(w * z).sum(1), weights=w, z_vals=z,
+                   sun_sc=rng.uniform(0, 1, (B, S, 1)), transparency_sc=np.cumprod(rng.uniform(0.8, 1, (B, S)), 1),
+                   weights_sc=rng.uniform(0, 0.1, (B, S)), sem_logits=rng.normal(size=(B, C)),
+                   beta=rng.uniform(0.01, 0.5, (B, S, 1)))
+        for k, v in raw.items():
+            inp[f"{k}_{typ}"] = v.astype(np.float32)
+    targets = rng.uniform(0, 1, (B, 3)).astype(np.float32)
+    depth_t = (inp["depth_coarse"] * rng.uniform(0.7, 1.3, B)).astype(np.float32)
+    depth_w = rng.uniform(0.2, 1, B).astype(np.float32)
+    valid = (rng.uniform(size=B) < 0.7).astype(np.int64)
+    dstd = rng.uniform(1e-3, 0.02, B).astype(np.float32)
+    labels = rng.choice([0, 1, 2, -100], size=B, p=[0.3, 0.3, 0.25, 0.15]).astype(np.int64)
+    data.update({"in_" + k: v for k, v in inp.items()})
+    data.update(in_targets=targets, in_depth_t=depth_t, in_depth_w=depth_w, in_valid=valid, in_dstd=dstd,
+                in_labels=labels)
+
+    def run(tag, keys, fn):
+        tens = {k: t(inp[k]) for k in keys}
+        loss, ld = fn(tens)
+        loss.backward()
+        data[f"{tag}|loss"] = np.array(float(loss))
+        for k, v in ld.items():
+            data[f"{tag}|term|{k}"] = np.array(float(v))
+        for k, v in tens.items():
+            data[f"{tag}|grad|{k}"] = (v.grad if v.grad is not None else torch.zeros_like(v)).numpy()
+
+    co = [k for k in inp if k.endswith("_coarse")]
+    al = list(inp)
+    tg = torch.tensor(targets)
+    dt, dw, dv, ds = torch.tensor(depth_t), torch.tensor(depth_w), torch.tensor(valid), torch.tensor(dstd)
+    run("snerf_sc", co, lambda x: metrics.SNerfLoss(lambda_sc=0.1)(x, tg))
+    run("snerf_fine", al, lambda x: metrics.SNerfLoss(lambda_sc=0.05)(x, tg))
+    run("satnerf_sc", co, lambda x: metrics.SatNerfLoss(lambda_sc=0.1)(x, tg))
+    run("satnerf_fine", al, lambda x: metrics.SatNerfLoss(lambda_sc=0.0)(x, tg))
+    run("depth_subset", co, lambda x: metrics.DepthLoss(lambda_ds=1.0, usealldepth=False)(x, dt, dw, dv, ds))
+    run("depth_subset_fine", al, lambda x: metrics.DepthLoss(lambda_ds=0.7, usealldepth=False)(x, dt, dw, dv, ds))
+    run("depth_gnll", co, lambda x: metrics.DepthLoss(lambda_ds=1.0, GNLL=True, usealldepth=False)(x, dt, dw, dv, ds))
+    run("depth_all", al, lambda x: metrics.DepthLoss(lambda_ds=1.0, usealldepth=True)(x, dt, dw, dv, ds))
+    lab = torch.tensor(labels)
+    run("sem", co, lambda x: metrics.SemanticLoss(lambda_ss=0.04)(x, lab))
+    run("sem_fine", al, lambda x: metrics.SemanticLoss(lambda_ss=1.0)(x, lab))
+    data["psnr"] = np.array(float(metrics.psnr(torch.tensor(inp["rgb_coarse"]), tg)))
+    np.savez_compressed(os.path.join(HERE, "losses.npz"), **data)
+    print("losses written", len(data), "arrays")
+
+
 def init_weights(ref_spnerf):
     """SPNeRF(...) built after torch.manual_seed(7): the reference's own initialisation, for the
     seeded-init equivalence test of the drop-in module (stored as per-parameter sums and
@@ -397,6 +475,7 @@ def main():
     unit_composite(ref_spnerf)
     init_weights(ref_spnerf)
     dropins(ref_spnerf, ref_rendering)
+    losses(a.ref)
 
 
 if __name__ == "__main__":

@@ -72,7 +72,7 @@ def step_grads(rank, world, precision):
                                      valid_depth=R.valid_depth[idx], target_depths=R.depths[idx],
                                      target_std=R.depth_std[idx], clamp_near_far=R.rays[gidx[0], 6:8])
     loss = SNerfLoss(lambda_sc=0.1)(res, R.rgbs[idx])[0]
-    loss = loss + DepthLoss(1.0)(res, R.depths[idx, 0], R.depths[idx, 1], R.valid_depth[idx], R.depth_std[idx])[0]
+    loss = loss + DepthLoss(1.0, usealldepth=False)(res, R.depths[idx, 0], R.depths[idx, 1], R.valid_depth[idx], R.depth_std[idx])[0]
     sl = SemanticLoss(1.0)(res, sem)[0]
     loss = loss + (dp.shard_ce(sl, sem, R.sems[gidx], world) if world > 1 else sl)
     loss.backward()

@@ -61,7 +61,7 @@ def test_graph_replay_matches_eager_step(precision):
     m_e = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=128, mapping=True, sem=True, precision=precision).to(DEV)
     m_g = copy.deepcopy(m_e)
     src = StaticRandom()
-    sl, dl, ce = SNerfLoss(lambda_sc=0.1), DepthLoss(1.0), SemanticLoss(1.0)
+    sl, dl, ce = SNerfLoss(lambda_sc=0.1), DepthLoss(1.0, usealldepth=False), SemanticLoss(1.0)
 
     def fwd_bwd(model):
         src.reset()
@@ -112,7 +112,7 @@ def test_graph_training_matches_eager_training():
     o_e = torch.optim.Adam(m_e.parameters(), lr=5e-4, fused=True)
     o_g = torch.optim.Adam(m_g.parameters(), lr=5e-4, fused=True)
     src = StaticRandom(3)
-    sl, dl, ce = SNerfLoss(lambda_sc=0.1), DepthLoss(1.0), SemanticLoss(1.0)
+    sl, dl, ce = SNerfLoss(lambda_sc=0.1), DepthLoss(1.0, usealldepth=False), SemanticLoss(1.0)
 
     def fwd_bwd(model):
         src.reset()

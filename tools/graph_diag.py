@@ -28,7 +28,7 @@ mode = sys.argv[1] if len(sys.argv) > 1 else "update+eager"
 m_e = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=128, mapping=True, sem=True).to(DEV)
 m_g = copy.deepcopy(m_e)
 src = StaticRandom()
-sl, dl, ce = SNerfLoss(lambda_sc=0.1), DepthLoss(1.0), SemanticLoss(1.0)
+sl, dl, ce = SNerfLoss(lambda_sc=0.1), DepthLoss(1.0, usealldepth=False), SemanticLoss(1.0)
 
 
 def fwd_bwd(model):
