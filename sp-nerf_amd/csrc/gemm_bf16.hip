@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void k_gemm_nt_bf16(NT16Args g, int ntiles) {
                 const int row = bm + wr * 64 + i * 32 + (lane >> 3) + 8 * q4;
                 if (row < g.M && colok) {
                     *reinterpret_cast<u32x4*>(g.C + (int64_t)row * g.ldc + col) = oc[q4];
-                    if (g.Dout) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
+                    if (g.Dout && sine_cols) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
                 }
             }
         }
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_bf16w(NT16Args g, in
                     const int row = bm + wr * MI * 32 + i * 32 + (lane >> 3) + 8 * q4;
                     if (row < g.M && colok) {
                         *reinterpret_cast<u32x4*>(g.C + (int64_t)row * g.ldc + col) = oc[q4];
-                        if (g.Dout) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
+                        if (g.Dout && sine_cols) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
                     }
                 }
             }
@@ -929,8 +929,11 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     SPN_ARG(a.rowbias == nullptr || (a.rows_per_ray > 0 && a.ld_rb % 4 == 0), "gemm_nt_bf16: rowbias");
     if (a.M == 0) return SPNERF_OK;
     const int ntiles = cdiv(a.M, HB) * cdiv(a.N, HB);
+    // algorithmic bytes: A and B once, C, the derivative of the sine columns, the Dmul read
+    const double dcols = (a.Dout && a.act == 1) ? (double)(a.N - std::min(a.n_lin, a.N)) : 0.0;
     ProfScope prof("gemm_nt_bf16", s, 2.0 * a.M * a.N * a.K,
-                   2.0 * ((double)a.M * a.K + (double)a.N * a.K + (2.0 + (a.Dmul ? 1 : 0)) * a.M * a.N));
+                   2.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N * (1.0 + (a.Dmul ? 1.0 : 0.0)) +
+                          (double)a.M * dcols));
     // variants: 1 / 2 = one block per tile, prefetch depth 1 / 2; 3 / 4 = persistent grid of
     // two blocks per CU (the LDS limit), depth 1 / 2
     const int v = variant > 0 ? variant : g_nt16_variant;

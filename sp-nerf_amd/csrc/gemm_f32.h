@@ -13,7 +13,8 @@ struct NTArgs {
     float* C = nullptr; int ldc = 0;
     int M = 0, N = 0, K = 0;
     // epilogue, in order: + bias[col] + rowbias[row/rows_per_ray][col] + r1_a[row]*r1_v[col];
-    // act==1 and col>=n_lin: y = sin(w0*v), Dout = w0*cos(w0*v) (else y = v, Dout = 1); y *= Dmul
+    // act==1 and col>=n_lin: y = sin(w0*v), Dout = w0*cos(w0*v); linear columns: y = v, Dout not
+    // written (nothing reads a linear derivative); y *= Dmul
     const float* bias = nullptr;
     const float* rowbias = nullptr; int ld_rb = 0; int rows_per_ray = 1;
     const float* r1_a = nullptr; int r1_lda = 0; const float* r1_v = nullptr;

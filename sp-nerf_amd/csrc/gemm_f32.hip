@@ -144,7 +144,6 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
                     float v = acc[i][j][r] + bias;
                     v += rbv[r];
                     if (g.r1_a) v += r1[r] * r1v;
-                    if (g.Dout) g.Dout[(int64_t)row * g.ld_dout + col] = 1.f;
                     g.C[(int64_t)row * g.ldc + col] = g.Dmul ? v * dm[r] : v;
                 }
             }
@@ -242,10 +241,10 @@ __global__ __launch_bounds__(256) void k_gemm_nt(NTArgs g) {
                 }
                 if (g.Dmul) y *= g.Dmul[(int64_t)row * g.ld_dmul + col];
                 if (g.C16) {
-                    if (g.D16) g.D16[(int64_t)row * g.ld_dout + col] = (bf16)dv;
+                    if (g.D16 && sine) g.D16[(int64_t)row * g.ld_dout + col] = (bf16)dv;
                     g.C16[(int64_t)row * g.ldc + col] = (bf16)y;
                 } else {
-                    if (g.Dout) g.Dout[(int64_t)row * g.ld_dout + col] = dv;
+                    if (g.Dout && sine) g.Dout[(int64_t)row * g.ld_dout + col] = dv;
                     g.C[(int64_t)row * g.ldc + col] = y;
                 }
             }
@@ -551,7 +550,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
                             float* pc = g.C + (int64_t)row * g.ldc + col;
                             st4(pc, f32x4{v[0], v[1], v[2], v[3]});
                             st4(pc + 4, f32x4{v[4], v[5], v[6], v[7]});
-                            if (g.Dout) {
+                            if (g.Dout && sine_cols) {
                                 float* pd = g.Dout + (int64_t)row * g.ld_dout + col;
                                 st4(pd, f32x4{d[0], d[1], d[2], d[3]});
                                 st4(pd + 4, f32x4{d[4], d[5], d[6], d[7]});
