@@ -794,51 +794,94 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(ReduceArgs g) {
 
 // Skinny weight gradient: slab[chunk][m][k] = Σ_{p in chunk} a_m(p) · B[p][k] for m < Ma
 // (a_m(p) = A[p*lda + m], plus a_Ma(p) = 1 when `ones`, i.e. the column sums of B), and
-// slab_b[chunk][m] = Σ_{p in chunk} a_m(p).  Threads own float4 column groups; the rows of a
-// chunk are split over `rph` row phases whose partials are combined through LDS.
+// slab_b[chunk][m] = Σ_{p in chunk} a_m(p).  A thread owns one 16-B column group (4 fp32 or 8
+// bf16 values of B) and walks the chunk's rows of its row phase four at a time, the four rows'
+// loads issued before their arithmetic (the rows still add in increasing order); the row phases'
+// partials are combined through LDS in phase order.
 template <int MA, typename TB>
 __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __restrict__ Bm) {
-    __shared__ float red[256 * 4];
+    constexpr int V = sizeof(TB) == 2 ? 8 : 4;     // B values per 16-B load
+    __shared__ float red[256 * V];
     const int tid = threadIdx.x;
-    const int kq = g.K >> 2;                      // float4 column groups (kq <= 256, checked on host)
-    const int rph = 256 / kq;                     // row phases
+    const int kq = g.K / V;                        // column groups (kq <= 256, checked on host)
+    const int rph = 256 / kq;                      // row phases
     const int c4 = tid % kq, ph = tid / kq;
     const bool live = ph < rph;
     const int64_t p0 = (int64_t)blockIdx.x * g.chunk;
     const int64_t p1 = min(g.P, p0 + g.chunk);
     const int Mt = g.Ma + (g.ones ? 1 : 0);
-    f32x4 acc[MA + 1];
+    float acc[MA + 1][V];
     float asum[MA];
 #pragma unroll
-    for (int m = 0; m <= MA; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m <= MA; ++m)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[m][e] = 0.f;
 #pragma unroll
     for (int m = 0; m < MA; ++m) asum[m] = 0.f;
-    if (live)
-        for (int64_t p = p0 + ph; p < p1; p += rph) {
-            const f32x4 b = ld4(Bm + p * g.ldb + 4 * c4);
-            const float* ar = g.A + p * g.lda;
+    auto load = [&](int64_t p, float (&bv)[V]) {
+        if constexpr (V == 8) {
+            unpack8(ldg16(reinterpret_cast<const bf16*>(Bm) + p * g.ldb + V * c4), bv);
+        } else {
+            const f32x4 x = ld4(reinterpret_cast<const float*>(Bm) + p * g.ldb + V * c4);
 #pragma unroll
-            for (int m = 0; m < MA; ++m)
-                if (m < g.Ma) {
-                    const float a = ar[m];
-                    acc[m] += a * b;
-                    asum[m] += a;
-                }
-            if (g.ones) acc[MA] += b;
+            for (int e = 0; e < 4; ++e) bv[e] = x[e];
         }
+    };
+    auto add = [&](int64_t p, const float (&bv)[V], const float (&av)[MA]) {
+#pragma unroll
+        for (int m = 0; m < MA; ++m)
+            if (m < g.Ma) {
+#pragma unroll
+                for (int e = 0; e < V; ++e) acc[m][e] += av[m] * bv[e];
+                asum[m] += av[m];
+            }
+        if (g.ones) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) acc[MA][e] += bv[e];
+        }
+    };
+    auto loada = [&](int64_t p, float (&av)[MA]) {
+        const float* ar = g.A + p * g.lda;
+#pragma unroll
+        for (int m = 0; m < MA; ++m) av[m] = m < g.Ma ? ar[m] : 0.f;
+    };
+    if (live) {
+        int64_t p = p0 + ph;
+        for (; p + 3 * rph < p1; p += 4 * rph) {
+            float b0[V], b1[V], b2[V], b3[V], a0[MA], a1[MA], a2[MA], a3[MA];
+            load(p, b0); load(p + rph, b1); load(p + 2 * rph, b2); load(p + 3 * rph, b3);
+            loada(p, a0); loada(p + rph, a1); loada(p + 2 * rph, a2); loada(p + 3 * rph, a3);
+            add(p, b0, a0); add(p + rph, b1, a1); add(p + 2 * rph, b2, a2); add(p + 3 * rph, b3, a3);
+        }
+        for (; p < p1; p += rph) {
+            float b0[V], a0[MA];
+            load(p, b0);
+            loada(p, a0);
+            add(p, b0, a0);
+        }
+    }
     // combine the row phases (every thread reaches every barrier)
     for (int m = 0; m < Mt; ++m) {
-        f32x4 v = acc[0];
+        const int q = m == g.Ma ? MA : m;
+        float v[V];
 #pragma unroll
-        for (int q = 0; q <= MA; ++q)
-            if (q == (m == g.Ma ? MA : m)) v = acc[q];
+        for (int e = 0; e < V; ++e) v[e] = 0.f;
+#pragma unroll
+        for (int qq = 0; qq <= MA; ++qq)
+            if (qq == q)
+#pragma unroll
+                for (int e = 0; e < V; ++e) v[e] = acc[qq][e];
         __syncthreads();
-        *reinterpret_cast<f32x4*>(red + 4 * tid) = v;
+#pragma unroll
+        for (int e = 0; e < V; ++e) red[V * tid + e] = v[e];
         __syncthreads();
         if (ph == 0) {
-            f32x4 sum = v;
-            for (int q = 1; q < rph; ++q) sum += *reinterpret_cast<const f32x4*>(red + 4 * (q * kq + c4));
-            *reinterpret_cast<f32x4*>(g.slab + ((int64_t)blockIdx.x * Mt + m) * g.K + 4 * c4) = sum;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                float sum = v[e];
+                for (int r = 1; r < rph; ++r) sum += red[V * (r * kq + c4) + e];
+                g.slab[((int64_t)blockIdx.x * Mt + m) * g.K + V * c4 + e] = sum;
+            }
         }
     }
     if (g.slab_b) {
@@ -909,6 +952,7 @@ int32_t tn_skinny(const SkinnyArgs& a0, hipStream_t s) {
     SkinnyArgs a = a0;
     SPN_ARG(a.Ma >= 1 && a.Ma <= 8 && a.K % 4 == 0 && a.K <= 1024 && a.ldb % 4 == 0, "tn_skinny: bad shape Ma=%d K=%d",
             a.Ma, a.K);
+    SPN_ARG(!a.B16 || (a.K % 8 == 0 && a.K <= 2048 && a.ldb % 8 == 0), "tn_skinny: bf16 rows need K, ldb multiples of 8");
     a.chunk = skinny_chunk(a.P);
     const int nb = cdiv(a.P, a.chunk);
     if (nb == 0) return SPNERF_OK;
