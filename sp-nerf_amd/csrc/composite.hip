@@ -3,7 +3,11 @@
 //
 // Lane l holds the EPL consecutive samples l*EPL .. l*EPL+EPL-1 (S ≤ 64*EPL); the exclusive
 // cumprod of (1-α+1e-10) is a lane-local product + a 6-step wavefront scan, the backward's
-// reversed cumsum a lane-local suffix sum + a 6-step suffix scan.  The backward follows torch
+// reversed cumsum a lane-local suffix sum + a 6-step suffix scan.  A ray's S x NO block of MLP
+// outputs is contiguous in HBM: the wave copies it into its own LDS slice with 16-B loads
+// (coalesced) and every per-sample column is read from there (a lane reading its samples' rows
+// straight from HBM walks them at a 44-56 B stride); the backward assembles the ray's d_out block
+// in LDS the same way and writes it out with 16-B stores.  The backward follows torch
 // autograd's formulas exactly where they differ from the textbook derivative: cumprod's
 // no-zero fast path  dIn_m = (Σ_{j≥m} out_j·gOut_j) / In_m  (FunctionsManual cumprod_backward),
 // clamp's inclusive pass-through mask, relu's result>0 mask, mean's division by S.
@@ -30,8 +34,9 @@ struct RayState {
 };
 
 // per-sample alpha / transparency / weights of one ray (spnerf.py:116-128)
+// rows: the ray's S x NO output block (LDS copy)
 template <int EPL>
-__device__ __forceinline__ void march(const CompArgs& a, int64_t ray, int lane, RayState<EPL>& st) {
+__device__ __forceinline__ void march(const CompArgs& a, int64_t ray, int lane, const float* rows, RayState<EPL>& st) {
     const int S = a.S;
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
@@ -44,7 +49,7 @@ __device__ __forceinline__ void march(const CompArgs& a, int64_t ray, int lane, 
         const int e = lane * EPL + j;
         if (e < S) {
             const int64_t p = ray * S + e;
-            float sg = a.out[p * a.NO + 3];
+            float sg = rows[e * a.NO + 3];
             if (a.noise) sg = sg + a.noise[p] * a.noise_std;
             const float zn = j + 1 < EPL ? st.z[j + 1] : zn0;
             const float dl = e == S - 1 ? 1e10f : zn - st.z[j];
@@ -78,29 +83,83 @@ __device__ __forceinline__ void march(const CompArgs& a, int64_t ray, int lane, 
     }
 }
 
+// the ray's contiguous S·NO floats: HBM → this wave's LDS slice, 16-B pieces when aligned, up to
+// 8 loads per lane in flight before their LDS stores
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, float* dst, int n, int lane) {
+    if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        const int nq = n >> 2;
+        for (int base = 0; base < nq; base += 512) {
+            f32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = min(base + lane + 64 * k, nq - 1);  // clamped: unconditional loads
+                v[k] = ld4(src + 4 * i);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = base + lane + 64 * k;
+                if (i < nq) reinterpret_cast<f32x4*>(dst)[i] = v[k];
+            }
+        }
+    } else {
+        for (int i = lane; i < n; i += 64) dst[i] = src[i];
+    }
+    wave_lds_sync();
+}
+
 template <int EPL>
 __global__ __launch_bounds__(256) void k_composite_fwd(CompArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sh_rows[];
     const int lane = threadIdx.x & 63;
-    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (ray >= a.B) return;
+    const int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (ray >= a.B) return;  // wave-uniform; the LDS slices are wave-private (no block barrier)
+    const int S = a.S, NO = a.NO;
+    float* rows = sh_rows + (threadIdx.x >> 6) * (S * NO);
+    if (a.weights_only) {   // σ is the only column read: stride loads of one column
+        for (int e = lane; e < S; e += 64) rows[e * NO + 3] = a.out[(ray * S + e) * NO + 3];
+        wave_lds_sync();
+    } else {
+        stage_rows(a.out + ray * (int64_t)(S * NO), rows, S * NO, lane);
+    }
     RayState<EPL> st;
-    march<EPL>(a, ray, lane, st);
-    const int S = a.S;
+    march<EPL>(a, ray, lane, rows, st);
     float dsum = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
+    float wv[EPL], tv[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
         const int e = lane * EPL + j;
+        wv[j] = st.w[j];
+        tv[j] = st.T[j];
         if (e >= S) continue;
-        const int64_t p = ray * S + e;
-        a.w[p] = st.w[j];
-        a.T[p] = st.T[j];
         dsum += st.w[j] * st.z[j];
         if (!a.weights_only) {
-            const float* o = a.out + p * a.NO;
+            const float* o = rows + e * NO;
             const float sun = o[4], om = 1.f - sun;
             c0 += (st.w[j] * o[0]) * (sun + om * o[5]);
             c1 += (st.w[j] * o[1]) * (sun + om * o[6]);
             c2 += (st.w[j] * o[2]) * (sun + om * o[7]);
+        }
+    }
+    // w, T: a lane's EPL consecutive samples as one store each
+    if (lane * EPL + EPL <= S && ((ray * S) % EPL) == 0) {
+        if constexpr (EPL == 4) {
+            *reinterpret_cast<f32x4*>(a.w + ray * S + lane * 4) = f32x4{wv[0], wv[1], wv[2], wv[3]};
+            *reinterpret_cast<f32x4*>(a.T + ray * S + lane * 4) = f32x4{tv[0], tv[1], tv[2], tv[3]};
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPL; ++j) {
+                a.w[ray * S + lane * EPL + j] = wv[j];
+                a.T[ray * S + lane * EPL + j] = tv[j];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) {
+            const int e = lane * EPL + j;
+            if (e < S) {
+                a.w[ray * S + e] = wv[j];
+                a.T[ray * S + e] = tv[j];
+            }
         }
     }
     dsum = wave_sum(dsum);
@@ -119,7 +178,7 @@ __global__ __launch_bounds__(256) void k_composite_fwd(CompArgs a) {
 #pragma unroll
         for (int j = 0; j < EPL; ++j) {
             const int e = lane * EPL + j;
-            if (e < S) s += a.out[(ray * S + e) * a.NO + a.sem_col + c];
+            if (e < S) s += rows[e * NO + a.sem_col + c];
         }
         s = wave_sum(s);
         if (lane == 0) a.sem[ray * a.n_sem + c] = s / (float)S;
@@ -128,13 +187,23 @@ __global__ __launch_bounds__(256) void k_composite_fwd(CompArgs a) {
 
 template <int EPL>
 __global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sh_rows[];
     const int lane = threadIdx.x & 63;
-    const int64_t ray = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (ray >= a.B) return;
-    RayState<EPL> st;
-    march<EPL>(a, ray, lane, st);
-    const int S = a.S;
+    const int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (ray >= a.B) return;  // wave-uniform; wave-private LDS slices
+    const int S = a.S, NO = a.NO;
+    float* rows = sh_rows + (threadIdx.x >> 6) * (2 * S * NO);
+    float* drows = rows + S * NO;   // the ray's d_out block, assembled here and stored whole
     const bool col = !a.weights_only;
+    if (col) {
+        stage_rows(a.out + ray * (int64_t)(S * NO), rows, S * NO, lane);
+    } else {
+        for (int e = lane; e < S; e += 64) rows[e * NO + 3] = a.out[(ray * S + e) * NO + 3];
+        wave_lds_sync();
+    }
+    for (int i = lane; i < S * NO; i += 64) drows[i] = 0.f;
+    RayState<EPL> st;
+    march<EPL>(a, ray, lane, rows, st);
     // clamp mask of rgb = clamp(Σ w·albedo·irr, 0, 1) (recomputed pre-clamp value)
     float gp[3] = {0.f, 0.f, 0.f};
     if (col && a.g_rgb) {
@@ -143,7 +212,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
         for (int j = 0; j < EPL; ++j) {
             const int e = lane * EPL + j;
             if (e >= S) continue;
-            const float* o = a.out + (ray * S + e) * a.NO;
+            const float* o = rows + e * NO;
             const float sun = o[4], om = 1.f - sun;
             for (int q = 0; q < 3; ++q) c[q] += (st.w[j] * o[q]) * (sun + om * o[5 + q]);
         }
@@ -155,6 +224,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
     }
     const float gd = a.g_depth ? a.g_depth[ray] : 0.f;
     float dal[EPL], q[EPL];
+    wave_lds_sync();   // the zero fill of drows is complete
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
         const int e = lane * EPL + j;
@@ -162,10 +232,10 @@ __global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
         q[j] = 0.f;
         if (e >= S) continue;
         const int64_t p = ray * S + e;
-        float* dO = a.d_out + p * a.NO;
+        float* dO = drows + e * NO;
         float dw = gd * st.z[j] + (a.g_w ? a.g_w[p] : 0.f);
         if (col) {
-            const float* o = a.out + p * a.NO;
+            const float* o = rows + e * NO;
             const float sun = o[4], om = 1.f - sun;
             float dsun = 0.f, dsun2 = 0.f;
             for (int c = 0; c < 3; ++c) {
@@ -180,10 +250,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
                 dO[5 + c] = dirr * om;
             }
             dO[4] = dsun - dsun2;
-        } else {
-            dO[0] = dO[1] = dO[2] = dO[4] = dO[5] = dO[6] = dO[7] = 0.f;
         }
-        for (int c = 8; c < a.NO; ++c) dO[c] = 0.f;
         if (col && a.g_sem)
             for (int c = 0; c < a.n_sem; ++c) dO[a.sem_col + c] = a.g_sem[ray * a.n_sem + c] / (float)S;
         const float dT = dw * st.al[j] + (a.g_T ? a.g_T[p] : 0.f);
@@ -214,15 +281,27 @@ __global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
         const float da = dal[j] - dt;
         const float dX = (-da) * st.E[j];
         const float dr = dX * (-st.dl[j]);
-        a.d_out[(ray * S + e) * a.NO + 3] = st.r[j] > 0.f ? dr : 0.f;
+        drows[e * NO + 3] = st.r[j] > 0.f ? dr : 0.f;
+    }
+    wave_lds_sync();
+    float* dst = a.d_out + ray * (int64_t)(S * NO);
+    const int n = S * NO;
+    if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (int i = lane; i < n / 4; i += 64) reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(drows)[i];
+    } else {
+        for (int i = lane; i < n; i += 64) dst[i] = drows[i];
     }
 }
 
 template <int EPL>
 static int32_t launch_comp(const CompArgs& a, bool fwd, hipStream_t s) {
-    const dim3 grid((unsigned)((a.B + 3) / 4)), block(256);
-    if (fwd) hipLaunchKernelGGL(k_composite_fwd<EPL>, grid, block, 0, s, a);
-    else hipLaunchKernelGGL(k_composite_bwd<EPL>, grid, block, 0, s, a);
+    // 4 waves (rays) per block, fewer when their LDS row blocks would not fit
+    const size_t per_wave = (size_t)(fwd ? 1 : 2) * a.S * a.NO * sizeof(float);
+    const int wpb = per_wave * 4 <= 64 * 1024 ? 4 : 1;
+    const dim3 grid((unsigned)((a.B + wpb - 1) / wpb)), block(64 * wpb);
+    const size_t lds = per_wave * wpb;
+    if (fwd) hipLaunchKernelGGL(k_composite_fwd<EPL>, grid, block, lds, s, a);
+    else hipLaunchKernelGGL(k_composite_bwd<EPL>, grid, block, lds, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
@@ -230,6 +309,8 @@ static int32_t launch_comp(const CompArgs& a, bool fwd, hipStream_t s) {
 static int32_t run_comp(const CompArgs& a, bool fwd, hipStream_t s) {
     SPN_ARG(a.S > 0 && a.S <= 256, "composite: n_samples %d must be in [1, 256]", a.S);
     SPN_ARG(a.NO >= 8 && a.sem_col + a.n_sem <= a.NO, "composite: bad output layout");
+    SPN_ARG((size_t)2 * a.S * a.NO * sizeof(float) <= 64 * 1024, "composite: n_samples x n_out = %d x %d too large", a.S,
+            a.NO);
     if (a.B == 0) return SPNERF_OK;
     const double P = (double)a.B * a.S;
     ProfScope prof(fwd ? "composite_fwd" : "composite_bwd", s, 0.0,
