@@ -158,13 +158,15 @@ def cpu_baseline(c, seconds: float, batch: int):
                       f"CPU, fp32, {threads} threads = the CPUs this job may use)"}
 
 
-def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int = 3, dev="cuda:0"):
-    """BASELINE.json's second metric, PSNR vs the reference: the HIP path (fp32) and the oracle
-    (the reference's render path restated on the CPU, oracle/ref_cpu.py, pinned to its golden
-    fixtures) train the same SPNeRF (W=512, config-2 flags, Adam lr 5e-4) from the same init on
-    the same ray batches and random draws of the synthetic JAX_269-camera scene (JAX_214 data is
-    not in the container), then render the same held-out rays.  Returns both PSNRs and their
-    difference (the north star asks for |delta| <= 0.05 dB)."""
+def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int = 3, dev="cuda:0",
+                precision: str = "fp32"):
+    """BASELINE.json's second metric, PSNR vs the reference: the HIP path (``precision`` MLP)
+    and the oracle (the reference's render path restated on the CPU in fp32, oracle/ref_cpu.py,
+    pinned to its golden fixtures) train the same SPNeRF (W=512, config-2 flags, Adam lr 5e-4)
+    from the same init on the same ray batches and random draws of the JAX_269-camera scene at
+    img_downscale 4 against the REAL JAX_269 images (JAX_214 is not in the container), then
+    render the same held-out rays.  Returns both PSNRs and their difference (the north star
+    asks for |delta| <= 0.05 dB)."""
     import numpy as np
     from oracle import ref_cpu
     from oracle.weights import ModelDims, make_weights
@@ -173,7 +175,7 @@ def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
     dims = ModelDims(width=512)
     w = make_weights(dims, seed)
-    model = spnerf_amd.SPNeRF(feat=512, mapping=True).to(dev)
+    model = spnerf_amd.SPNeRF(feat=512, mapping=True, precision=precision).to(dev)
     model.load_state_dict({k: torch.tensor(v) for k, v in w.items()})
     p = ref_cpu.to_params(w, requires_grad=True)
     opt_g = torch.optim.Adam(model.parameters(), lr=5e-4)
@@ -217,11 +219,12 @@ def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int
         ec = ref_cpu.render_rays(p, dims, args, rays[idx], None, None, "test", draw=ref_cpu_replay(dr))["rgb_coarse"]
     pg = psnr(float(torch.mean((eg - rgbs[idx]) ** 2)))
     pc = psnr(float(torch.mean((ec - rgbs[idx]) ** 2)))
-    return {"psnr_gpu_db": pg, "psnr_cpu_reference_db": pc, "delta_db": pg - pc, "steps": steps, "batch_rays": batch,
-            "held_out_rays": n_eval, "loss_first_last": [losses[0], losses[-1]],
+    return {"psnr_gpu_db": pg, "psnr_cpu_reference_db": pc, "delta_db": pg - pc, "gpu_mlp": precision, "steps": steps,
+            "batch_rays": batch, "held_out_rays": n_eval, "loss_first_last": [losses[0], losses[-1]],
             "max_train_loss_rel_diff": max(abs(a - b) / max(abs(b), 1e-12) for a, b in losses),
+            "targets": scene.rgb_source,
             "setup": "W=512 config-2 flags, same init (oracle/weights.py seed 3), same batches and draws, Adam lr 5e-4; "
-                     "synthetic JAX_269-camera scene (JAX_214 absent); CPU side = oracle/ref_cpu.py"}
+                     "JAX_269 cameras at img_downscale 4 (JAX_214 absent); CPU side = oracle/ref_cpu.py (fp32)"}
 
 
 def ref_cpu_replay(draws):
@@ -607,7 +610,8 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": c["precision"],
-        "data": "synthetic targets on real JAX_269 RPC camera rays (JAX_214 proxy, resident in HBM), seeded-random SPNeRF init",
+        "data": f"{scene.rgb_source} colour targets, synthetic depth priors / labels, on real JAX_269 RPC camera rays "
+                "(JAX_214 proxy, resident in HBM), seeded-random SPNeRF init",
         "config": {"workload": c["workload"], "global_batch": B * world, "rays_per_rank": B,
                    "samples_per_ray": s_final, "parallelism": f"dp{world}"},
         "roofline": roofline_of(dom, nt, traffic, traffic_src),
@@ -620,8 +624,8 @@ def run_train(a, config, rank, world, dev, secondary=False):
     del graph
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not secondary:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or B)
-        if config == "c2":
-            out["psnr_parity"] = psnr_parity(dev=dev)
+        if config in ("c2", "c4"):
+            out["psnr_parity"] = {p: psnr_parity(dev=dev, precision=p) for p in ("fp32", "bf16")}
     return out
 
 

@@ -8,15 +8,19 @@ datasets/satellite_scene.py) at the requested ``img_downscale``, in the dataset'
 (images concatenated, pixels row-major; satellite_scene.py:186-221).  The JSONs carry
 sun_elevation = sun_azimuth = 0, hence sun_d = (0, 1, 0).
 
-Targets are synthetic (no GeoTIFF I/O on the GPU box): a smooth albedo field of the ray's
-ground point; depth priors valid on ~68 % of the rays (JAX_269's 2D-point coverage
-438,256 / 644,709) with GT depth far·U(0.3, 0.7) and std (1-corr)·0.05+1e-4; semantic labels
-{0, 1, 2, -100} with fixed frequencies.
+Colour targets: at img_downscale 4 the REAL JAX_269 images (data/jax269_rgb_ds4.npz, made from
+the reference's GeoTIFFs by tools/make_rgb_targets.py the way its dataset downsamples them,
+satellite_scene.py:71-86); at other scales (no GeoTIFF I/O on the GPU box) a smooth synthetic
+albedo field of the ray's ground point.  Depth priors valid on ~68 % of the rays (JAX_269's
+2D-point coverage 438,256 / 644,709) with GT depth far·U(0.3, 0.7) and std (1-corr)·0.05+1e-4;
+semantic labels {0, 1, 2, -100} with fixed frequencies.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from .satellite import image_rays, load_cameras
@@ -33,10 +37,22 @@ class Scene:
     depth_std: torch.Tensor   # (N,)
     sems: torch.Tensor        # (N,) int64 in {0, 1, 2, -100}
     view_sizes: list
+    rgb_source: str = "synthetic"
 
     def to(self, device):
         return Scene(*(getattr(self, f).to(device) for f in ("rays", "rgbs", "depths", "valid_depth", "depth_std", "sems")),
-                     self.view_sizes)
+                     self.view_sizes, self.rgb_source)
+
+
+def real_rgbs(views, img_downscale: float):
+    """The views' real pixels (N, 3) in the rays' order, or None when not shipped at this scale."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", f"jax269_rgb_ds{int(img_downscale)}.npz")
+    if img_downscale != int(img_downscale) or not os.path.exists(path):
+        return None
+    with np.load(path, allow_pickle=False) as z:
+        if not all(v in z.files for v in views):
+            return None
+        return torch.tensor(np.concatenate([z[v] for v in views]))
 
 
 def synthetic_scene(img_downscale: float = 4.0, views=VIEWS, seed: int = 0, device="cuda") -> Scene:
@@ -49,10 +65,16 @@ def synthetic_scene(img_downscale: float = 4.0, views=VIEWS, seed: int = 0, devi
     rays = torch.cat(rays)
     n = rays.shape[0]
     g = torch.Generator(device="cpu").manual_seed(seed)
-    mid = rays[:, 0:3] + 0.5 * rays[:, 7:8] * rays[:, 3:6]
-    gx, gy = mid[:, 0] + mid[:, 2], mid[:, 1]
-    rgbs = torch.stack([0.45 + 0.3 * torch.sin(9 * gx), 0.5 + 0.25 * torch.cos(7 * gy), 0.4 + 0.2 * torch.sin(5 * (gx + gy))],
-                       1).clamp(0, 1)
+    rgbs = real_rgbs(views, img_downscale)
+    source = "real JAX_269 RGB" if rgbs is not None else "synthetic"
+    if rgbs is not None:
+        assert rgbs.shape[0] == n, (rgbs.shape, n)
+        rgbs = rgbs.to(rays.device)
+    else:
+        mid = rays[:, 0:3] + 0.5 * rays[:, 7:8] * rays[:, 3:6]
+        gx, gy = mid[:, 0] + mid[:, 2], mid[:, 1]
+        rgbs = torch.stack([0.45 + 0.3 * torch.sin(9 * gx), 0.5 + 0.25 * torch.cos(7 * gy),
+                            0.4 + 0.2 * torch.sin(5 * (gx + gy))], 1).clamp(0, 1)
     valid = (torch.rand(n, generator=g) < 438256 / 644709).long()
     gt = rays[:, 7].cpu() * (0.3 + 0.4 * torch.rand(n, generator=g))
     corr = 0.2 + 0.8 * torch.rand(n, generator=g)
@@ -61,4 +83,4 @@ def synthetic_scene(img_downscale: float = 4.0, views=VIEWS, seed: int = 0, devi
     sems = torch.where(sems == 3, torch.full_like(sems, -100), sems)
     dev = rays.device
     return Scene(rays, rgbs.float(), torch.stack([gt, corr], 1).float().to(dev), valid.to(dev), std.float().to(dev),
-                 sems.to(dev), sizes)
+                 sems.to(dev), sizes, source)

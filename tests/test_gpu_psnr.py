@@ -1,8 +1,8 @@
 """Training parity in PSNR (BASELINE.json metric "PSNR vs ref", north star: within 0.05 dB) —
 needs an MI355X.  The HIP path and the pinned CPU restatement of the reference train the same
 network from the same init on the same batches and draws, then render the same held-out rays
-(bench.psnr_parity; JAX_214 images are not available, so the scene is the synthetic
-JAX_269-camera one)."""
+(bench.psnr_parity: the JAX_269 cameras at img_downscale 4 with the real JAX_269 images as
+targets; JAX_214 is not available), for the fp32 MLP and for the bf16 MLP of configs 3-5."""
 import os
 import sys
 
@@ -12,9 +12,11 @@ pytestmark = pytest.mark.gpu
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def test_training_psnr_matches_cpu_reference():
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_training_psnr_matches_cpu_reference(precision):
     import bench
-    r = bench.psnr_parity(steps=20, batch=128, n_eval=512)
+    r = bench.psnr_parity(steps=20, batch=128, n_eval=512, precision=precision)
     print(r)
+    assert r["targets"] == "real JAX_269 RGB"
     assert r["loss_first_last"][-1][0] < r["loss_first_last"][0][0]  # it trains
     assert abs(r["delta_db"]) <= 0.05, r
