@@ -243,13 +243,15 @@ def measured_traffic(config, kernel_class):
     (tools/pmc_bench.sh + tools/traffic_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
     bytes = 2*FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md's gfx950 correction).  PMC
     counters cannot be read from inside the bench process, hence the profile file."""
-    path = os.path.join(ROOT, "profiles", "r01", f"traffic_{config}.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)[kernel_class]
-        return t["hbm_bytes_per_launch"], f"profiles/r01/traffic_{config}.json ({t['launches']} launches)"
-    except (OSError, KeyError, ValueError):
-        return None, None
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, f"traffic_{config}.json")
+        try:
+            with open(path) as f:
+                t = json.load(f)[kernel_class]
+            return t["hbm_bytes_per_launch"], f"profiles/{rnd}/traffic_{config}.json ({t['launches']} launches)"
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 
@@ -351,7 +353,7 @@ def run_inference(a, c, rank, world, dev):
         "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": c["n_samples"],
                    "parallelism": f"ray-shard{world}", "image_rays": h * w},
         "image_seconds_projected": h * w * c["n_samples"] / value,
-        "roofline": roofline_of(dom, nt),
+        "roofline": roofline_of(dom, nt, *measured_traffic(a.config, dom)),
         "mlp_gemms": gemm_totals(a.steps),
         "finite": bool(torch.isfinite(res["rgb_coarse"]).all()),
     }

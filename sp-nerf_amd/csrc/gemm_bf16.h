@@ -22,6 +22,7 @@ struct NT16Args {
     int act = 0; float w0 = 1.f; int n_lin = 0;
     bf16* Dout = nullptr; int ld_dout = 0;
     const bf16* Dmul = nullptr; int ld_dmul = 0;
+    int k_alg = 0;  // algorithmic K for the FLOP count (0 = K; the hi/lo layer-0 GEMM: K0p of its K = 4·K0p)
 };
 
 // slab[s][n][k] = Σ_{p in split s} A[p][n] · B[p][k] (B split along k at K1),

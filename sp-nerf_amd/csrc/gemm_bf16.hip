@@ -931,7 +931,7 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     const int ntiles = cdiv(a.M, HB) * cdiv(a.N, HB);
     // algorithmic bytes: A and B once, C, the derivative of the sine columns, the Dmul read
     const double dcols = (a.Dout && a.act == 1) ? (double)(a.N - std::min(a.n_lin, a.N)) : 0.0;
-    ProfScope prof("gemm_nt_bf16", s, 2.0 * a.M * a.N * a.K,
+    ProfScope prof("gemm_nt_bf16", s, 2.0 * a.M * a.N * (a.k_alg > 0 ? a.k_alg : a.K),
                    2.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N * (1.0 + (a.Dmul ? 1.0 : 0.0)) +
                           (double)a.M * dcols));
     // variants: 1 / 2 = one block per tile, prefetch depth 1 / 2; 3 / 4 = persistent grid of

@@ -1042,7 +1042,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
                 a.bias[l] = c.pk(c.k.bt[l]);
                 a.Hs[l] = save ? c.hb(c.w.Hb[l]) : (l == d.L - 1 ? c.hb(c.w.Hb[l & 1]) : nullptr);
                 a.Ds[l] = save ? c.hb(c.w.Db[l]) : nullptr;
-                ksum += l == 0 ? 4 * d.K0p : c.k.Kp[l];
+                ksum += l == 0 ? d.K0p : c.k.Kp[l];   // algorithmic K (layer 0 runs 4·K0p on hi/lo planes)
             }
             a.rb_skip = d.sem ? c.at(c.w.rb4) : nullptr;
             a.P = P; a.S = S; a.L = d.L; a.skip = d.skip; a.K0p = d.K0p;
@@ -1070,6 +1070,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
             if (rb) { g.rowbias = rb; g.ld_rb = W; g.rows_per_ray = S; }
             g.act = 1; g.w0 = 30.f; g.n_lin = 0;
             if (save) { g.Dout = reinterpret_cast<bf16*>(dd); g.ld_dout = W; }
+            g.k_alg = d.K0p;   // FLOPs counted at the layer's own K (the split's 4x MFMA work is overhead)
             SPN_TRY(gemm_nt_bf16(g, s));
         } else if (i == 0) {
             NTArgs g;

@@ -1,7 +1,7 @@
 """Per-launch HBM traffic of the GEMM classes from tools/pmc_bench.sh output, with the gfx950
 correction of MI355X_MICROARCH.md §HBM: bytes = 2 × FETCH_SIZE + WRITE_SIZE (both in KiB).
-Writes profiles/r01/traffic_<cfg>.json for bench.py's roofline.traffic.
-    python tools/traffic_summary.py gpurun_out/pmc_bench profiles/r01"""
+Writes <dst>/traffic_<cfg>.json for bench.py's roofline.traffic.
+    python tools/traffic_summary.py gpurun_out/pmc_bench profiles/r02 c4 c5"""
 import collections
 import csv
 import glob
@@ -10,10 +10,11 @@ import os
 import sys
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_bench"
-dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01"
+dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r02"
+CFGS = sys.argv[3:] or ["c4", "c5"]
 CLASSES = {"k_gemm_nt<": "gemm_nt_f32", "k_gemm_nt_w<": "gemm_nt_f32", "k_gemm_tn<": "gemm_tn_f32",
            "k_gemm_nt_bf16": "gemm_nt_bf16", "k_gemm_tn_bf16": "gemm_tn_bf16", "k_trunk_bf16": "trunk_bf16"}
-for cfg in ("c2", "c3"):
+for cfg in CFGS:
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         for f in glob.glob(os.path.join(src, f"{cfg}_{ctr}", "**", "*counter_collection.csv"), recursive=True):
@@ -36,7 +37,7 @@ for cfg in ("c2", "c3"):
         out[cls] = {"launches": len(c["FETCH_SIZE"]), "hbm_read_bytes_per_launch": fetch,
                     "hbm_write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
                     "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over `bench.py --config "
-                              f"{cfg} --eager --steps 3 --warmup 1`; bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB, gfx950 "
+                              f"{cfg} --eager --steps 2 --warmup 1`; bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB, gfx950 "
                               "correction, MI355X_MICROARCH.md HBM)"}
     if out:
         os.makedirs(dst, exist_ok=True)
