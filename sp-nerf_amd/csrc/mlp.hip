@@ -289,6 +289,48 @@ __global__ __launch_bounds__(256) void k_heads_fwd(HeadsArgs<T> a, PackedOffs k)
 }
 
 int g_heads_variant = 1;  // 0 = the one-point-at-a-time k_heads_fwd (ablation)
+// backward: 2 = weight gradients on a second stream beside the dX chain; 1 = one stream (default:
+// measured on MI355X, the two streams' GEMMs contend for HBM / L2 and the step got 3% slower,
+// in eager mode and as a captured graph alike — C4 at 512 rays 4.99 -> 5.15 ms)
+int g_bwd_streams = 1;
+
+// The backward's second stream: the weight-gradient GEMMs, their slab reductions and the per-ray
+// parameter sums run there, beside the dX chain on the caller's stream, joined by events
+// (fork: main → side after an input is produced; join: side → main at the end, so the caller
+// sees the usual stream order).  Inside a captured HIP graph the same calls record a fork/join
+// graph.  One library-owned non-blocking stream and an event ring per device.
+namespace {
+struct Side {
+    hipStream_t s = nullptr;
+    hipEvent_t ev[64] = {};
+    int next = 0;
+    bool ok = false;
+};
+Side g_side[64];
+
+Side* side_stream() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    Side& sd = g_side[dev];
+    if (!sd.ok) {
+        if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        for (auto& e : sd.ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        sd.ok = true;
+    }
+    return &sd;
+}
+
+// `to` waits for everything issued so far on `from`
+int32_t stream_dep(Side* sd, hipStream_t from, hipStream_t to) {
+    if (!sd || from == to) return SPNERF_OK;
+    hipEvent_t e = sd->ev[sd->next];
+    sd->next = (sd->next + 1) % 64;
+    SPN_HIP(hipEventRecord(e, from));
+    SPN_HIP(hipStreamWaitEvent(to, e, 0));
+    return SPNERF_OK;
+}
+}  // namespace
 int g_l0_split = 1;       // bf16 MLP: fc_net.0 on bf16 hi/lo planes (0 = fp32 MFMA GEMM)
 int g_trunk_l0 = 1;       // ... and inside the fused trunk launch: 1 = when nothing is saved (inference;
                           // saving, 64-point tiles, it measured slower than the separate GEMM), 2 = always
@@ -1245,7 +1287,7 @@ static int32_t ray_rowsum(const T* in, int ld, int c0, int N, int S, int64_t n_r
 // sin' as Dmul, and the per-ray sums R0 / R4 / RQ feeding the per-ray parameters.
 template <typename T>
 static int32_t backward_points(const Ctx& c, int mode, const float* packed, const float* d_out, int64_t n_rays,
-                               float* grad, hipStream_t s) {
+                               float* grad, hipStream_t s, hipStream_t s2, Side* sd) {
     using G = Gemms<T>;
     using NT = typename G::NT;
     constexpr bool BF = std::is_same<T, bf16>::value;
@@ -1281,86 +1323,106 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         else hipLaunchKernelGGL(k_heads_bwd<T>, dim3(grid), dim3(256), 0, s, a, (PackedOffs)c.k);
         SPN_HIP(hipGetLastError());
     }
+    // from here on: dX chain on s, weight gradients on s2 (each after a fork from s)
+    SPN_TRY(stream_dep(sd, s, s2));
     // 2. narrow-head weights: reductions over points
-    SPN_TRY(skinny(c, P, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), W, 0, gp(x.sigb), nullptr, s));
-    SPN_TRY(skinny(c, P, hpre + 4, d.HP, 1, buf(c.w.S3), H, H, gp(x.s4W), H, 0, gp(x.s4b), nullptr, s));
+    SPN_TRY(skinny(c, P, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), W, 0, gp(x.sigb), nullptr, s2));
+    SPN_TRY(skinny(c, P, hpre + 4, d.HP, 1, buf(c.w.S3), H, H, gp(x.s4W), H, 0, gp(x.s4b), nullptr, s2));
     if (mode == 0) {
-        SPN_TRY(skinny(c, P, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), H, 0, gp(x.r2b), nullptr, s));
-        if (d.beta) SPN_TRY(skinny(c, P, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), H, 0, gp(x.b2b), nullptr, s));
-        if (d.sem) SPN_TRY(skinny(c, P, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), H, 0, gp(x.m2b), nullptr, s));
+        SPN_TRY(skinny(c, P, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), H, 0, gp(x.r2b), nullptr, s2));
+        if (d.beta) SPN_TRY(skinny(c, P, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), H, 0, gp(x.b2b), nullptr, s2));
+        if (d.sem) SPN_TRY(skinny(c, P, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), H, 0, gp(x.m2b), nullptr, s2));
     }
     // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
     {
+        SPN_TRY(tn_grad<T>(c, dS3, H, H, buf(c.w.S2), H, nullptr, 0, H, H, s2, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}));
         NT g;
         g.A = dS3; g.lda = H; g.K1 = H; g.B = G::w(c, c.k.Ws3T, c.k.Ws3T16); g.ldb = H; g.C = dS2; g.ldc = H;
         g.M = (int)P; g.N = H; g.K = H; g.Dmul = buf(c.w.DS2); g.ld_dmul = H;
         SPN_TRY(G::nt(g, s));
-        SPN_TRY(tn_grad<T>(c, dS3, H, H, buf(c.w.S2), H, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}));
+        SPN_TRY(stream_dep(sd, s, s2));
+        SPN_TRY(tn_grad<T>(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s2, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
         NT g2 = g;
         g2.A = dS2; g2.B = G::w(c, c.k.Ws2T, c.k.Ws2T16); g2.C = dZQ; g2.ldc = d.NQ; g2.Dmul = buf(c.w.DQ); g2.ld_dmul = d.NQ;
         SPN_TRY(G::nt(g2, s));
-        SPN_TRY(tn_grad<T>(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
+        SPN_TRY(stream_dep(sd, s, s2));
     }
     // 4. feat: dF = dZ_Q · WQ → dZG[:, :W];  dWQ = dZ_Q^T · feat
     const int NQ = mode == 0 ? d.NQ : H;
     {
+        if (mode == 0) {
+            if (d.beta)
+                SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, NQ, Gb, d.NG, nullptr, 0, W, W, s2,
+                                   {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b)),
+                                    red(2 * H, H, W, gp(x.b1W), ld(x.b1W), gp(x.b1b))}));
+            else
+                SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, NQ, Gb, d.NG, nullptr, 0, W, W, s2,
+                                   {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b))}));
+        } else {
+            SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s2, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
+        }
+        // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns
+        SPN_TRY(ray_rowsum<T>(dZQ, d.NQ, 0, NQ, S, n_rays, c.at(c.w.RQ), d.NQ, s2));
         NT g;
         g.A = dZQ; g.lda = d.NQ; g.K1 = NQ; g.B = G::w(c, c.k.WQT, c.k.WQT16); g.ldb = d.NQ; g.C = dZG; g.ldc = d.NG;
         g.M = (int)P; g.N = W; g.K = NQ;
         SPN_TRY(G::nt(g, s));
-        if (mode == 0) {
-            if (d.beta)
-                SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, NQ, Gb, d.NG, nullptr, 0, W, W, s,
-                                   {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b)),
-                                    red(2 * H, H, W, gp(x.b1W), ld(x.b1W), gp(x.b1b))}));
-            else
-                SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, NQ, Gb, d.NG, nullptr, 0, W, W, s,
-                                   {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b))}));
-        } else {
-            SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
-        }
-        // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns
-        SPN_TRY(ray_rowsum<T>(dZQ, d.NQ, 0, NQ, S, n_rays, c.at(c.w.RQ), d.NQ, s));
+        SPN_TRY(stream_dep(sd, s, s2));
     }
     // 5. H_L: dH_L = dZ_G · WG + dσ ⊗ w_σ ;  dZ_{L-1} = dH_L ⊙ D_L ;  dWG = dZ_G^T · H_L
     const int NG = mode == 0 ? d.NG : W;
-    T* dZ = buf(c.w.dZa);
-    T* dZn = buf(c.w.dZb);
+    // trunk dZ buffers in rotation: the dX GEMM of layer i writes the buffer whose dZ_{i+2} the
+    // side stream's weight gradient of layer i+2 read (it waits for that, not for layer i+1's)
+    T* dzb[3] = {buf(c.w.dZa), buf(c.w.dZb), buf(c.w.dZc)};
+    std::vector<hipEvent_t> tn_done(d.L + 2, nullptr);
+    int cur = 0;
+    T* dZ = dzb[cur];
     {
+        if (mode == 0 && d.sem)
+            SPN_TRY(tn_grad<T>(c, dZG, d.NG, d.NG, HL, W, nullptr, 0, W, W, s2,
+                               {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
+        else
+            SPN_TRY(tn_grad<T>(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s2, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
         NT g;
         g.A = dZG; g.lda = d.NG; g.K1 = NG; g.B = G::w(c, c.k.WGT, c.k.WGT16); g.ldb = d.NG; g.C = dZ; g.ldc = W;
         g.M = (int)P; g.N = W; g.K = NG;
         g.r1_a = hpre; g.r1_lda = d.HP; g.r1_v = c.pk(c.k.wsig);
         g.Dmul = buf(c.w.Db[d.L - 1]); g.ld_dmul = W;
         SPN_TRY(G::nt(g, s));
-        if (mode == 0 && d.sem)
-            SPN_TRY(tn_grad<T>(c, dZG, d.NG, d.NG, HL, W, nullptr, 0, W, W, s,
-                               {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
-        else
-            SPN_TRY(tn_grad<T>(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
+        SPN_TRY(stream_dep(sd, s, s2));
     }
     // 6. trunk, top to bottom
     const T* X0 = BF ? buf(c.w.X0b) : buf(c.w.X0);
     for (int i = d.L - 1; i >= 0; --i) {
-        // dZ holds dL/d(pre-activation of layer i)
+        // dZ (buffer cur) holds dL/d(pre-activation of layer i); the side stream has it
         const T* In = i == 0 ? X0 : buf(c.w.Hb[i - 1]);
         const int ldin = i == 0 ? d.K0p : W;
         const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
         if (i == d.skip)
-            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, W, X0, d.K0p, W, W + d.K0p, s,
+            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, W, X0, d.K0p, W, W + d.K0p, s2,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
         else
-            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s,
+            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s2,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
         if (d.sem && (i == 0 || i == d.skip)) {
-            SPN_TRY(ray_rowsum<T>(dZ, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s));
+            SPN_TRY(ray_rowsum<T>(dZ, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
+        }
+        if (sd && s2 != s) {   // this layer's reads of buffer `cur` are issued on s2
+            tn_done[i] = sd->ev[sd->next];
+            sd->next = (sd->next + 1) % 64;
+            SPN_HIP(hipEventRecord(tn_done[i], s2));
         }
         if (i > 0) {
+            const int nxt = (cur + 1) % 3;
+            // buffer nxt last held dZ_{i+2}: its weight gradient (layer i+2) must be done
+            if (i + 2 <= d.L - 1 && tn_done[i + 2]) SPN_HIP(hipStreamWaitEvent(s, tn_done[i + 2], 0));
             NT g;
-            g.A = dZ; g.lda = W; g.K1 = W; g.B = G::w(c, c.k.WTt[i], BF ? c.k.WTt16[i] : -1); g.ldb = W; g.C = dZn; g.ldc = W;
-            g.M = (int)P; g.N = W; g.K = W; g.Dmul = buf(c.w.Db[i - 1]); g.ld_dmul = W;
+            g.A = dZ; g.lda = W; g.K1 = W; g.B = G::w(c, c.k.WTt[i], BF ? c.k.WTt16[i] : -1); g.ldb = W; g.C = dzb[nxt];
+            g.ldc = W; g.M = (int)P; g.N = W; g.K = W; g.Dmul = buf(c.w.Db[i - 1]); g.ld_dmul = W;
             SPN_TRY(G::nt(g, s));
-            std::swap(dZ, dZn);
+            SPN_TRY(stream_dep(sd, s, s2));
+            cur = nxt;
+            dZ = dzb[cur];
         }
     }
     return SPNERF_OK;
@@ -1384,8 +1446,13 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
     if (P == 0) return SPNERF_OK;
     auto gp = [&](int pi) { return grad + specs[pi].off; };
     auto ld = [&](int pi) { return (int)specs[pi].ld(); };
-    if (d.bf) SPN_TRY(backward_points<bf16>(c, mode, packed, d_out, n_rays, grad, s));
-    else SPN_TRY(backward_points<float>(c, mode, packed, d_out, n_rays, grad, s));
+    Side* sd = g_bwd_streams >= 2 ? side_stream() : nullptr;
+    hipStream_t s2 = sd ? sd->s : s;
+    if (d.bf) SPN_TRY(backward_points<bf16>(c, mode, packed, d_out, n_rays, grad, s, s2, sd));
+    else SPN_TRY(backward_points<float>(c, mode, packed, d_out, n_rays, grad, s, s2, sd));
+    SPN_TRY(stream_dep(sd, s, s2));   // step 7 reads d_out and the workspace written on s
+    const hipStream_t s_main = s;
+    s = s2;                           // step 7 (per-ray parameters) runs on the side stream
     // 7. per-ray parameters: sun-direction columns, t columns, sky MLP, semantic embedding
     {
         const int sky_on = mode == 0;
@@ -1420,6 +1487,7 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
             SPN_HIP(hipGetLastError());
         }
     }
+    SPN_TRY(stream_dep(sd, s2, s_main));  // join: the caller's stream sees every gradient
     return SPNERF_OK;
 }
 
@@ -1442,6 +1510,7 @@ static int* option_slot(const char* name) {
     if (n == "heads_variant") return &g_heads_variant;
     if (n == "l0_split") return &g_l0_split;
     if (n == "trunk_l0") return &g_trunk_l0;
+    if (n == "bwd_streams") return &g_bwd_streams;
     return nullptr;
 }
 

@@ -215,8 +215,9 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         w.dZQ = act(P * d.NQ);
         w.dS3 = act(P * H);
         w.dS2 = act(P * H);
-        w.dZa = act(P * W);
-        w.dZb = act(P * W);
+        w.dZa = act(P * W);   // trunk dZ: three buffers in rotation, so the weight gradient of
+        w.dZb = act(P * W);   // layer i (side stream) reads dZ_i while the main stream writes
+        w.dZc = act(P * W);   // dZ_{i-1} into another
         w.hpre = take(P * d.HP);
         // largest TN slab over every weight-gradient GEMM of the backward
         int64_t slab = 0, slab_b = 0;

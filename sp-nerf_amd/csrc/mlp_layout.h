@@ -67,7 +67,7 @@ Packed packed_layout(const Dims& d);
 
 // Workspace offsets (floats).  SAVE keeps every activation + derivative for the backward.
 // With Dims::bf the activation / derivative / pre-activation-gradient buffers (Hb, Db, G, DG,
-// Q, DQ, S2, DS2, S3, DS3, dZG, dZQ, dS3, dS2, dZa, dZb, X0b) hold bf16 at the same float offset.
+// Q, DQ, S2, DS2, S3, DS3, dZG, dZQ, dS3, dS2, dZa, dZb, dZc, X0b) hold bf16 at the same float offset.
 struct WS {
     int64_t P, B;
     int64_t X0, X0b;
@@ -76,7 +76,7 @@ struct WS {
     int64_t G, DG, Q, DQ, S2, DS2, S3, DS3, hsave;
     int64_t rb0, rb4, rbQ, skyh, sky;
     // backward
-    int64_t dZG, dZQ, dS3, dS2, dZa, dZb, hpre, slab, slab_b, RQ, R0, R4, dsky, skyd, skydh, gemb, embr, sk_slab, sk_slab_b;
+    int64_t dZG, dZQ, dS3, dS2, dZa, dZb, dZc, hpre, slab, slab_b, RQ, R0, R4, dsky, skyd, skydh, gemb, embr, sk_slab, sk_slab_b;
     int64_t total;
 };
 WS ws_layout(const Dims& d, int64_t n_rays, int32_t n_samples, int32_t flags);
