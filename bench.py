@@ -49,7 +49,8 @@ GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt_w (fp32 MFMA, 256x128 persistent tile
                 "gemm_tn_f32": ("k_gemm_tn (fp32 MFMA, weight gradients)", FP32_MFMA_PEAK_TFLOPS),
                 "gemm_nt_bf16": ("k_gemm_nt_bf16w (bf16 MFMA, 256x256 persistent tiles)", BF16_MFMA_PEAK_TFLOPS),
                 "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA, weight gradients)", BF16_MFMA_PEAK_TFLOPS),
-                "trunk_bf16": ("k_trunk_bf16 (fused bf16 trunk, layers 1..7 LDS-resident)", BF16_MFMA_PEAK_TFLOPS)}
+                "trunk_bf16": ("k_trunk_bf16 (fused bf16 trunk, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
+                "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS)}
 
 CONFIGS = {
     "c2": dict(workload="C2: JAX_214-shape scene (3 JAX_269 RPC cameras, GPU-generated rays), img_downscale=4, "
@@ -588,7 +589,7 @@ def run_train(a, config, rank, world, dev, secondary=False):
 
     kernels = {}
     for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "trunk_bf16", "tn_skinny", "encode", "heads_fwd",
-              "heads_bwd", "composite_fwd", "composite_bwd", "sample_guided", "render_loss", "pack", "adam"):
+              "heads_bwd", "heads_fused", "composite_fwd", "composite_bwd", "sample_guided", "render_loss", "pack", "adam"):
         s = _lib.prof_read(k)
         if s["launches"]:
             kernels[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / prof_steps,

@@ -44,6 +44,7 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);
 // tiles fed by LDS-DMA (when P % 32 == 0 as well);
 // <= 0 = library default (g_tn16_variant)
 extern int g_tn16_variant;
+extern int g_tn16_min_points;  // fewest points per split (option "tn_bf16_min_points")
 int tn_splits_bf16(int P, int N, int K, int variant = -1);
 int32_t gemm_tn_bf16(const TN16Args& a, int splits, hipStream_t s);
 

@@ -959,6 +959,8 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     return SPNERF_OK;
 }
 
+int g_tn16_min_points = 1024;  // fewest points per split of a bf16 weight-gradient GEMM
+
 int tn_splits_bf16(int P, int N, int K, int variant) {
     const bool wide = tn_wide(N, K, variant);
     const int tiles = wide ? cdiv(N, TW) * cdiv(K, TW) : cdiv(N, HB) * cdiv(K, HB);
@@ -966,7 +968,7 @@ int tn_splits_bf16(int P, int N, int K, int variant) {
     // second round (N = 768, K = 512 rounded up to 258 wide blocks: 221 us, two rounds)
     int splits = (wide ? 256 : 512) / tiles;
     if (splits > 64) splits = 64;
-    const int max_splits = cdiv(P, 1024);
+    const int max_splits = cdiv(P, g_tn16_min_points);
     if (splits > max_splits) splits = max_splits;
     return splits < 1 ? 1 : splits;
 }

@@ -30,7 +30,8 @@ namespace spn {
 struct PackPiece {
     const float* src;
     // bf: 1 = bf16 destination (dst in bf16 units); 2 = bf16 in the fused trunk's MFMA fragment
-    // order (trunk_frag_off, dst_ld = the layer's padded K); 3 = split into bf16 planes
+    // order (trunk_frag_off, dst_ld = the layer's padded K); 5 = the same for 32 features per
+    // wave (frag_off NA = 1: the fused heads' 256-wide layers); 3 = split into bf16 planes
     // [hi | hi | lo | lo] of width dst_ld / 4 each (hi = bf16(v), lo = bf16(v − hi)); 4 = the
     // same planes in the fused trunk's fragment order (dst_ld = 4·K0p)
     int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
         const int r = r0 + (tid >> 6) + 4 * e, c = c0 + (tid & 63);
         if (r >= pc.rows || c >= pc.cols) continue;
         const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
-        if (pc.bf >= 3) {
+        if (pc.bf == 3 || pc.bf == 4) {
             bf16* dst = reinterpret_cast<bf16*>(a.packed) + pc.dst;
             const int kp = pc.dst_ld / 4;
             const bf16 hi = (bf16)v, lo = (bf16)(v - (float)hi);
@@ -93,6 +94,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             continue;
         }
         const int64_t o = pc.dst + (pc.bf == 2        ? trunk_frag_off(r, c, pc.dst_ld)
+                                    : pc.bf == 5   ? frag_off(r, c, pc.dst_ld, 1)
                                     : pc.transpose ? (int64_t)c * pc.dst_ld + r
                                                    : (int64_t)r * pc.dst_ld + c);
         if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)v;
@@ -945,6 +947,14 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
         SPN_TRY(piece(x.s2W, 0, H, H, k.Ws2T16, H, 1, 1));
         SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3_16, H, 0, 1));
         SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3T16, H, 1, 1));
+        if (k.Ffeat16 >= 0) {  // the fused inference heads' fragment streams
+            if (d.sem) SPN_TRY(piece(x.m1W, 0, H, W, k.Fsem16, W, 0, 5));
+            SPN_TRY(piece(x.featW, 0, W, W, k.Ffeat16, W, 0, 2));
+            SPN_TRY(piece(x.s1W, 0, H, W, k.FQ16, W, 0, 2));
+            SPN_TRY(piece(x.r1W, 0, H, W, k.FQ16 + (int64_t)H * W, W, 0, 2));  // rows H.. of Q (64-row waves)
+            SPN_TRY(piece(x.s2W, 0, H, H, k.Fs2_16, H, 0, 5));
+            SPN_TRY(piece(x.s3W, 0, H, H, k.Fs3_16, H, 0, 5));
+        }
     }
     return launch_pack(v, packed, s);
 }
@@ -1050,6 +1060,10 @@ static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int M
 static bool fused_trunk_on(const Ctx& c) {
     return c.d.bf && g_fused_trunk && !c.k.Wf16.empty() && c.k.Wf16[1] >= 0;
 }
+// inference (nothing saved) of the full or the σ-only heads: the fused heads kernel after the trunk
+static bool heads_fused_on(const Ctx& c, bool save, int mode) {
+    return !save && (mode == 0 || mode == 1) && c.d.bf && c.k.Ffeat16 >= 0 && heads_bf16_supported(c.d);
+}
 static bool trunk_l0_on(const Ctx& c, bool save) {
     return fused_trunk_on(c) && g_l0_split && (g_trunk_l0 == 2 || (g_trunk_l0 == 1 && !save)) && c.k.Wf16[0] >= 0 &&
            trunk_l0_supported(c.d.K0p, save);
@@ -1144,6 +1158,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
         HL = dst;
     }
     if (mode == 1) return SPNERF_OK;
+    if (BF && heads_fused_on(c, save, mode)) return SPNERF_OK;  // G, Q, sun_v 2/3 inside the fused heads
     T* S2buf = save ? G::buf(c, c.w.S2) : G::buf(c, c.w.Hb[((d.L - 1) & 1) ^ 1]);
     T* S3buf = save ? G::buf(c, c.w.S3) : G::buf(c, c.w.Hb[2]);
     // G = H_L · [feat ; sem hidden]^T   (feat linear, sem hidden sin)
@@ -1227,6 +1242,17 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
     }
     if (d.bf) SPN_TRY(forward_gemms<bf16>(c, save, mode, s));
     else SPN_TRY(forward_gemms<float>(c, save, mode, s));
+    if (heads_fused_on(c, save, mode)) {
+        const int64_t hl = c.w.Hb[(d.L - 1) & 1];
+        HeadsFusedArgs a;
+        a.HL = c.hb(hl); a.packed = packed; a.rbQ = c.at(c.w.rbQ); a.sky = c.at(c.w.sky); a.out = out;
+        a.P = P; a.S = S; a.NO = d.NO; a.C = d.sem ? d.C : 0; a.sem_col = d.sem_col; a.mode = mode;
+        const double flop = mode == 1 ? 2.0 * P * W
+                                      : 2.0 * P * ((double)W * (W + 2 * H) + 2.0 * H * H + (d.sem ? (double)H * W + H * d.C : 0.0) +
+                                                   W + 4.0 * H);
+        SPN_TRY(heads_bf16(a, c.k, s, flop, 2.0 * P * W + 4.0 * P * (mode == 1 ? 1 : d.NO)));
+        return SPNERF_OK;
+    }
     {
         const int64_t L = d.L - 1;
         const int64_t hl = save ? c.w.Hb[L] : c.w.Hb[L & 1];
@@ -1511,6 +1537,8 @@ static int* option_slot(const char* name) {
     if (n == "l0_split") return &g_l0_split;
     if (n == "trunk_l0") return &g_trunk_l0;
     if (n == "bwd_streams") return &g_bwd_streams;
+    if (n == "tn_bf16_min_points") return &g_tn16_min_points;
+    if (n == "fused_heads") return &g_fused_heads;
     return nullptr;
 }
 

@@ -163,6 +163,13 @@ Packed packed_layout(const Dims& d) {
         k.Ws3_16 = take16((int64_t)H * H);
         k.Ws3T16 = take16((int64_t)H * H);
         k.W0s16 = take16((int64_t)W * 4 * k.Kp[0]);
+        if (heads_bf16_shape_ok(d)) {
+            if (d.sem) k.Fsem16 = take16((int64_t)H * W);
+            k.Ffeat16 = take16((int64_t)W * W);
+            k.FQ16 = take16((int64_t)2 * H * W);
+            k.Fs2_16 = take16((int64_t)H * H);
+            k.Fs3_16 = take16((int64_t)H * H);
+        }
     }
     k.total = off;
     return k;

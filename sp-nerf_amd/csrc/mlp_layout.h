@@ -54,6 +54,10 @@ struct PackedOffs {
     int64_t WG16 = -1, WGT16 = -1, WQ16 = -1, WQT16 = -1, Ws2_16 = -1, Ws2T16 = -1, Ws3_16 = -1, Ws3T16 = -1;
     // fc_net.0 as four bf16 planes [W][4·K0p] = [hi | hi | lo | lo] for the split layer 0
     int64_t W0s16 = -1;
+    // fused inference heads (heads_bf16.hip), MFMA fragment order (frag_off): semantic hidden
+    // [H][W] and sun_v 2 / 3 [H][H] with 32 features per wave, feat [W][W] and Q = [sun_v.0 ;
+    // rgb.0] [2H][W] with 64 per wave; -1 where the fused heads do not apply
+    int64_t Fsem16 = -1, Ffeat16 = -1, FQ16 = -1, Fs2_16 = -1, Fs3_16 = -1;
     int64_t total;
 };
 struct Packed : PackedOffs {

@@ -38,6 +38,37 @@ __host__ __device__ inline int64_t trunk_frag_off(int n, int k, int Kp) {
            (k & 7);
 }
 
+// MFMA A-fragment order for a layer whose waves own NA 32-feature tiles each (NA = 2: the trunk's
+// layout above; NA = 1: 32 features per wave, for 256-wide layers)
+__host__ __device__ inline int64_t frag_off(int n, int k, int Kp, int NA) {
+    const int nks = Kp >> 4, per = 32 * NA;
+    return ((((int64_t)(n / per) * nks + (k >> 4)) * NA + (n >> 5) % NA) * 64 + (n & 31) + 32 * ((k >> 3) & 1)) * 8 +
+           (k & 7);
+}
+
+// Fused inference heads (heads_bf16.hip): from the trunk's last activation H_L (bf16 [P][W]) to
+// the output rows, one persistent launch, a 128-point tile's activations resident in LDS:
+// σ = softplus(w_σ·H + b); semantic hidden = sin(W_m1 H + b) → logits (its C dot products in
+// the epilogue); feat = W_f H + b; [sun1 | rgb1] = sin(W_Q feat + b + per-ray sun rows);
+// albedo from rgb1; sun2 = sin(W_s2 sun1 + b); sun3 = sin(W_s3 sun2 + b); sun = sigmoid(w_s4
+// sun3 + b); sky from the per-ray rows.  W = 512, H = 256, no β head, C ≤ 4
+// (models/spnerf.py:332-367).
+struct HeadsFusedArgs {
+    const bf16* HL = nullptr;
+    const float* packed = nullptr;
+    const float* rbQ = nullptr;   // per-ray sun-direction rows of Q [B][2H]
+    const float* sky = nullptr;   // per-ray sky colour [B][4]
+    float* out = nullptr;
+    int64_t P = 0;
+    int S = 1, NO = 8, C = 0, sem_col = 8, mode = 0;  // mode: 0 all heads, 1 σ only
+};
+struct PackedOffs;
+struct Dims;
+bool heads_bf16_shape_ok(const Dims& d);   // the packed layout carries the fused heads' weights
+bool heads_bf16_supported(const Dims& d);  // ... and the option is on
+int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes);
+
+extern int g_fused_heads;  // 1 = bf16 inference runs the fused heads where supported (default)
 extern int g_fused_trunk;  // 1 = bf16 forwards use the fused trunk where supported (default)
 extern int g_trunk_tile;   // 0 = tile by mode; 64 / 128 = force
 extern int g_trunk_dbg;    // profiling ablations (outputs invalid): 1 = no HBM copy-outs

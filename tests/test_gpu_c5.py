@@ -108,3 +108,36 @@ def test_c5_full_chunk_properties_and_bf16_vs_fp32():
         e = gu.rel_err(r[k].cpu().numpy(), out["fp32"][k].cpu().numpy())
         print(k, f"{e:.2e}")
         assert e < OUT_TOL, (k, e)
+
+
+@pytest.mark.parametrize("sem", [True, False])
+def test_fused_inference_heads_match_layer_by_layer_heads(sem):
+    """bf16 inference with the fused heads kernel (σ, semantic hidden → logits, feat, Q, albedo,
+    sun_v 2/3 → sun, sky on an LDS-resident 128-point tile; csrc/heads_bf16.hip) against the
+    G / Q / sun_v GEMMs + k_heads_fwd_v path (option fused_heads=0) on the same rays and draws:
+    same bf16 rounding points, other fp32 summation orders → norm-relative 2e-3 per key."""
+    from spnerf_amd import _lib
+    from oracle.weights import ModelDims
+    g = torch.Generator(device="cpu").manual_seed(5)
+    B, S = 3000, 128
+    rays = torch.tensor(gu.synthetic_rays(B, 21), device=DEV)
+    u = torch.rand(B, S, generator=g).to(DEV)
+    labels = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    args = gu.args_of({"args": dict(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                                    sc_lambda=0.0, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+    model = make_model(ModelDims(width=512, sem=sem), 6, "bf16")
+    outs = []
+    try:
+        for fused in (1, 0):
+            _lib.set_option("fused_heads", fused)
+            with torch.no_grad(), random_source(FixedU(u)):
+                outs.append(spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels if sem else None,
+                                                   mode="test"))
+    finally:
+        _lib.set_option("fused_heads", 1)
+    for k in outs[1]:
+        a, b = outs[0][k].cpu().numpy(), outs[1][k].cpu().numpy()
+        assert np.isfinite(a).all(), k
+        e = gu.rel_err(a, b)
+        print(k, f"{e:.2e}")
+        assert e < 2e-3, (k, e)
