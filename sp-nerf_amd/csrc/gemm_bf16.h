@@ -23,6 +23,8 @@ struct NT16Args {
     bf16* Dout = nullptr; int ld_dout = 0;
     const bf16* Dmul = nullptr; int ld_dmul = 0;
     int k_alg = 0;  // algorithmic K for the FLOP count (0 = K; the hi/lo layer-0 GEMM: K0p of its K = 4·K0p)
+    int dbg = 0;    // ablations (tools only; variant 8): 1 = no MFMAs, 2 = no epilogue, 4 = no DMA wait
+    unsigned long long* stamps = nullptr;  // diagnostic builds (-DND_STAMPS, tools only)
 };
 
 // slab[s][n][k] = Σ_{p in split s} A[p][n] · B[p][k] (B split along k at K1),

@@ -433,6 +433,260 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_bf16w(NT16Args g, in
     }
 }
 
+// 256 x 256 NT tile fed by LDS-DMA through a ring that runs across tile boundaries
+// (nt_bf16_variant 8).  k_gemm_nt_bf16w keeps one K-step of loads in flight and leaves HBM idle
+// through each tile's epilogue, whose Dmul loads then wait one full latency per 32 x 64 piece
+// (C4's backward dX GEMMs ran at 41% of HBM).  Here:
+//  * K-steps of 32 (64-B rows, 16-B chunk c of row r at c ^ ((r >> 2) & 3): conflict-free
+//    ds_read_b128 for the 32x32x16 fragments) land by global_load_lds_dwordx4 in four 32 KB
+//    stages, three steps in flight; the step sequence is flat over the block's tiles, so the
+//    next tile's first three steps are loading while this tile's epilogue runs;
+//  * the epilogue stages 32 x 64 fp32 pieces (256-B rows, chunks XOR row & 1) in the stage the
+//    tile's last step was read from (waves 4..7) and in a 32 KB area outside the ring (waves
+//    0..3), and the next piece's Dmul rows load while a piece is finished.
+// Same k order as k_gemm_nt_bf16w (16-wide k blocks in increasing k): bit-identical outputs.
+// K and K1 must be multiples of 32 (host-checked).
+constexpr int ND_K = 32, ND_STAGES = 4, ND_STG = 512 * 64;
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+#ifdef ND_STAMPS
+// diagnostic build only (tools/gemm_bench_bf16 -DND_STAMPS): lane 0 of waves 0 and 4 of block 0
+// record s_memtime at the phase boundaries; never compiled into the library
+#define ND_STAMP(slot)                                                                          \
+    do {                                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        unsigned long long t_;                                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        if (st_on) g.stamps[st_base + st_n] = t_ * 16 + (slot);                                \
+        ++st_n;                                                                                 \
+    } while (0)
+#else
+#define ND_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
+// DM: the backward dX epilogue only (C = acc · Dmul, no bias / rank-1 / sine): every epilogue
+// load is unconditional, so no branch drains the in-flight DMAs (vmcnt(0)).
+template <bool DM>
+__global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
+    __shared__ __attribute__((aligned(16))) char smem[ND_STAGES * ND_STG + 8 * 4096];
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+    constexpr int MI = 4, NJ = 2;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nN = (g.N + 255) / 256;
+    const int G = gridDim.x;
+    int t = xcd_remap(blockIdx.x, G);
+    if (t >= ntiles) return;  // block-uniform
+    const int nk = g.K / ND_K;
+
+    // DMA: instruction q = wid + 8 i fills stage rows 16 q .. 16 q + 15 (rows < 256: A, else B);
+    // lane l lands at row 16 q + l / 4, chunk position l % 4, so it loads the logical chunk
+    // (l % 4) ^ ((row >> 2) & 3)
+    int is_t = t, is_k = 0;  // issue pointer: tile, K-step
+    auto issue = [&](int stg) {
+        const int tile = is_t < ntiles ? is_t : t;  // past the last tile: re-reads, never consumed
+        const int bm = (tile / nN) * 256, bn = (tile % nN) * 256;
+        const int k0 = is_k * ND_K;
+        const bool seg2 = k0 >= g.K1;
+        const bf16* pa = seg2 ? g.A2 + (k0 - g.K1) : g.A + k0;
+        const int lda = seg2 ? g.lda2 : g.lda;
+        const int el = opaque(lane);
+        const int ni = (g.dbg & 16) ? 2 : 4;  // ablation: A only
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i >= ni) break;
+            const int q = wid + 8 * i;
+            const int row = 16 * q + (el >> 2);
+            const int c8 = ((el & 3) ^ ((row >> 2) & 3)) * 8;
+            const bf16* src = i < 2 ? pa + (int64_t)min(bm + row, g.M - 1) * lda + c8
+                                    : g.B + (int64_t)min(bn + row - 256, g.N - 1) * g.ldb + k0 + c8;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(smem + stg * ND_STG + q * 1024), 16, 0, 0);
+        }
+        if (++is_k == nk) {
+            is_k = 0;
+            is_t += G;
+        }
+    };
+
+    f32x16 acc[MI][NJ];
+    const int wr = wid >> 2, wc = wid & 3, r32 = lane & 31, h = lane >> 5;
+    auto compute = [&](int stg) {
+        const int swz = (r32 >> 2) & 3;
+        const char* sA = smem + stg * ND_STG + (wr * 128 + r32) * 64;
+        const char* sB = smem + stg * ND_STG + (256 + wc * 64 + r32) * 64;
+#pragma unroll
+        for (int ks = 0; ks < ND_K / 16; ++ks) {
+            const int off = ((2 * ks + h) ^ swz) * 16;
+            bf16x8 a[MI], b[NJ];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(sA + i * 32 * 64 + off);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(sB + j * 32 * 64 + off);
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+#ifdef ND_STAMPS
+    const bool st_on = g.stamps && blockIdx.x == 0 && (wid == 0 || wid == 4) && lane == 0;
+    const int st_base = (wid >> 2) * 4096;
+    int st_n = 0;
+#endif
+    int gs = 0;  // flat step counter: step gs sits in stage gs % ND_STAGES
+    issue(0);
+    issue(1);
+    issue(2);
+    while (true) {
+        const int bm = (t / nN) * 256, bn = (t % nN) * 256;
+        const int tn = t + G;
+        const bool more = tn < ntiles;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int kt = 0; kt < nk; ++kt, ++gs) {
+            // step gs has landed when at most the two newer steps' DMAs (4 each) are outstanding
+            // (after an epilogue its stores are newer still: the wait is then stricter, not
+            // wrong); the barrier publishes every wave's DMAs and retires the reads of stage
+            // (gs + 3) % 4 (step gs - 1, or the previous epilogue's staging)
+            ND_STAMP(0);
+            if (g.dbg & 16) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (!(g.dbg & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            ND_STAMP(1);
+            __builtin_amdgcn_s_barrier();
+            ND_STAMP(2);
+            issue((gs + 3) % ND_STAGES);
+            ND_STAMP(3);
+            if (!(g.dbg & 1)) compute(gs % ND_STAGES);
+        }
+        ND_STAMP(4);
+        if (g.dbg & 2) {
+            if (tn >= ntiles) break;
+            t = tn;
+            continue;
+        }
+        // ---- epilogue: the wave's 128 x 64 outputs as four 32 x 64 pieces
+        const int el = opaque(lane), cq = (el & 7) * 8, erow = el >> 3, er32 = el & 31, eh = el >> 5;
+        const int col = bn + wc * 64 + cq;
+        const bool colok = col < g.N;
+        const int colc = colok ? col : g.N - 8;
+        const int rbase = bm + wr * 128 + erow;
+        auto dload = [&](u32x4 (&dm)[4], float (&r1a)[4], int i) {
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int row = min(rbase + i * 32 + 8 * q4, g.M - 1);
+                if constexpr (DM) {
+                    dm[q4] = ldg16(g.Dmul + (int64_t)row * g.ld_dmul + colc);
+                    r1a[q4] = 0.f;
+                } else {
+                    dm[q4] = g.Dmul ? ldg16(g.Dmul + (int64_t)row * g.ld_dmul + colc) : u32x4{0u, 0u, 0u, 0u};
+                    r1a[q4] = g.r1_a ? g.r1_a[(int64_t)row * g.r1_lda] : 0.f;
+                }
+            }
+        };
+        // Dmul rows in flight one piece ahead
+        constexpr int NB = 2;  // all four at once measured slower (546 vs 510 us, 524 288 x 512 x 512)
+        u32x4 dm[NB][4];
+        float r1a[NB][4];
+#pragma unroll
+        for (int p = 0; p + 1 < NB; ++p) dload(dm[p], r1a[p], p);
+        float bias8[8], r1v8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            bias8[e] = !DM && g.bias ? g.bias[colc + e] : 0.f;
+            r1v8[e] = !DM && g.r1_a ? g.r1_v[colc + e] : 0.f;
+        }
+        // every wave is done reading stage (gs - 1) % 4 before waves 4..7 stage into it
+        ND_STAMP(5);
+        __builtin_amdgcn_s_barrier();
+        ND_STAMP(6);
+        float* stage = wid < 4 ? reinterpret_cast<float*>(smem + ND_STAGES * ND_STG + wid * 8192)
+                               : reinterpret_cast<float*>(smem + ((gs + 3) % ND_STAGES) * ND_STG + (wid - 4) * 8192);
+        const bool sine_cols = !DM && g.act == 1 && col >= g.n_lin;  // n_lin is a multiple of 8
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            if (i + NB - 1 < MI) dload(dm[(i + NB - 1) % NB], r1a[(i + NB - 1) % NB], i + NB - 1);
+            lds_order();
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = (r & 3) + 8 * (r >> 2) + 4 * eh, cc = j * 32 + er32;
+                    stage[rr * 64 + ((((cc >> 2) ^ (rr & 1)) << 2) | (cc & 3))] = acc[i][j][r];
+                }
+            lds_order();
+            u32x4 oc[4], od[4];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int rr = erow + 8 * q4;
+                const int row = rbase + i * 32 + 8 * q4;
+                const f32x4 lo = ld4(stage + rr * 64 + (((cq >> 2) ^ (rr & 1)) << 2));
+                const f32x4 hi = ld4(stage + rr * 64 + ((((cq >> 2) + 1) ^ (rr & 1)) << 2));
+                float v[8], d[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = lo[e] + bias8[e];
+                    v[e + 4] = hi[e] + bias8[e + 4];
+                }
+                if (!DM && g.rowbias) {
+                    const float* rb = g.rowbias + (int64_t)(min(row, g.M - 1) / g.rows_per_ray) * g.ld_rb + colc;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += rb[e];
+                }
+                if (!DM && g.r1_a) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += r1a[i % NB][q4] * r1v8[e];
+                }
+                if (sine_cols) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        float sn, cs;
+                        fast_sincos(g.w0 * v[e], &sn, &cs);
+                        v[e] = sn;
+                        d[e] = g.w0 * cs;
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) d[e] = 1.f;
+                }
+                if (DM || g.Dmul) {
+                    float m[8];
+                    unpack8(dm[i % NB][q4], m);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] *= m[e];
+                }
+                oc[q4] = pack8(v);
+                od[q4] = pack8(d);
+                // materialise the piece's results here: hipcc otherwise sinks the arithmetic
+                // (and the Dmul waits, as vmcnt(0)) into the guarded stores below
+                asm volatile("" : "+v"(oc[q4]));
+                if constexpr (!DM) asm volatile("" : "+v"(od[q4]));
+            }
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int row = rbase + i * 32 + 8 * q4;
+                if (row < g.M && colok) {
+                    *reinterpret_cast<u32x4*>(g.C + (int64_t)row * g.ldc + col) = oc[q4];
+                    if (!DM && g.Dout && sine_cols) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
+                }
+            }
+            ND_STAMP(8);
+        }
+        ND_STAMP(7);
+        if (!more) break;  // block-uniform
+        t = tn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-read DMAs land before the block exits
+#ifdef ND_STAMPS
+    if (st_on) g.stamps[st_base + 4095] = st_n;
+#endif
+}
+
 // ------------------------------------------------------------------------------------------
 // TN (weight gradients)
 // ------------------------------------------------------------------------------------------
@@ -905,7 +1159,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
-int g_nt16_variant = 5;
+int g_nt16_variant = 8;
 int g_tn16_variant = 2;
 
 static bool tn_wide(int N, int K, int variant) {
@@ -936,7 +1190,16 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
                           (double)a.M * dcols));
     // variants: 1 / 2 = one block per tile, prefetch depth 1 / 2; 3 / 4 = persistent grid of
     // two blocks per CU (the LDS limit), depth 1 / 2
-    const int v = variant > 0 ? variant : g_nt16_variant;
+    int v = variant > 0 ? variant : g_nt16_variant;
+    if (v == 8 && (a.K % ND_K != 0 || (a.K1 != a.K && a.K1 % ND_K != 0))) v = 5;  // DMA needs whole 32-wide K-steps
+    if (v == 8) {
+        const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
+        const bool dm = a.Dmul && !a.bias && !a.rowbias && !a.r1_a && a.act == 0 && !a.Dout;
+        if (dm) hipLaunchKernelGGL(k_gemm_nt_bf16d<true>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else hipLaunchKernelGGL(k_gemm_nt_bf16d<false>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        SPN_HIP(hipGetLastError());
+        return SPNERF_OK;
+    }
     if (v >= 5) {  // generalised tiles, persistent with one block per CU
         if (v == 5) {
             const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);

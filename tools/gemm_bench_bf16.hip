@@ -100,7 +100,8 @@ static void check_nt(int M, int N, int K, int K1, bool sine, bool timing) {
     g.B = B.d; g.ldb = K; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K;
     if (sine) { g.bias = dbias; g.act = 1; g.w0 = 1.f; g.Dout = D; g.ld_dout = N; }
     else { g.Dmul = Dm.d; g.ld_dmul = N; }
-    for (int v : {1, 3, 5, 6, 7}) {
+    std::vector<uint16_t> c5;
+    for (int v : {1, 3, 5, 6, 7, 8}) {
     CK(hipMemset(C, 0, (size_t)M * N * 2));
     if (gemm_nt_bf16(g, 0, v) != 0) { printf("launch refused\n"); fails++; return; }
     CK(hipDeviceSynchronize());
@@ -118,7 +119,13 @@ static void check_nt(int M, int N, int K, int K1, bool sine, bool timing) {
             if (sine) worstd = std::max(worstd, std::fabs(refd - dd[(size_t)r * N + n]));
         }
     }
-    const bool ok = worst < 2e-2 && worstd < 2e-2;  // bf16 output rounding: |y| <= ~2, ulp 2^-8
+    bool ok = worst < 2e-2 && worstd < 2e-2;  // bf16 output rounding: |y| <= ~2, ulp 2^-8
+    {   // variants 5 and 8 accumulate in the same k order: bit-identical C
+        std::vector<uint16_t> raw((size_t)M * N);
+        CK(hipMemcpy(raw.data(), C, raw.size() * 2, hipMemcpyDeviceToHost));
+        if (v == 5) c5 = raw;
+        if (v == 8 && raw != c5) { printf("[v8 != v5 bitwise] "); ok = false; }
+    }
     if (!ok) fails++;
     printf("nt%d M=%-7d N=%-4d K=%-4d K1=%-4d %s  max|err| C %.2e D %.2e  %s", v, M, N, K, K1, sine ? "sine" : "dmul", worst,
            worstd, ok ? "ok" : "FAIL");
@@ -226,12 +233,59 @@ int main(int argc, char** argv) {
         NT16Args g;
         g.A = A.d; g.lda = 512; g.K1 = 512; g.B = B.d; g.ldb = 512; g.C = C; g.ldc = 512; g.M = P; g.N = 512; g.K = 512;
         g.bias = dbias; g.act = 1; g.Dout = D; g.ld_dout = 512;
-        const char* names[] = {"128x128 persistent", "256x256 8 waves", "256x128 8 waves", "128x256 4 waves"};
-        const int vs[] = {3, 5, 6, 7};
-        for (int i = 0; i < 4; ++i) {
+        const char* names[] = {"128x128 persistent", "256x256 8 waves", "256x128 8 waves", "128x256 4 waves",
+                               "256x256 DMA ring"};
+        const int vs[] = {3, 5, 6, 7, 8};
+        for (int i = 0; i < 5; ++i) {
             const double us = time_it([&] { gemm_nt_bf16(g, 0, vs[i]); });
             printf("variant %-20s %8.1f us %7.1f TF/s\n", names[i], us, 2.0 * P * 512 * 512 / us * 1e-6);
         }
+        // variant 8 ablations on the backward (xDmul) shape
+        HMat Dm(P, 512, 1.f, 4);
+        NT16Args gd = g;
+        gd.bias = nullptr; gd.act = 0; gd.Dout = nullptr; gd.Dmul = Dm.d; gd.ld_dmul = 512;
+        const char* an[] = {"dmul full", "no MFMA", "no epilogue", "no MFMA+epi", "no DMA wait", "no wait+MFMA+epi",
+                            "A only", "A only no MFMA+epi", "A only no epi", "A only no MFMA"};
+        const int ad[] = {0, 1, 2, 3, 4, 7, 16, 19, 18, 17};
+        for (int i = 0; i < 10; ++i) {
+            gd.dbg = ad[i];
+            const double us = time_it([&] { gemm_nt_bf16(gd, 0, 8); });
+            printf("nt8 ablation %-18s %8.1f us\n", an[i], us);
+        }
+#ifdef ND_STAMPS
+        {   // phase shares of one block's waves 0 and 4 (diagnostic build: read shares, not lengths)
+            unsigned long long* st;
+            CK(hipMalloc(&st, 8192 * 8));
+            CK(hipMemset(st, 0, 8192 * 8));
+            gd.dbg = 0;
+            gd.stamps = st;
+            gemm_nt_bf16(gd, 0, 8);
+            CK(hipDeviceSynchronize());
+            std::vector<unsigned long long> h(8192);
+            CK(hipMemcpy(h.data(), st, 8192 * 8, hipMemcpyDeviceToHost));
+            const char* ph[] = {"top->waited", "waited->barrier", "barrier->issued", "issued->next top (compute)",
+                                "loop end->epi barrier", "epi barrier", "epi->piece 0", "piece i->i+1"};
+            for (int w = 0; w < 2; ++w) {
+                const unsigned long long* v = h.data() + 4096 * w;
+                const int n = (int)v[4095];
+                double sum[9] = {0};
+                for (int k = 1; k < n; ++k) {
+                    const int from = (int)(v[k - 1] & 15);
+                    const double dt = (double)((v[k] >> 4) - (v[k - 1] >> 4));
+                    int cls = from <= 2 ? from : (from == 3 ? 3 : (from == 4 ? 4 : (from == 5 ? 5 : (from == 6 ? 6 : 7))));
+                    if (from == 8 && (v[k] & 15) == 0) cls = 8;  // last piece -> next tile's loop
+                    sum[cls] += dt;
+                }
+                double tot = 0;
+                for (double x : sum) tot += x;
+                printf("stamps wave %d: %d stamps, %.0f cycles\n", w * 4, n, tot);
+                for (int c = 0; c < 8; ++c) printf("   %-28s %5.1f%%\n", ph[c], 100 * sum[c] / tot);
+                printf("   %-28s %5.1f%%\n", "last piece->next tile", 100 * sum[8] / tot);
+            }
+            gd.stamps = nullptr;
+            CK(hipFree(st));
+        }
+#endif
         CK(hipFree(C)); CK(hipFree(D));
     }
     check_tn(P, 512, 512, 512, true);
