@@ -114,6 +114,34 @@ __device__ __forceinline__ float fast_cos(float x) {
     return __builtin_amdgcn_cosf(r);
 }
 
+// The saved pre-activation Z of a bf16 trunk layer is stored as fp16 (11-bit significand: 4x
+// finer than bf16 at the same 2 bytes; hidden-layer |Z| is O(1), far inside fp16's range), and
+// the layer computes H = sin(Z), D = cos(Z) from that rounded Z, so every consumer recomputes
+// them bit-identically.  zr16: x rounded to fp16 and back.
+__device__ __forceinline__ float zr16(float x) { return (float)(_Float16)x; }
+__device__ __forceinline__ uint32_t pack2_f16(float lo, float hi) {
+    const _Float16 a = (_Float16)lo, b = (_Float16)hi;
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+__device__ __forceinline__ u32x4 pack8_f16(const float (&f)[8]) {
+    return u32x4{pack2_f16(f[0], f[1]), pack2_f16(f[2], f[3]), pack2_f16(f[4], f[5]), pack2_f16(f[6], f[7])};
+}
+__device__ __forceinline__ void unpack8_f16(u32x4 v, float (&f)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[2 * i] = (float)__builtin_bit_cast(_Float16, (uint16_t)(v[i] & 0xffffu));
+        f[2 * i + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(v[i] >> 16));
+    }
+}
+// 8 saved Z (fp16) -> 8 bf16 sin(Z): the H a saved-Z trunk layer stands for
+__device__ __forceinline__ u32x4 sin8_z(u32x4 v) {
+    float f[8];
+    unpack8_f16(v, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fast_sin(f[e]);
+    return pack8(f);
+}
+
 // a copy of x the compiler cannot see through: lane-derived addresses computed from it are
 // recomputed where used instead of being hoisted out of every loop and kept live across the
 // MFMA main loop (where the accumulators need the registers)

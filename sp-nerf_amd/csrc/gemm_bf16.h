@@ -23,6 +23,10 @@ struct NT16Args {
     bf16* Dout = nullptr; int ld_dout = 0;
     const bf16* Dmul = nullptr; int ld_dmul = 0;
     int k_alg = 0;  // algorithmic K for the FLOP count (0 = K; the hi/lo layer-0 GEMM: K0p of its K = 4·K0p)
+    // saved-pre-activation trunk layers (w0 = 1; option "zsave"): zround rounds the sine columns'
+    // v to fp16 before sin / cos, dout_z stores that v (Z, fp16 bits) in Dout instead of
+    // D = cos, and dmul_z reads Dmul as Z (fp16) and multiplies by cos(Z)
+    int zround = 0, dout_z = 0, dmul_z = 0;
     int dbg = 0;    // ablations (tools only; variant 8): 1 = no MFMAs, 2 = no epilogue, 4 = no DMA wait
     unsigned long long* stamps = nullptr;  // diagnostic builds (-DND_STAMPS, tools only)
 };
@@ -37,6 +41,7 @@ struct TN16Args {
     float* slab_b = nullptr;
     int P = 0, N = 0, K = 0;
     int p_per_split = 0;  // set by gemm_tn_bf16
+    int b_sin = 0;        // B's columns [0, K1) hold a saved Z (fp16): staged as bf16(sin(Z)) (= the layer's H)
 };
 
 // variant: prefetch depth in K-steps (1 or 2); <= 0 = library default (g_nt16_variant)

@@ -210,9 +210,10 @@ __global__ __launch_bounds__(256) void k_gemm_nt_bf16(NT16Args g, int ntiles) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         float sn, cs;
-                        fast_sincos(g.w0 * v[e], &sn, &cs);
+                        const float z = g.zround ? zr16(v[e]) : v[e];
+                        fast_sincos(g.w0 * z, &sn, &cs);
                         v[e] = sn;
-                        d[e] = g.w0 * cs;
+                        d[e] = g.dout_z ? z : g.w0 * cs;
                     }
                 } else {
 #pragma unroll
@@ -220,12 +221,18 @@ __global__ __launch_bounds__(256) void k_gemm_nt_bf16(NT16Args g, int ntiles) {
                 }
                 if (g.Dmul) {
                     float m[8];
-                    unpack8(dm[i][q4], m);
+                    if (g.dmul_z) {  // Dmul holds the saved Z (fp16): D = cos(Z)
+                        unpack8_f16(dm[i][q4], m);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) m[e] = fast_cos(m[e]);
+                    } else {
+                        unpack8(dm[i][q4], m);
+                    }
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[e] *= m[e];
                 }
                 oc[q4] = pack8(v);
-                od[q4] = pack8(d);
+                od[q4] = g.dout_z ? pack8_f16(d) : pack8(d);
             }
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4) {
@@ -398,9 +405,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_bf16w(NT16Args g, in
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
                             float sn, cs;
-                            fast_sincos(g.w0 * v[e], &sn, &cs);
+                            const float z = g.zround ? zr16(v[e]) : v[e];
+                            fast_sincos(g.w0 * z, &sn, &cs);
                             v[e] = sn;
-                            d[e] = g.w0 * cs;
+                            d[e] = g.dout_z ? z : g.w0 * cs;
                         }
                     } else {
 #pragma unroll
@@ -408,12 +416,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_bf16w(NT16Args g, in
                     }
                     if (g.Dmul) {
                         float m[8];
-                        unpack8(dm[q4], m);
+                        if (g.dmul_z) {  // Dmul holds the saved Z (fp16): D = cos(Z)
+                            unpack8_f16(dm[q4], m);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) m[e] = fast_cos(m[e]);
+                        } else {
+                            unpack8(dm[q4], m);
+                        }
 #pragma unroll
                         for (int e = 0; e < 8; ++e) v[e] *= m[e];
                     }
                     oc[q4] = pack8(v);
-                    od[q4] = pack8(d);
+                    od[q4] = g.dout_z ? pack8_f16(d) : pack8(d);
                 }
 #pragma unroll
                 for (int q4 = 0; q4 < 4; ++q4) {
@@ -646,9 +660,10 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         float sn, cs;
-                        fast_sincos(g.w0 * v[e], &sn, &cs);
+                        const float z = g.zround ? zr16(v[e]) : v[e];
+                        fast_sincos(g.w0 * z, &sn, &cs);
                         v[e] = sn;
-                        d[e] = g.w0 * cs;
+                        d[e] = g.dout_z ? z : g.w0 * cs;
                     }
                 } else {
 #pragma unroll
@@ -656,12 +671,18 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                 }
                 if (DM || g.Dmul) {
                     float m[8];
-                    unpack8(dm[i % NB][q4], m);
+                    if (g.dmul_z) {  // Dmul holds the saved Z (fp16): D = cos(Z)
+                        unpack8_f16(dm[i % NB][q4], m);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) m[e] = fast_cos(m[e]);
+                    } else {
+                        unpack8(dm[i % NB][q4], m);
+                    }
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[e] *= m[e];
                 }
                 oc[q4] = pack8(v);
-                od[q4] = pack8(d);
+                od[q4] = g.dout_z ? pack8_f16(d) : pack8(d);
                 // materialise the piece's results here: hipcc otherwise sinks the arithmetic
                 // (and the Dmul waits, as vmcnt(0)) into the guarded stores below
                 asm volatile("" : "+v"(oc[q4]));
@@ -722,6 +743,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
     const int nc = min(n0 + 8 * ch, g.N - 8);
     const int kc = min(k0 + 8 * ch, g.K - 8);
     const bf16* pb = kc < g.K1 ? g.B + kc : g.B2 + (kc - g.K1);
+    const bool bsin = g.b_sin && kc < g.K1;  // this thread's B chunk is a saved Z: stage sin(Z)
     const int ldb = kc < g.K1 ? g.ldb : g.ldb2;
     const int lda = g.lda;
     int p_ld = 0;
@@ -750,7 +772,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
             }
             const int o = tn_off(lrow + 16 * i, ch);
             *reinterpret_cast<u32x4*>(sA + o) = v;
-            *reinterpret_cast<u32x4*>(sB + o) = pin ? rb[i] : z;
+            *reinterpret_cast<u32x4*>(sB + o) = pin ? (bsin ? sin8_z(rb[i]) : rb[i]) : z;
         }
     };
 
@@ -865,6 +887,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
     const int nc = min(n0 + 8 * ch, g.N - 8);
     const int kc = min(k0 + 8 * ch, g.K - 8);
     const bf16* pb = kc < g.K1 ? g.B + kc : g.B2 + (kc - g.K1);
+    const bool bsin = g.b_sin && kc < g.K1;  // this thread's B chunk is a saved Z: stage sin(Z)
     const int ldb = kc < g.K1 ? g.ldb : g.ldb2;
     const int lda = g.lda;
     const int soff = (ch >> 4) * 64 * 256;  // half of the tile this thread's chunk lands in
@@ -894,7 +917,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
             }
             const int o = tn_off(lrow + 16 * i, ch & 15);
             *reinterpret_cast<u32x4*>(sA + o) = v;
-            *reinterpret_cast<u32x4*>(sB + o) = pin ? rb[i] : z;
+            *reinterpret_cast<u32x4*>(sB + o) = pin ? (bsin ? sin8_z(rb[i]) : rb[i]) : z;
         }
     };
 
@@ -1250,7 +1273,7 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     if (tn_wide(a.N, a.K, -1)) {
         const int nb = cdiv(a.N, TW) * cdiv(a.K, TW);
         const int v = g_tn16_variant;
-        if (v == 3 && a.P % TD_STEP == 0)  // DMA needs whole 32-point steps (p_per_split is a multiple of 64)
+        if (v == 3 && a.P % TD_STEP == 0 && !a.b_sin)  // DMA: whole 32-point steps, B staged as is
             hipLaunchKernelGGL(k_gemm_tn_bf16d, dim3(nb * splits), dim3(512), 0, s, a);
         else
             hipLaunchKernelGGL(k_gemm_tn_bf16w, dim3(nb * splits), dim3(512), 0, s, a);

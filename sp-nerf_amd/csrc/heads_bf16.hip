@@ -127,7 +127,7 @@ __device__ __forceinline__ float row_dot(const char* smem, int row, int ch0, int
 
 __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs k, int ntiles) {
     __shared__ __attribute__((aligned(16))) char smem[LDS];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     float* ost = reinterpret_cast<float*>(smem + OST_OFF);
     float* part = reinterpret_cast<float*>(smem + PART_OFF);
     const float* Pk = g.packed;

@@ -1002,13 +1002,14 @@ struct Gemms<bf16> {
 
 template <typename T>
 static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int ldb, const T* B2, int ldb2, int K1,
-                       int K, hipStream_t s, std::initializer_list<ReduceArgs> outs) {
+                       int K, hipStream_t s, std::initializer_list<ReduceArgs> outs, bool b_sin = false) {
     using G = Gemms<T>;
     const int P = (int)c.w.P;
     const int splits = G::splits(P, N, K);
     typename G::TN t;
     t.A = A; t.lda = lda;
     t.B = B; t.ldb = ldb; t.B2 = B2; t.ldb2 = ldb2; t.K1 = K1;
+    if constexpr (std::is_same<T, bf16>::value) t.b_sin = b_sin ? 1 : 0;  // B[:, :K1] holds a saved Z
     t.slab = c.at(c.w.slab); t.ld_slab = K; t.slab_stride = (int64_t)N * K;
     t.slab_b = c.at(c.w.slab_b);
     t.P = P; t.N = N; t.K = K;
@@ -1057,6 +1058,14 @@ static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int M
 // Trunk + G/Q/sun_v GEMMs of the forward (spnerf.py:323-355).  In the bf16 MLP, layer 0 stays
 // an fp32 GEMM (sin(30·x) amplifies operand rounding 30x) that writes bf16 H_1 / D_1.
 // bf16 MLP: layer 0 runs inside the fused trunk launch (reading the fp32 PE rows itself)
+// bf16 trunk layers 1 .. L-1 (w0 = 1) compute H = sin(Z) with Z = fp16(pre-activation), and the
+// training forward saves Z alone for layers 1 .. L-2 (Z and H for the last): the backward stages
+// sin(Z) for the weight gradients and multiplies by cos(Z) in the dX epilogues, so the forward
+// writes one [P][512] tensor per layer instead of H and D (option "zsave"; must not change
+// between a forward and its backward).  Off by default: measured on C4 (tools/gpu_ab_opt.sh) the
+// trunk saves 0.9 ms per step but the weight gradients' sin staging costs 1.25 ms (31.3 vs 31.9 ms)
+int g_zsave = 0;
+
 static bool fused_trunk_on(const Ctx& c) {
     return c.d.bf && g_fused_trunk && !c.k.Wf16.empty() && c.k.Wf16[1] >= 0;
 }
@@ -1081,6 +1090,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
     const T* h = nullptr;
     T* HL = nullptr;
     const bool fused = BF && fused_trunk_on(c);
+    const bool zs = BF && g_zsave;
     const int first = fused && trunk_l0_on(c, save) ? 0 : 1;  // first layer of the fused launch
     for (int i = 0; i < d.L; ++i) {
         if (fused && i == first) {
@@ -1096,16 +1106,19 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
             for (int l = first; l < d.L; ++l) {
                 a.Wf[l] = c.pk16(c.k.Wf16[l]);
                 a.bias[l] = c.pk(c.k.bt[l]);
-                a.Hs[l] = save ? c.hb(c.w.Hb[l]) : (l == d.L - 1 ? c.hb(c.w.Hb[l & 1]) : nullptr);
+                const bool zonly = zs && l >= 1 && l < d.L - 1;  // Z alone (in Db) for the backward
+                a.Hs[l] = save ? (zonly ? nullptr : c.hb(c.w.Hb[l])) : (l == d.L - 1 ? c.hb(c.w.Hb[l & 1]) : nullptr);
                 a.Ds[l] = save ? c.hb(c.w.Db[l]) : nullptr;
                 ksum += l == 0 ? d.K0p : c.k.Kp[l];   // algorithmic K (layer 0 runs 4·K0p on hi/lo planes)
             }
             a.rb_skip = d.sem ? c.at(c.w.rb4) : nullptr;
             a.P = P; a.S = S; a.L = d.L; a.skip = d.skip; a.K0p = d.K0p;
+            a.zround = zs ? 1 : 0;
             // algorithmic HBM bytes: the first layer's input (fp32 PE, or H_1 and the bf16 PE)
-            // in, H (and D) of every layer out when saving
+            // in; out when saving H and D of every layer, or Z of every layer and the last H
             const double in = first == 0 ? 4.0 * P * d.K0p : 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0));
-            const double bytes = in + 2.0 * P * W * (save ? 2.0 * (d.L - first) : 1.0);
+            const double nout = !save ? 1.0 : (zs ? d.L - first + 1.0 : 2.0 * (d.L - first));
+            const double bytes = in + 2.0 * P * W * nout;
             SPN_TRY(trunk_bf16(a, s, 2.0 * P * W * ksum, bytes));
             HL = reinterpret_cast<T*>(a.Hs[d.L - 1]);
             break;
@@ -1152,6 +1165,10 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
             if (rb) { g.rowbias = rb; g.ld_rb = W; g.rows_per_ray = S; }
             g.act = 1; g.w0 = 1.f; g.n_lin = 0;
             if (save) { g.Dout = dd; g.ld_dout = W; }
+            if constexpr (BF) {
+                g.zround = zs ? 1 : 0;
+                g.dout_z = zs ? 1 : 0;
+            }
             SPN_TRY(G::nt(g, s));
         }
         h = dst;
@@ -1317,6 +1334,7 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     using G = Gemms<T>;
     using NT = typename G::NT;
     constexpr bool BF = std::is_same<T, bf16>::value;
+    const bool zs = BF && g_zsave;  // the forward saved Z for the trunk layers >= 1 (forward_gemms)
     const Dims& d = c.d;
     const int64_t P = c.w.P;
     const int W = d.W, H = d.H, S = c.S;
@@ -1414,22 +1432,25 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         g.M = (int)P; g.N = W; g.K = NG;
         g.r1_a = hpre; g.r1_lda = d.HP; g.r1_v = c.pk(c.k.wsig);
         g.Dmul = buf(c.w.Db[d.L - 1]); g.ld_dmul = W;
+        if constexpr (BF) g.dmul_z = zs ? 1 : 0;
         SPN_TRY(G::nt(g, s));
         SPN_TRY(stream_dep(sd, s, s2));
     }
     // 6. trunk, top to bottom
     const T* X0 = BF ? buf(c.w.X0b) : buf(c.w.X0);
     for (int i = d.L - 1; i >= 0; --i) {
-        // dZ (buffer cur) holds dL/d(pre-activation of layer i); the side stream has it
-        const T* In = i == 0 ? X0 : buf(c.w.Hb[i - 1]);
+        // dZ (buffer cur) holds dL/d(pre-activation of layer i); the side stream has it.  The
+        // input of layer i >= 2 is saved as Z (option zsave): staged as sin(Z) by the TN
+        const bool zin = zs && i >= 2;
+        const T* In = i == 0 ? X0 : buf(zin ? c.w.Db[i - 1] : c.w.Hb[i - 1]);
         const int ldin = i == 0 ? d.K0p : W;
         const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
         if (i == d.skip)
             SPN_TRY(tn_grad<T>(c, dZ, W, W, In, W, X0, d.K0p, W, W + d.K0p, s2,
-                               {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
+                               {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
         else
             SPN_TRY(tn_grad<T>(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s2,
-                               {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}));
+                               {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
         if (d.sem && (i == 0 || i == d.skip)) {
             SPN_TRY(ray_rowsum<T>(dZ, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
         }
@@ -1445,6 +1466,7 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
             NT g;
             g.A = dZ; g.lda = W; g.K1 = W; g.B = G::w(c, c.k.WTt[i], BF ? c.k.WTt16[i] : -1); g.ldb = W; g.C = dzb[nxt];
             g.ldc = W; g.M = (int)P; g.N = W; g.K = W; g.Dmul = buf(c.w.Db[i - 1]); g.ld_dmul = W;
+            if constexpr (BF) g.dmul_z = zs && i >= 2;   // Db[i - 1] holds Z for layers >= 1
             SPN_TRY(G::nt(g, s));
             SPN_TRY(stream_dep(sd, s, s2));
             cur = nxt;
@@ -1539,6 +1561,7 @@ static int* option_slot(const char* name) {
     if (n == "bwd_streams") return &g_bwd_streams;
     if (n == "tn_bf16_min_points") return &g_tn16_min_points;
     if (n == "fused_heads") return &g_fused_heads;
+    if (n == "zsave") return &g_zsave;
     return nullptr;
 }
 

@@ -8,8 +8,8 @@ namespace spn {
 constexpr int kTrunkMaxL = 16;
 
 // fc_net layers 1 .. L-1 over P points: H1 (layer-0 output, [P][512] bf16) in, the output of
-// layer i to Hs[i] and its derivative cos(z) to Ds[i] where non-null (the last layer's Hs is
-// required).  The skip layer reads [H | X0b] and adds the per-ray rows rb_skip[p / S].
+// layer i to Hs[i] and its derivative cos(z) (with zround: Z itself) to Ds[i] where non-null
+// (the last layer's Hs is required).  The skip layer reads [H | X0b] and adds the per-ray rows rb_skip[p / S].
 // With X0 set, layer 0 runs in the same launch instead (H1 unused): its input is the fp32
 // encoding X0 [P][K0p], split in LDS into the bf16 planes [hi | lo | hi | lo] against the
 // weights' [hi | hi | lo | lo] (Wf[0], K = 4·K0p), w0 = 30, per-ray rows rb0[p / S]; the skip
@@ -27,6 +27,9 @@ struct TrunkArgs {
     int64_t P = 0;
     int S = 1, L = 0, skip = -1, K0p = 0;
     int dbg = 0;  // set from g_trunk_dbg by trunk_bf16
+    // layers >= 1 (w0 = 1): H = sin(Z), Z = the pre-activation rounded to fp16; when saving, Ds[i]
+    // receives Z as fp16 (consumers recompute cos(Z) and sin(Z)) and Hs[i] may be null
+    int zround = 0;
 };
 
 // Offset (bf16 elements) of W[n][k] of a [512][Kp] layer in MFMA A-fragment order: wave w =

@@ -262,8 +262,9 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             bf16* Ds = ka->Ds[i];
             const float* rb = i == 0 ? g.rb0 : (skip ? g.rb_skip : nullptr);
             const float w0 = i == 0 ? 30.f : 1.f;  // SIREN w0 of fc_net.0 (×1 elsewhere: exact)
-            // kpass 0: cos into the image (TMt = 128 when saving: it leaves between two
-            // barriers); 1: sin into the image; 2: sin into the image and cos into the D image
+            const bool zr = g.zround && i >= 1;     // block-uniform: Z = fp16(v), the D slot gets Z
+            // kpass 0: cos (or Z) into the image (TMt = 128 when saving: it leaves between two
+            // barriers); 1: sin into the image; 2: sin into the image and cos (or Z) into the D image
             auto epilogue = [&](auto kpass) {
                 constexpr int pass = decltype(kpass)::value;
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
@@ -288,13 +289,26 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                             float y[4], c[4];
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
-                                const float x = w0 * v[e];
-                                if (pass == 2) fast_sincos(x, &y[e], &c[e]);
-                                else y[e] = pass ? fast_sin(x) : w0 * fast_cos(x);
-                                if (pass == 2) c[e] *= w0;
+                                const float z = zr ? zr16(v[e]) : v[e];
+                                const float x = w0 * z;
+                                if (pass == 2) {
+                                    fast_sincos(x, &y[e], &c[e]);
+                                    c[e] = zr ? z : w0 * c[e];
+                                } else if (pass == 1) {
+                                    y[e] = fast_sin(x);
+                                } else {
+                                    y[e] = zr ? z : w0 * fast_cos(x);
+                                }
                             }
-                            *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
-                            if (pass == 2) *reinterpret_cast<u32x2*>(smem + IMG + o) = u32x2{pack2(c[0], c[1]), pack2(c[2], c[3])};
+                            // Z (zr: into the D image, or into the image by pass 0) is stored as fp16
+                            if (pass == 0 && zr)
+                                *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2_f16(y[0], y[1]), pack2_f16(y[2], y[3])};
+                            else
+                                *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                            if (pass == 2) {
+                                if (zr) *reinterpret_cast<u32x2*>(smem + IMG + o) = u32x2{pack2_f16(c[0], c[1]), pack2_f16(c[2], c[3])};
+                                else *reinterpret_cast<u32x2*>(smem + IMG + o) = u32x2{pack2(c[0], c[1]), pack2(c[2], c[3])};
+                            }
                         }
                         __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
                     }

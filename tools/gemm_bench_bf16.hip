@@ -138,6 +138,114 @@ static void check_nt(int M, int N, int K, int K1, bool sine, bool timing) {
     CK(hipFree(C)); CK(hipFree(D)); CK(hipFree(dbias));
 }
 
+// saved-Z trunk layers (option zsave): Z stored as fp16 bits; forward zround + dout_z, backward
+// dmul_z (x cos(Z)) and TN b_sin (B staged as bf16(sin(Z)))
+struct ZMat {
+    int rows, cols;
+    std::vector<float> h;  // fp16-rounded values
+    bf16* d = nullptr;     // fp16 bits
+    ZMat(int r, int c, float scale, unsigned seed) : rows(r), cols(c), h((size_t)r * c) {
+        srand(seed);
+        std::vector<uint16_t> raw(h.size());
+        for (size_t i = 0; i < h.size(); ++i) {
+            const _Float16 z = (_Float16)(scale * (2.f * (float)rand() / (float)RAND_MAX - 1.f));
+            h[i] = (float)z;
+            raw[i] = __builtin_bit_cast(uint16_t, z);
+        }
+        CK(hipMalloc(&d, raw.size() * 2));
+        CK(hipMemcpy(d, raw.data(), raw.size() * 2, hipMemcpyHostToDevice));
+    }
+    float at(int r, int c) const { return h[(size_t)r * cols + c]; }
+};
+
+static void check_z(int M) {
+    const int N = 512, K = 512;
+    HMat A(M, K, 1.f, 11), B(N, K, 0.1f, 12);
+    ZMat Z(M, N, 3.f, 13);
+    bf16 *C, *D;
+    CK(hipMalloc(&C, (size_t)M * N * 2));
+    CK(hipMalloc(&D, (size_t)M * N * 2));
+    for (int v : {1, 5, 8}) {
+        NT16Args g;
+        g.A = A.d; g.lda = K; g.K1 = K; g.B = B.d; g.ldb = K; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K;
+        g.Dmul = Z.d; g.ld_dmul = N; g.dmul_z = 1;
+        if (gemm_nt_bf16(g, 0, v) != 0) { printf("launch refused\n"); fails++; return; }
+        CK(hipDeviceSynchronize());
+        auto c = dl16(C, (size_t)M * N);
+        double worst = 0;
+        for (int s = 0; s < 128; ++s) {
+            const int r = (int)((int64_t)s * 7919 % M);
+            for (int n = 0; n < N; ++n) {
+                double acc = 0;
+                for (int k = 0; k < K; ++k) acc += (double)A.at(r, k) * B.at(n, k);
+                worst = std::max(worst, std::fabs(acc * std::cos((double)Z.at(r, n)) - c[(size_t)r * N + n]));
+            }
+        }
+        const bool ok = worst < 2e-2;
+        if (!ok) fails++;
+        printf("nt%d dmul_z  M=%d max|err| %.2e  %s\n", v, M, worst, ok ? "ok" : "FAIL");
+        // forward: zround + dout_z (w0 = 1)
+        NT16Args f;
+        f.A = A.d; f.lda = K; f.K1 = K; f.B = B.d; f.ldb = K; f.C = C; f.ldc = N; f.M = M; f.N = N; f.K = K;
+        f.act = 1; f.w0 = 1.f; f.Dout = D; f.ld_dout = N; f.zround = 1; f.dout_z = 1;
+        if (gemm_nt_bf16(f, 0, v) != 0) { printf("launch refused\n"); fails++; return; }
+        CK(hipDeviceSynchronize());
+        auto cc = dl16(C, (size_t)M * N);
+        std::vector<uint16_t> dz((size_t)M * N);
+        CK(hipMemcpy(dz.data(), D, dz.size() * 2, hipMemcpyDeviceToHost));
+        double wc = 0, wz = 0;
+        for (int s = 0; s < 128; ++s) {
+            const int r = (int)((int64_t)s * 7919 % M);
+            for (int n = 0; n < N; ++n) {
+                double acc = 0;
+                for (int k = 0; k < K; ++k) acc += (double)A.at(r, k) * B.at(n, k);
+                const float zf = (float)(_Float16)(float)acc;
+                const float got = (float)__builtin_bit_cast(_Float16, dz[(size_t)r * N + n]);
+                wz = std::max(wz, std::fabs((double)zf - got) / std::max(1.0, std::fabs(acc)));
+                wc = std::max(wc, std::fabs(std::sin((double)got) - cc[(size_t)r * N + n]));
+            }
+        }
+        const bool okf = wz < 2e-3 && wc < 8e-3;
+        if (!okf) fails++;
+        printf("nt%d zround  M=%d max|err| Z %.2e  sin(Z) %.2e  %s\n", v, M, wz, wc, okf ? "ok" : "FAIL");
+    }
+    CK(hipFree(C)); CK(hipFree(D));
+    // TN with B = Z (b_sin)
+    const int P = M;
+    HMat Ad(P, N, 1.f, 14);
+    ZMat Zb(P, K, 3.f, 15);
+    for (int tv : {1, 2}) {
+        g_tn16_variant = tv;
+        const int sp = tn_splits_bf16(P, N, K);
+        float *slab, *slab_b, *dW;
+        CK(hipMalloc(&slab, (size_t)sp * N * K * 4));
+        CK(hipMalloc(&slab_b, (size_t)sp * N * 4));
+        CK(hipMalloc(&dW, (size_t)N * K * 4));
+        TN16Args t;
+        t.A = Ad.d; t.lda = N; t.B = Zb.d; t.ldb = K; t.K1 = K; t.b_sin = 1;
+        t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K; t.slab_b = slab_b; t.P = P; t.N = N; t.K = K;
+        ReduceArgs r;
+        r.slab = slab; r.ld_slab = K; r.slab_stride = t.slab_stride; r.splits = sp; r.N = N; r.slab_b = slab_b;
+        r.row0 = 0; r.nrows = N; r.ncols = K; r.dst = dW; r.ld_dst = K; r.dst_b = nullptr;
+        if (gemm_tn_bf16(t, sp, 0) != 0 || reduce_slabs(r, 0) != 0) { printf("launch refused\n"); fails++; return; }
+        CK(hipDeviceSynchronize());
+        std::vector<float> w((size_t)N * K);
+        CK(hipMemcpy(w.data(), dW, w.size() * 4, hipMemcpyDeviceToHost));
+        double worst = 0, scale = std::sqrt((double)P);
+        for (int s = 0; s < 512; ++s) {
+            const int n = (int)((int64_t)s * 131 % N), k = (int)((int64_t)s * 977 % K);
+            double acc = 0;
+            for (int p = 0; p < P; ++p) acc += (double)Ad.at(p, n) * bfr(std::sin(Zb.at(p, k)));
+            worst = std::max(worst, std::fabs(acc - w[(size_t)n * K + k]) / scale);
+        }
+        const bool ok = worst < 2e-3;  // bf16(sin) on the device's v_sin vs libm: ulp-level differences
+        if (!ok) fails++;
+        printf("tn%d b_sin  P=%d max|err|/sqrt(P) %.2e  %s\n", tv, P, worst, ok ? "ok" : "FAIL");
+        CK(hipFree(slab)); CK(hipFree(slab_b)); CK(hipFree(dW));
+    }
+    g_tn16_variant = 2;
+}
+
 // dW[n][k] = Σ_p A[p][n] B[p][k], B = [B1 | B2] split at K1; bias[n] = Σ_p A[p][n]
 static void check_tn(int P, int N, int K, int K1, bool timing) {
     HMat A(P, N, 1.f, 5), B1(P, K1, 1.f, 6), B2(P, std::max(8, K - K1), 1.f, 7);
@@ -202,6 +310,12 @@ int main(int argc, char** argv) {
             check_tn(P, 256, 256, 256, true);
             check_tn(P, 512, 576, 512, true);
         }
+        printf("%s\n", fails ? "SOME CHECKS FAILED" : "all checks ok");
+        return fails ? 1 : 0;
+    }
+    if (argc > 3 && !strcmp(argv[3], "z")) {  // saved-Z epilogues / staging only
+        check_z(4100);
+        check_z(20000);
         printf("%s\n", fails ? "SOME CHECKS FAILED" : "all checks ok");
         return fails ? 1 : 0;
     }
