@@ -42,6 +42,7 @@ struct TN16Args {
     int P = 0, N = 0, K = 0;
     int p_per_split = 0;  // set by gemm_tn_bf16
     int b_sin = 0;        // B's columns [0, K1) hold a saved Z (fp16): staged as bf16(sin(Z)) (= the layer's H)
+    int dbg = 0;          // ablations (tools only; wide tiles): 1 = no MFMAs
 };
 
 // variant: prefetch depth in K-steps (1 or 2); <= 0 = library default (g_nt16_variant)

@@ -969,7 +969,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
         for (int st = 0; st < ns; ++st) {
             gload(p_beg + 64 * (st + 1));
             __builtin_amdgcn_sched_barrier(0);
-            compute(st & 1);
+            if (!(g.dbg & 1)) compute(st & 1);
             __builtin_amdgcn_sched_barrier(0);
             sstore((st + 1) & 1);
             __syncthreads();
@@ -1144,7 +1144,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES);
-            compute(st % TD_STAGES);
+            if (!(g.dbg & 1)) compute(st % TD_STAGES);
             if (do_bias) bias_rows(st % TD_STAGES);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 // host
 // ------------------------------------------------------------------------------------------
 int g_nt16_variant = 8;
-int g_tn16_variant = 2;
+int g_tn16_variant = 3;
 
 static bool tn_wide(int N, int K, int variant) {
     const int v = variant > 0 ? variant : g_tn16_variant;

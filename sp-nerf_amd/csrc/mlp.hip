@@ -1000,11 +1000,38 @@ struct Gemms<bf16> {
     static int32_t tn(const TN& a, int sp, hipStream_t s) { return gemm_tn_bf16(a, sp, s); }
 };
 
+int g_tn_split_tail = 1;  // option "tn_split_tail": see tn_grad
+
 template <typename T>
 static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int ldb, const T* B2, int ldb2, int K1,
-                       int K, hipStream_t s, std::initializer_list<ReduceArgs> outs, bool b_sin = false) {
+                       int K, hipStream_t s, const std::vector<ReduceArgs>& outs, bool b_sin = false) {
     using G = Gemms<T>;
     const int P = (int)c.w.P;
+    // bf16 skip layer ([H | x0], K = 512 + K0p): the K = 576 GEMM has no 256-wide tiling and ran
+    // on the 128x128 kernel at 710 us per 524 288 points; split into the wide K = 512 part and
+    // the K0p tail (two passes over dZ, the tail's slab reduced into columns K1..) it is ≈470.
+    // Below 2^18 points the single launch is as fast
+    bool split = std::is_same<T, bf16>::value && g_tn_split_tail && B2 && K > K1 && P >= (1 << 18) &&
+                 N % 256 == 0 && K1 % 256 == 0 && (N / 256) * (K1 / 256) >= 4;
+    for (const ReduceArgs& r : outs) split = split && !r.transpose;
+    if (split) {
+        std::vector<ReduceArgs> head, tail;
+        for (ReduceArgs r : outs) {
+            ReduceArgs h = r;
+            h.ncols = std::min(r.ncols, K1);
+            head.push_back(h);
+            if (r.ncols > K1) {
+                ReduceArgs t = r;
+                t.dst = r.dst + K1;
+                t.ncols = r.ncols - K1;
+                t.dst_b = nullptr;  // the column sums come with the head
+                tail.push_back(t);
+            }
+        }
+        SPN_TRY(tn_grad<T>(c, A, lda, N, B, ldb, nullptr, 0, K1, K1, s, head, b_sin));
+        if (!tail.empty()) SPN_TRY(tn_grad<T>(c, A, lda, N, B2, ldb2, nullptr, 0, K - K1, K - K1, s, tail));
+        return SPNERF_OK;
+    }
     const int splits = G::splits(P, N, K);
     typename G::TN t;
     t.A = A; t.lda = lda;
@@ -1562,6 +1589,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_min_points") return &g_tn16_min_points;
     if (n == "fused_heads") return &g_fused_heads;
     if (n == "zsave") return &g_zsave;
+    if (n == "tn_split_tail") return &g_tn_split_tail;
     return nullptr;
 }
 

@@ -58,14 +58,13 @@ def test_fp32_gemm_variants_bitwise_equal(opts):
         assert torch.equal(g0[k], g1[k]), (opts, k)
 
 
-def _render_bf16(opts):
+def _render_bf16(opts, n=300):
     old = {k: _lib.get_option(k) for k in opts}
     for k, v in opts.items():
         _lib.set_option(k, v)
     try:
         args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
                                         sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
-        n = 300
         rays = torch.tensor(gu_rays(n, 22), device=DEV)
         g = torch.Generator(device="cpu").manual_seed(5)
         kw = dict(valid_depth=(torch.rand(n, generator=g) < 0.7).long().to(DEV),
@@ -99,5 +98,19 @@ def test_bf16_tn_tilings_agree(variant):
     assert sorted(g1) == sorted(g2)
     for k in g1:
         assert torch.isfinite(g2[k]).all(), k
+        scale = g1[k].abs().max().item()
+        assert (g1[k] - g2[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
+
+
+def test_bf16_skip_layer_tail_split_agrees():
+    """The skip layer's weight gradient ([H | x0], K = 512 + K0p) at >= 2^18 points runs as the
+    wide K = 512 GEMM plus the K0p tail (option tn_split_tail): gradients within 1e-4 of the
+    single-launch 128x128 tiling's (different point splits: fp32 summation-order noise), renders
+    bit-identical."""
+    r1, g1 = _render_bf16({"tn_split_tail": 0}, n=2048)
+    r2, g2 = _render_bf16({"tn_split_tail": 1}, n=2048)
+    for k in r1:
+        assert torch.equal(r1[k], r2[k]), k
+    for k in g1:
         scale = g1[k].abs().max().item()
         assert (g1[k] - g2[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k

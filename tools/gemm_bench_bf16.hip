@@ -286,6 +286,10 @@ static void check_tn(int P, int N, int K, int K1, bool timing) {
         const double us = time_it([&] { gemm_tn_bf16(t, sp, 0); });
         const double usr = time_it([&] { reduce_slabs(r, 0); });
         printf("   %8.1f us %7.1f TF/s (+ reduce %.1f us)", us, 2.0 * P * N * K / us * 1e-6, usr);
+        t.dbg = 1;
+        const double un = time_it([&] { gemm_tn_bf16(t, sp, 0); });
+        t.dbg = 0;
+        printf("  [no MFMA %.1f us]", un);
     }
     printf("\n");
     CK(hipFree(slab)); CK(hipFree(slab_b)); CK(hipFree(dW)); CK(hipFree(db));
