@@ -481,7 +481,10 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 #endif
 // DM: the backward dX epilogue only (C = acc · Dmul, no bias / rank-1 / sine): every epilogue
 // load is unconditional, so no branch drains the in-flight DMAs (vmcnt(0)).
-template <bool DM>
+// IP: issue placement of the next K-step's DMAs, as k_gemm_tn_bf16d (option nt_bf16_ip; the
+// backward xDmul epilogue only, 2 by default: 536 -> 429 us on 524 288 x 512 x 512 in isolation,
+// within noise in the C4 step)
+template <bool DM, int IP = 0>
 __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
     __shared__ __attribute__((aligned(16))) char smem[ND_STAGES * ND_STG + 8 * 4096];
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
 
     f32x16 acc[MI][NJ];
     const int wr = wid >> 2, wc = wid & 3, r32 = lane & 31, h = lane >> 5;
-    auto compute = [&](int stg) {
+    auto compute = [&](int stg, auto&& mid) {
         const int swz = (r32 >> 2) & 3;
         const char* sA = smem + stg * ND_STG + (wr * 128 + r32) * 64;
         const char* sB = smem + stg * ND_STG + (256 + wc * 64 + r32) * 64;
@@ -541,6 +544,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             for (int i = 0; i < MI; ++i)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+            if (ks == 0) mid();
         }
     };
 
@@ -574,9 +578,16 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             ND_STAMP(1);
             __builtin_amdgcn_s_barrier();
             ND_STAMP(2);
-            issue((gs + 3) % ND_STAGES);
-            ND_STAMP(3);
-            if (!(g.dbg & 1)) compute(gs % ND_STAGES);
+            if constexpr (IP == 2) {  // the next step's DMAs between this step's two k-halves
+                compute(gs % ND_STAGES, [&] { issue((gs + 3) % ND_STAGES); });
+            } else if constexpr (IP == 1) {  // after this step's MFMAs
+                compute(gs % ND_STAGES, [] {});
+                issue((gs + 3) % ND_STAGES);
+            } else {
+                issue((gs + 3) % ND_STAGES);
+                ND_STAMP(3);
+                if (!(g.dbg & 1)) compute(gs % ND_STAGES, [] {});
+            }
         }
         ND_STAMP(4);
         if (g.dbg & 2) {
@@ -1013,6 +1024,10 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
 // only when every split holds whole 32-point steps (P % 32 == 0).  Bias sums are read back from
 // the landed stage (k0 == 0 blocks only).
 constexpr int TD_STEP = 32, TD_STAGES = 4, TD_STG = 4 * TD_STEP * 256;  // bytes per stage
+// IP: where a step issues the next DMA step: 0 = before its MFMAs, 1 = after them, 2 = between
+// its two k-halves (default, option tn_bf16_ip: a wave stalled on the DMA issue then has MFMAs
+// in flight; 393 -> 365 us on 524 288 x 512 x 512, C4 TN 7.18 -> 6.81 ms/step)
+template <int IP>
 __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
     __shared__ __attribute__((aligned(16))) char smem[TD_STAGES * TD_STG];  // [stage][A0|A1|B0|B1]
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -1085,7 +1100,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
         return __builtin_bit_cast(bf16x8, v);
     };
     constexpr int HALF = TD_STEP * 256;
-    auto compute = [&](int stg) {
+    auto compute = [&](int stg, auto&& mid) {
         const char* sA = smem + stg * TD_STG + wa * HALF;
         const char* sB = smem + stg * TD_STG + (2 + (wb >> 1)) * HALF;
         const int cb = (wb & 1) * 64;
@@ -1118,6 +1133,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+            if (ks == 0) mid();
         }
     };
     // bias: thread (chunk ch of 32, row phase lrow of 16) sums rows lrow, lrow + 16 of each step
@@ -1143,8 +1159,16 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
             // barrier publishes every wave's DMAs and retires step st-1's reads of stage (st+3)%4
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             __builtin_amdgcn_s_barrier();
-            issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES);
-            if (!(g.dbg & 1)) compute(st % TD_STAGES);
+            auto nxt = [&] { issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES); };
+            if constexpr (IP == 2) {
+                compute(st % TD_STAGES, nxt);
+            } else if constexpr (IP == 1) {
+                compute(st % TD_STAGES, [] {});
+                nxt();
+            } else {
+                nxt();
+                if (!(g.dbg & 1)) compute(st % TD_STAGES, [] {});
+            }
             if (do_bias) bias_rows(st % TD_STAGES);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
@@ -1183,6 +1207,8 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 // host
 // ------------------------------------------------------------------------------------------
 int g_nt16_variant = 8;
+int g_nt16_ip = 2;  // DMA NT / TN: where a K-step issues the next step's DMAs (0 before its MFMAs, 1 after, 2 between the k-halves)
+int g_tn16_ip = 2;
 int g_tn16_variant = 3;
 
 static bool tn_wide(int N, int K, int variant) {
@@ -1218,7 +1244,10 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     if (v == 8) {
         const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
         const bool dm = a.Dmul && !a.bias && !a.rowbias && !a.r1_a && a.act == 0 && !a.Dout;
-        if (dm) hipLaunchKernelGGL(k_gemm_nt_bf16d<true>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        const int ip = (a.dbg & 64) ? 2 : (a.dbg & 32) ? 1 : g_nt16_ip;
+        if (dm && ip == 2) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else if (dm && ip == 1) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else if (dm) hipLaunchKernelGGL(k_gemm_nt_bf16d<true>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else hipLaunchKernelGGL(k_gemm_nt_bf16d<false>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         SPN_HIP(hipGetLastError());
         return SPNERF_OK;
@@ -1274,7 +1303,12 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
         const int nb = cdiv(a.N, TW) * cdiv(a.K, TW);
         const int v = g_tn16_variant;
         if (v == 3 && a.P % TD_STEP == 0 && !a.b_sin)  // DMA: whole 32-point steps, B staged as is
-            hipLaunchKernelGGL(k_gemm_tn_bf16d, dim3(nb * splits), dim3(512), 0, s, a);
+        {
+            const int ip = (a.dbg & 4) ? 2 : (a.dbg & 2) ? 1 : g_tn16_ip;
+            if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, dim3(nb * splits), dim3(512), 0, s, a);
+            else if (ip == 1) hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, dim3(nb * splits), dim3(512), 0, s, a);
+            else hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, dim3(nb * splits), dim3(512), 0, s, a);
+        }
         else
             hipLaunchKernelGGL(k_gemm_tn_bf16w, dim3(nb * splits), dim3(512), 0, s, a);
     } else {

@@ -288,8 +288,12 @@ static void check_tn(int P, int N, int K, int K1, bool timing) {
         printf("   %8.1f us %7.1f TF/s (+ reduce %.1f us)", us, 2.0 * P * N * K / us * 1e-6, usr);
         t.dbg = 1;
         const double un = time_it([&] { gemm_tn_bf16(t, sp, 0); });
+        t.dbg = 2;
+        const double ua = time_it([&] { gemm_tn_bf16(t, sp, 0); });
+        t.dbg = 4;
+        const double um = time_it([&] { gemm_tn_bf16(t, sp, 0); });
         t.dbg = 0;
-        printf("  [no MFMA %.1f us]", un);
+        printf("  [no MFMA %.1f us, DMA after %.1f, mid %.1f]", un, ua, um);
     }
     printf("\n");
     CK(hipFree(slab)); CK(hipFree(slab_b)); CK(hipFree(dW)); CK(hipFree(db));
@@ -363,9 +367,10 @@ int main(int argc, char** argv) {
         NT16Args gd = g;
         gd.bias = nullptr; gd.act = 0; gd.Dout = nullptr; gd.Dmul = Dm.d; gd.ld_dmul = 512;
         const char* an[] = {"dmul full", "no MFMA", "no epilogue", "no MFMA+epi", "no DMA wait", "no wait+MFMA+epi",
-                            "A only", "A only no MFMA+epi", "A only no epi", "A only no MFMA"};
-        const int ad[] = {0, 1, 2, 3, 4, 7, 16, 19, 18, 17};
-        for (int i = 0; i < 10; ++i) {
+                            "A only", "A only no MFMA+epi", "A only no epi", "A only no MFMA", "DMA after MFMAs",
+                            "DMA mid MFMAs"};
+        const int ad[] = {0, 1, 2, 3, 4, 7, 16, 19, 18, 17, 32, 64};
+        for (int i = 0; i < 12; ++i) {
             gd.dbg = ad[i];
             const double us = time_it([&] { gemm_nt_bf16(gd, 0, 8); });
             printf("nt8 ablation %-18s %8.1f us\n", an[i], us);
