@@ -47,8 +47,9 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6    # dense bf16 = 16 x the f32 MFMA rate (MI355X_
 HBM_PEAK_GBS = 8000.0
 GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt_w (fp32 MFMA, 256x128 persistent tiles, 2 blocks/CU, LDS-DMA)", FP32_MFMA_PEAK_TFLOPS),
                 "gemm_tn_f32": ("k_gemm_tn (fp32 MFMA, weight gradients)", FP32_MFMA_PEAK_TFLOPS),
-                "gemm_nt_bf16": ("k_gemm_nt_bf16w (bf16 MFMA, 256x256 persistent tiles)", BF16_MFMA_PEAK_TFLOPS),
-                "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA, weight gradients)", BF16_MFMA_PEAK_TFLOPS),
+                "gemm_nt_bf16": ("k_gemm_nt_bf16d (bf16 MFMA, 256x256 persistent tiles, LDS-DMA ring across tiles)",
+                                 BF16_MFMA_PEAK_TFLOPS),
+                "gemm_tn_bf16": ("k_gemm_tn_bf16d (bf16 MFMA, weight gradients, LDS-DMA)", BF16_MFMA_PEAK_TFLOPS),
                 "trunk_bf16": ("k_trunk_bf16 (fused bf16 trunk, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
                 "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS)}
 

@@ -114,19 +114,7 @@ __global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, co
     if (i >= P * K0p) return;
     const int64_t p = i / K0p;
     const int c = (int)(i % K0p);
-    float v = 0.f;
-    if (c < K0) {
-        const float* ray = rays + (p / S) * rs;
-        const float zz = z[p];
-        if (n_freq == 0) {
-            v = __fadd_rn(ray[c], __fmul_rn(ray[dir_off + c], zz));
-        } else {
-            const int k = c / 6, j = c % 6, dim = j % 3;
-            const float x = __fadd_rn(ray[dim], __fmul_rn(ray[dir_off + dim], zz));
-            const float arg = __fmul_rn((float)(1 << k), x);
-            v = j < 3 ? sinf(arg) : cosf(arg);
-        }
-    }
+    const float v = c < K0 ? pe_value(rays + (p / S) * rs, dir_off, z[p], c, n_freq, K0) : 0.f;
     if (X0) X0[i] = v;
     const bf16 hi = (bf16)v;
     if (X0b) X0b[i] = hi;
@@ -968,6 +956,10 @@ struct Ctx {
     float* ws;       // workspace base
     int S;
     int acc = 0;     // backward: gradient reductions add into the flat gradient
+    // the forward's ray inputs (the fused inference trunk encodes layer 0's input itself)
+    const float* rays = nullptr;
+    const float* z = nullptr;
+    int rs = 0, dir_off = 0;
     float* at(int64_t off) const { return ws + off; }
     const float* pk(int64_t off) const { return P + off; }
     bf16* hb(int64_t off) const { return reinterpret_cast<bf16*>(ws + off); }          // bf16 workspace buffer
@@ -1100,6 +1092,10 @@ static bool fused_trunk_on(const Ctx& c) {
 static bool heads_fused_on(const Ctx& c, bool save, int mode) {
     return !save && (mode == 0 || mode == 1) && c.d.bf && c.k.Ffeat16 >= 0 && heads_bf16_supported(c.d);
 }
+int g_pe_inline = 1;  // option "pe_inline": inference trunk with layer 0 encodes o + dir·z itself (no k_encode)
+static bool trunk_l0_on(const Ctx& c, bool save);
+static bool pe_inline_on(const Ctx& c, bool save) { return g_pe_inline && !save && trunk_l0_on(c, save); }
+
 static bool trunk_l0_on(const Ctx& c, bool save) {
     return fused_trunk_on(c) && g_l0_split && (g_trunk_l0 == 2 || (g_trunk_l0 == 1 && !save)) && c.k.Wf16[0] >= 0 &&
            trunk_l0_supported(c.d.K0p, save);
@@ -1126,7 +1122,12 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
             a.H1 = reinterpret_cast<const bf16*>(h);
             a.X0b = c.hb(c.w.X0b);
             if (first == 0) {
-                a.X0 = c.at(c.w.X0);
+                if (pe_inline_on(c, save)) {
+                    a.rays = c.rays; a.rs = c.rs; a.dir_off = c.dir_off; a.z = c.z;
+                    a.n_freq = d.K0 == 3 ? 0 : d.K0 / 6; a.K0 = d.K0;
+                } else {
+                    a.X0 = c.at(c.w.X0);
+                }
                 a.rb0 = d.sem ? c.at(c.w.rb0) : nullptr;
             }
             double ksum = 0.0;
@@ -1143,7 +1144,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
             a.zround = zs ? 1 : 0;
             // algorithmic HBM bytes: the first layer's input (fp32 PE, or H_1 and the bf16 PE)
             // in; out when saving H and D of every layer, or Z of every layer and the last H
-            const double in = first == 0 ? 4.0 * P * d.K0p : 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0));
+            const double in = first == 0 ? (a.rays ? 4.0 * P : 4.0 * P * d.K0p) : 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0));
             const double nout = !save ? 1.0 : (zs ? d.L - first + 1.0 : 2.0 * (d.L - first));
             const double bytes = in + 2.0 * P * W * nout;
             SPN_TRY(trunk_bf16(a, s, 2.0 * P * W * ksum, bytes));
@@ -1271,8 +1272,10 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
             SPN_HIP(hipGetLastError());
         }
     }
-    // positional encoding (fp32 for layer 0, plus a bf16 copy for the skip layer / dW_0)
-    {
+    // positional encoding (fp32 for layer 0, plus a bf16 copy for the skip layer / dW_0); the
+    // fused inference trunk with layer 0 computes it in its staging instead
+    c.rays = rays; c.rs = rs; c.dir_off = dir_off; c.z = z;
+    if (!pe_inline_on(c, save)) {
         const int64_t n = P * d.K0p;
         // bf16 MLP, layer 0 on bf16 planes: a separate GEMM reads the planes X0s; inside the
         // fused trunk it splits the fp32 rows itself
@@ -1591,6 +1594,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_min_points") return &g_tn16_min_points;
     if (n == "fused_heads") return &g_fused_heads;
     if (n == "zsave") return &g_zsave;
+    if (n == "pe_inline") return &g_pe_inline;
     if (n == "tn_split_tail") return &g_tn_split_tail;
     return nullptr;
 }

@@ -14,6 +14,19 @@ constexpr int kTrunkMaxL = 16;
 // encoding X0 [P][K0p], split in LDS into the bf16 planes [hi | lo | hi | lo] against the
 // weights' [hi | hi | lo | lo] (Wf[0], K = 4·K0p), w0 = 30, per-ray rows rb0[p / S]; the skip
 // layer's PE columns are the hi plane.
+// One positional-encoding value (rendering.py:147; spnerf.py:32-37): channel c of point p at
+// depth zz on ray `ray` (o at [0, 3), dir at [dir_off, dir_off + 3)); n_freq = 0: xyz itself.
+// o + dir*z as two rounded ops like the reference (no FMA contraction: sin(2^9 x) amplifies a
+// 1-ulp difference in x by 512).  k_encode and the fused trunk's inline layer-0 staging share it.
+__device__ __forceinline__ float pe_value(const float* ray, int dir_off, float zz, int c, int n_freq, int K0) {
+    if (c >= K0) return 0.f;
+    if (n_freq == 0) return __fadd_rn(ray[c], __fmul_rn(ray[dir_off + c], zz));
+    const int k = c / 6, j = c % 6, dim = j % 3;
+    const float x = __fadd_rn(ray[dim], __fmul_rn(ray[dir_off + dim], zz));
+    const float arg = __fmul_rn((float)(1 << k), x);
+    return j < 3 ? sinf(arg) : cosf(arg);
+}
+
 struct TrunkArgs {
     const bf16* H1 = nullptr;
     const bf16* X0b = nullptr;
@@ -30,6 +43,11 @@ struct TrunkArgs {
     // layers >= 1 (w0 = 1): H = sin(Z), Z = the pre-activation rounded to fp16; when saving, Ds[i]
     // receives Z as fp16 (consumers recompute cos(Z) and sin(Z)) and Hs[i] may be null
     int zround = 0;
+    // layer 0 from the rays themselves (inference, option "pe_inline"): with rays set and X0 null
+    // the staging computes the encoding of o + dir·z (pe_value) instead of reading X0 rows
+    const float* rays = nullptr;
+    const float* z = nullptr;
+    int rs = 0, dir_off = 0, n_freq = 0, K0 = 0;
 };
 
 // Offset (bf16 elements) of W[n][k] of a [512][Kp] layer in MFMA A-fragment order: wave w =

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     const int x0ch = g.K0p >> 3;
     constexpr int nmain = TW / 16;  // k-steps over the activation image
     const int ntail = g.K0p >> 4;   // extra k-steps over the PE at the skip layer
-    const bool l0 = g.X0 != nullptr;  // layer 0 in this launch (block-uniform)
+    const bool l0 = g.X0 != nullptr || g.rays != nullptr;  // layer 0 in this launch (block-uniform)
     const int first = l0 ? 0 : 1;
     const int nk0 = g.K0p >> 2;     // layer 0's k-steps: the 4·K0p split planes
     auto nks_of = [&](int i) { return i == 0 ? nk0 : nmain + (i == g.skip ? ntail : 0); };
@@ -128,12 +128,23 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             // (layer 0's B operand) and the skip layer's PE tile (= hi, as X0b)
             for (int u = st; u < TMt * x0ch; u += 512) {
                 const int row = u / x0ch, q = u % x0ch;
-                const float* src = g.X0 + std::min<int64_t>(p0 + row, g.P - 1) * g.K0p + q * 8;
-                const f32x4 v0 = ld4(src), v1 = ld4(src + 4);
+                const int64_t pr = std::min<int64_t>(p0 + row, g.P - 1);
+                float xv[8];
+                if (g.rays) {  // block-uniform: encode o + dir·z here (pe_value, as k_encode)
+                    const float* ray = g.rays + (pr / g.S) * g.rs;
+                    const float zz = g.z[pr];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) xv[e] = pe_value(ray, g.dir_off, zz, q * 8 + e, g.n_freq, g.K0);
+                } else {
+                    const float* src = g.X0 + pr * g.K0p + q * 8;
+                    const f32x4 v0 = ld4(src), v1 = ld4(src + 4);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) xv[e] = e < 4 ? v0[e] : v1[e - 4];
+                }
                 float hf[8], lf[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    const float x = e < 4 ? v0[e] : v1[e - 4];
+                    const float x = xv[e];
                     hf[e] = (float)(bf16)x;
                     lf[e] = x - hf[e];
                 }
@@ -363,7 +374,8 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     bool save = false;
     for (int i = 1; i < a.L; ++i) save |= a.Ds[i] != nullptr;
     const int tm = trunk_tile(save);
-    SPN_ARG(!a.X0 || (a.Wf[0] && trunk_l0_supported(a.K0p, save)), "trunk_bf16: layer 0 unsupported for K0p=%d",
+    SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0 && !save), "trunk_bf16: inline encoding needs z, rs, inference");
+    SPN_ARG(!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, save)), "trunk_bf16: layer 0 unsupported for K0p=%d",
             a.K0p);
     TrunkArgs ad = a;
     ad.dbg = g_trunk_dbg;

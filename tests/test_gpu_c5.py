@@ -141,3 +141,31 @@ def test_fused_inference_heads_match_layer_by_layer_heads(sem):
         e = gu.rel_err(a, b)
         print(k, f"{e:.2e}")
         assert e < 2e-3, (k, e)
+
+
+def test_inline_encoding_bit_identical():
+    """The fused inference trunk encodes o + dir·z itself when it runs layer 0 (option pe_inline,
+    no k_encode launch, no [P][64] fp32 PE round trip): the same pe_value arithmetic as k_encode,
+    so every output is bit-identical to the k_encode path, with and without the semantic head."""
+    from spnerf_amd import _lib
+    from oracle.weights import ModelDims
+    g = torch.Generator(device="cpu").manual_seed(9)
+    B, S = 2000, 128
+    rays = torch.tensor(gu.synthetic_rays(B, 23), device=DEV)
+    u = torch.rand(B, S, generator=g).to(DEV)
+    labels = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    args = gu.args_of({"args": dict(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                                    sc_lambda=0.0, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+    for sem in (True, False):
+        model = make_model(ModelDims(width=512, sem=sem), 8, "bf16")
+        outs = []
+        try:
+            for inline in (1, 0):
+                _lib.set_option("pe_inline", inline)
+                with torch.no_grad(), random_source(FixedU(u)):
+                    outs.append(spnerf_amd.render_rays({"coarse": model}, args, rays, None,
+                                                       semantics=labels if sem else None, mode="test"))
+        finally:
+            _lib.set_option("pe_inline", 1)
+        for k in outs[1]:
+            assert torch.equal(outs[0][k], outs[1][k]), (sem, k)

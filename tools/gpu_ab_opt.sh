@@ -1,7 +1,9 @@
-# C4 default line under library options: bash tools/gpu_ab_opt.sh "zsave=0" "zsave=1" ...
+# Bench line under library options: bash tools/gpu_ab_opt.sh "zsave=0" "zsave=1" ...
+# (CONFIG=c5 for the inference line; default the C4 training line)
 cd $GRAFT_REPO_ROOT
+CONFIG=${CONFIG:-c4}
 for o in "$@"; do
 args=""; for kv in $o; do args="$args --option $kv"; done
-r=$(timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-secondary $args 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']; print(round(d['ms_per_step'],3), round(d['value']/1e6,2), 'trunk', round(k['trunk_bf16']['ms_per_step'],2), 'nt', round(k['gemm_nt_bf16']['ms_per_step'],2), 'tn', round(k['gemm_tn_bf16']['ms_per_step'],2), 'frac', round(d['roofline']['frac'],3))")
-echo "c4 [$o] ms,Msps=$r"
+r=$(timeout -k 10 200 python bench.py --config $CONFIG --steps 20 --warmup 5 --no-cpu-baseline --no-secondary $args 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernels', {}); print(round(d['ms_per_step'],3), round(d['value']/1e6,2), {c: round(v['ms_per_step'],2) for c, v in k.items() if v['ms_per_step'] > 0.2}, 'frac', round(d['roofline']['frac'],3), 'mlp', round(d.get('mlp_gemms', {}).get('frac', 0),3))")
+echo "$CONFIG [$o] ms,Msps=$r"
 done

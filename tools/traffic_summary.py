@@ -13,7 +13,8 @@ src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_bench"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r02"
 CFGS = sys.argv[3:] or ["c4", "c5"]
 CLASSES = {"k_gemm_nt<": "gemm_nt_f32", "k_gemm_nt_w<": "gemm_nt_f32", "k_gemm_tn<": "gemm_tn_f32",
-           "k_gemm_nt_bf16": "gemm_nt_bf16", "k_gemm_tn_bf16": "gemm_tn_bf16", "k_trunk_bf16": "trunk_bf16"}
+           "k_gemm_nt_bf16": "gemm_nt_bf16", "k_gemm_tn_bf16": "gemm_tn_bf16", "k_trunk_bf16": "trunk_bf16",
+           "k_heads_bf16": "heads_fused", "k_composite_fwd": "composite_fwd"}
 for cfg in CFGS:
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -26,7 +27,7 @@ for cfg in CFGS:
                 names[d] = r["Kernel_Name"]
             for d, v in per.items():
                 for key, cls in CLASSES.items():
-                    if key in names[d] and not ("bf16" in names[d] and "bf16" not in cls):
+                    if key in names[d] and not ("bf16" in names[d] and cls.endswith("_f32")):
                         acc[cls][ctr].append(v)
     out = {}
     for cls, c in acc.items():
