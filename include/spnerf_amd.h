@@ -163,6 +163,22 @@ int32_t spnerf_rpc_rays(const double* rpc, double downscale, double min_alt, dou
                         const float* center, float range, const float* sun, float* rays, int32_t ray_stride,
                         void* stream);
 
+/* ---- DSM extraction from a rendered depth (datasets/satellite_scene.py:475-568,
+ *      modules/utils.py:103-139).  spnerf_dsm_points: per ray, x = o + d·depth (normalised scene,
+ *      rays of stride rs >= 6), denormalised by `range` and the 3 host doubles `center` to ECEF,
+ *      then lat / lon (degrees) / alt by the reference's ecef_to_latlon_custom into lla[n][3] and
+ *      UTM easting / northing / alt (WGS-84, `utm_zone`, `south`; Krüger series — pyproj is not
+ *      available: parity unpinned) into ena[n][3]; either output may be NULL.
+ *      spnerf_dsm_rasterize: plyflatten(cloud, xoff, yoff, resolution, xsize, ysize, radius,
+ *      sigma) restated (parity unpinned): dsm[ysize][xsize] = weighted mean altitude of the
+ *      points whose (2·radius+1)² window covers the cell, NaN where none; sigma = +inf for plain
+ *      means; acc = 2·xsize·ysize doubles of device workspace. */
+int32_t spnerf_dsm_points(const float* rays, int32_t rs, int64_t n, const float* depth, const double* center,
+                          double range, int32_t utm_zone, int32_t south, double* lla, double* ena, void* stream);
+int32_t spnerf_dsm_rasterize(const double* ena, int64_t n, double xoff, double yoff, double resolution,
+                             int32_t xsize, int32_t ysize, int32_t radius, double sigma, double* acc, double* dsm,
+                             void* stream);
+
 /* ---- kernel selection (no reference counterpart: A/B switches for tests and benches) ----
  *      "fused_trunk" (1 = bf16 trunk layers 1..L-1 in one persistent LDS-resident launch,
  *      the default; 0 = layer by layer), "nt_f32_variant", "tn_f32_variant",

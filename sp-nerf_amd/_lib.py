@@ -66,6 +66,10 @@ SIGNATURES = {
     "spnerf_rpc_rays": (c_int32, [POINTER(c_double), c_double, c_double, c_double, c_int32, c_int32, c_int32, c_int32,
                                   c_void_p, c_int64, POINTER(c_float), c_float, POINTER(c_float), c_void_p, c_int32,
                                   c_void_p]),
+    "spnerf_dsm_points": (c_int32, [c_void_p, c_int32, c_int64, c_void_p, POINTER(c_double), c_double, c_int32, c_int32,
+                                    c_void_p, c_void_p, c_void_p]),
+    "spnerf_dsm_rasterize": (c_int32, [c_void_p, c_int64, c_double, c_double, c_double, c_int32, c_int32, c_int32,
+                                       c_double, c_void_p, c_void_p, c_void_p]),
     "spnerf_set_option": (c_int32, [c_char_p, c_int32]),
     "spnerf_get_option": (c_int32, [c_char_p, POINTER(c_int32)]),
     "spnerf_adam_step": (c_int32, [c_int32, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),

@@ -434,11 +434,96 @@ def rpc_rays(ref: str) -> dict:
     return out
 
 
+def dsm_latlon(ref: str) -> None:
+    """datasets/satellite_scene.py:475-505 (get_latlonalt_from_nerf_prediction, with
+    modules/utils.py:103-122 ecef_to_latlon_custom) run by the reference itself on 4096 real
+    JAX_269_007 rays (rpc_rays.npz, ds 8) at a drawn depth between each ray's near and far; its
+    I/O-only imports stubbed as in rpc_rays.  Pins oracle/dsm_ref.latlonalt_from_prediction and
+    spnerf_dsm_points.  (Its UTM step calls pyproj and the DSM step plyflatten: both absent, so
+    those stay parity unpinned.)"""
+    import json
+    import types
+    from unittest import mock
+    stubs = ["rasterio", "rpcm", "torchvision", "torchvision.transforms", "cv2", "pyproj", "utm", "osgeo", "gdal",
+             "plyflatten", "kornia", "kornia.losses", "srtm4", "numba", "lpips", "PIL", "PIL.Image"]
+    saved = {k: sys.modules.get(k) for k in stubs}
+    for k in stubs:
+        sys.modules[k] = mock.MagicMock()
+    try:
+        import datasets.satellite_scene as ss
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    jdir = os.path.join(ref, "Dataset", "DFC2019_269", "JSON")
+    loc = json.load(open(os.path.join(jdir, "scene.loc")))
+    center = torch.tensor([float(loc["X_offset"]), float(loc["Y_offset"]), float(loc["Z_offset"])])
+    rng = torch.max(torch.tensor([float(loc["X_scale"]), float(loc["Y_scale"]), float(loc["Z_scale"])]))
+    holder = types.SimpleNamespace(center=center, range=rng)
+    rays_all = np.load(os.path.join(HERE, "rpc_rays.npz"))["007_ds8|rays"]
+    sel = np.sort(np.random.default_rng(0).choice(rays_all.shape[0], 4096, replace=False))
+    rays = torch.tensor(rays_all[sel])
+    g = torch.Generator().manual_seed(0)
+    depth = rays[:, 6] + (rays[:, 7] - rays[:, 6]) * torch.rand(rays.shape[0], generator=g)
+    lats, lons, alts = ss.SatelliteSceneDataset.get_latlonalt_from_nerf_prediction(holder, rays, depth.view(-1, 1))
+    np.savez_compressed(os.path.join(HERE, "dsm_latlon.npz"), rays=rays.numpy(), depth=depth.numpy(),
+                        center=center.numpy(), range=np.array(rng.item(), np.float32), lats=np.asarray(lats),
+                        lons=np.asarray(lons), alts=np.asarray(alts))
+    print("dsm_latlon written", rays.shape)
+    # DSM end-to-end data: every JAX_269_007 ds-8 ray with the depth at which it meets the lidar
+    # ground truth (Truth/JAX_269_DSM.tif on its ROI grid, Truth/JAX_269_DSM.txt), found by
+    # bisection through the oracle's lat/lon/alt + UTM (geometry input only — the expected
+    # values are the reference's lidar DSM itself, stored as float16 heights: 1.6 cm steps)
+    from PIL import Image
+    from oracle import dsm_ref
+    tdir = os.path.join(ref, "Dataset", "DFC2019_269", "Truth")
+    gt = np.array(Image.open(os.path.join(tdir, "JAX_269_DSM.tif")), np.float64)
+    roi = np.loadtxt(os.path.join(tdir, "JAX_269_DSM.txt"))
+    xoff, yoff, xsize, ysize, res = dsm_ref.dsm_grid(None, None, roi=roi)
+    r = rays_all.astype(np.float64)
+    c = center.numpy().astype(np.float64)
+    rg = float(np.float32(rng.item()))
+    lat0, lon0, _ = dsm_ref.latlonalt_from_prediction(r[:1], r[:1, 6], c, rg)
+    zone = dsm_ref.utm_zone(float(lat0[0]), float(lon0[0]))[0]
+
+    def f(t):
+        la, lo, al = dsm_ref.latlonalt_from_prediction(r, t, c, rg)
+        e, n = dsm_ref.utm(la, lo, zone)
+        i = np.floor((e - xoff) / res).astype(np.int64)
+        j = np.floor((yoff - n) / res).astype(np.int64)
+        ok = (i >= 0) & (j >= 0) & (i < xsize) & (j < ysize)
+        h = np.full(t.shape, np.nan)
+        h[ok] = gt[j[ok], i[ok]]
+        return al - h
+
+    lo_t, hi_t = r[:, 6].copy(), r[:, 7].copy()
+    for _ in range(60):
+        mid = 0.5 * (lo_t + hi_t)
+        fm = f(mid)
+        above = fm > 0   # the ray is still above the surface: go deeper
+        lo_t = np.where(above, mid, lo_t)
+        hi_t = np.where(above, hi_t, mid)
+    t = 0.5 * (lo_t + hi_t)
+    hit = np.isfinite(f(t))
+    np.savez_compressed(os.path.join(HERE, "dsm_truth.npz"), rays=rays_all[hit], depth=t[hit].astype(np.float32),
+                        center=center.numpy(), range=np.array(rng.item(), np.float32), roi=roi,
+                        gt=gt.astype(np.float16), zone=np.array(zone))
+    print("dsm_truth written", int(hit.sum()), "of", r.shape[0], "rays on the ROI")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None, help="regenerate one fixture group only (dsm)")
     a = ap.parse_args()
     torch.set_num_threads(8)
+    if a.only == "dsm":
+        sys.path.insert(0, a.ref)
+        sys.dont_write_bytecode = True
+        dsm_latlon(a.ref)
+        return
     ref_spnerf, ref_rendering = load_reference(a.ref)
     real = rpc_rays(a.ref)
     # config 1: the 16x16 crop of JAX_269_006 (rows/cols 400-415; rays through the reference's
@@ -476,6 +561,7 @@ def main():
     init_weights(ref_spnerf)
     dropins(ref_spnerf, ref_rendering)
     losses(a.ref)
+    dsm_latlon(a.ref)
 
 
 if __name__ == "__main__":
