@@ -1209,6 +1209,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 int g_nt16_variant = 8;
 int g_nt16_ip = 2;  // DMA NT / TN: where a K-step issues the next step's DMAs (0 before its MFMAs, 1 after, 2 between the k-halves)
 int g_tn16_ip = 2;
+int g_nt16_ip_gen = 2;  // the same for the general (bias / sine / rank-1) epilogue instances
 int g_tn16_variant = 3;
 
 static bool tn_wide(int N, int K, int variant) {
@@ -1248,6 +1249,7 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
         if (dm && ip == 2) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else if (dm && ip == 1) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else if (dm) hipLaunchKernelGGL(k_gemm_nt_bf16d<true>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else if (g_nt16_ip_gen == 2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else hipLaunchKernelGGL(k_gemm_nt_bf16d<false>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         SPN_HIP(hipGetLastError());
         return SPNERF_OK;
