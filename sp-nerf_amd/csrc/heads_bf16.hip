@@ -46,15 +46,20 @@ __device__ __forceinline__ int img_off(int row, int ch) { return row * 1024 + ((
 
 // acc[a][j] (features 32·NA·w + 32a.., points 32j..) = Σ_k W[n][k] · image[point][k] over nks
 // k-steps of 16; wsrc = this wave's fragment stream (+ lane · 8)
+// the first TPD k-steps of a layer's weight stream (issuing them one phase early, before the
+// previous layer's epilogue, measured slower: the live ring across the epilogue spills)
 template <int NA>
-__device__ __forceinline__ void layer_mm(const bf16* __restrict__ wsrc, int nks, const char* smem, int lane,
-                                         f32x16 (&acc)[NA][NJ]) {
-    const int r32 = lane & 31, h = lane >> 5, sw = r32 & 15;
-    u32x4 ring[TPD][NA];
+__device__ __forceinline__ void layer_prime(const bf16* __restrict__ wsrc, u32x4 (&ring)[TPD][NA]) {
 #pragma unroll
     for (int d = 0; d < TPD; ++d)
 #pragma unroll
         for (int a = 0; a < NA; ++a) ring[d][a] = ldg16(wsrc + (d * NA + a) * 512);
+}
+
+template <int NA>
+__device__ __forceinline__ void layer_mm(const bf16* __restrict__ wsrc, int nks, const char* smem, int lane,
+                                         f32x16 (&acc)[NA][NJ], u32x4 (&ring)[TPD][NA]) {
+    const int r32 = lane & 31, h = lane >> 5, sw = r32 & 15;
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
@@ -111,18 +116,46 @@ __device__ __forceinline__ float wtotal(float v) {
            (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
 }
 
-// lane-partial dot of image row `row`, chunks [ch0, ch0 + nch), with fp32 weights w[8·(chunk - ch0) ..]
-__device__ __forceinline__ float row_dot(const char* smem, int row, int ch0, int nch, const float* __restrict__ w,
-                                         int lane_) {
-    const int lane = opaque(lane_);  // keeps the weight loads in the loop (hoisted, they stay live)
-    if (lane >= nch) return 0.f;
-    const u32x4 x = *reinterpret_cast<const u32x4*>(smem + img_off(row, ch0 + lane));
+// lane-partial dot of one 16-B image chunk with 8 fp32 weights held in registers
+__device__ __forceinline__ float dot8(u32x4 x, f32x4 w0, f32x4 w1) {
     float f[8];
     unpack8(x, f);
-    const f32x4 w0 = ld4(w + 8 * lane), w1 = ld4(w + 8 * lane + 4);
     return ((f[0] * w0[0] + f[1] * w0[1]) + (f[2] * w0[2] + f[3] * w0[3])) +
            ((f[4] * w1[0] + f[5] * w1[1]) + (f[6] * w1[2] + f[7] * w1[3]));
 }
+
+// the narrow heads' dot products for the 16 points of wave w, four points at a time: each lane
+// owns chunk ch0 + lane (lanes >= nch contribute 0), its NDOT weight octets loaded once per tile;
+// fn(r, t[NDOT]) receives every point's wave totals (the same per-lane expression and wave sum
+// as one point at a time: bit-identical)
+template <int NDOT, typename F>
+__device__ __forceinline__ void dots16(const char* smem, int w, int lane_, int ch0, int nch, const float* __restrict__ wp,
+                                       int wstride, F fn) {
+    const int lane = opaque(lane_);
+    const bool on = lane < nch;
+    f32x4 w0[NDOT], w1[NDOT];
+#pragma unroll
+    for (int c = 0; c < NDOT; ++c) {
+        w0[c] = on ? ld4(wp + c * wstride + 8 * lane) : f32x4{0.f, 0.f, 0.f, 0.f};
+        w1[c] = on ? ld4(wp + c * wstride + 8 * lane + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll 1
+    for (int r0 = 16 * w; r0 < 16 * w + 16; r0 += 4) {
+        u32x4 x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            x[q] = *reinterpret_cast<const u32x4*>(smem + img_off(r0 + q, ch0 + (on ? lane : 0)));
+        float t[4][NDOT];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int c = 0; c < NDOT; ++c) t[q][c] = wtotal(on ? dot8(x[q], w0[c], w1[c]) : 0.f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fn(r0 + q, t[q]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs k, int ntiles) {
@@ -186,17 +219,16 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
 
         // σ: wave w takes points 16w .. 16w + 15 (loops of dot products stay rolled and fenced:
         // unrolled, their hoisted LDS reads stayed live into the GEMM phases and spilled)
-#pragma unroll 1
-        for (int r = 16 * w; r < 16 * w + 16; ++r) {
-            const float spre = wtotal(row_dot(smem, r, 0, 64, Pk + k.wsig, lane)) + Pk[k.bsig];
-            if (lane == 0) ost[r * OST_LD + 3] = softplusf_(spre);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+        dots16<1>(smem, w, lane, 0, 64, Pk + k.wsig, 0, [&](int r, const float (&t)[1]) {
+            if (lane == 0) ost[r * OST_LD + 3] = softplusf_(t[0] + Pk[k.bsig]);
+        });
         if (full) {
             // semantic hidden (256) → logits through W_m2 in the epilogue
             if (C > 0) {
                 f32x16 acc[1][NJ];
-                layer_mm<1>(stream(k.Fsem16, HW / 16, 1), HW / 16, smem, lane, acc);
+                u32x4 ring1[TPD][1];
+                layer_prime<1>(stream(k.Fsem16, HW / 16, 1), ring1);
+                layer_mm<1>(stream(k.Fsem16, HW / 16, 1), HW / 16, smem, lane, acc, ring1);
                 // logits partials over this wave's 32 features, per point (lane halves hold 4 + 4)
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
                 float sacc[NJ][4];
@@ -234,7 +266,9 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
             __builtin_amdgcn_sched_barrier(0);
             {
                 f32x16 acc[2][NJ];
-                layer_mm<2>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc);
+                u32x4 ring2[TPD][2];
+                layer_prime<2>(stream(k.Ffeat16, HW / 16, 2), ring2);
+                layer_mm<2>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc, ring2);
                 __syncthreads();  // every wave is done reading H_L
                 epi(std::integral_constant<int, 2>{}, acc, [&](int, int, int, int f0, int row, const float (&v)[4]) {
                     const f32x4 bv = ld4(Pk + k.bG + f0);
@@ -246,7 +280,9 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
             // [sun1 | rgb1] = sin(W_Q feat + b + per-ray sun rows) → the image
             {
                 f32x16 acc[2][NJ];
-                layer_mm<2>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc);
+                u32x4 ring2[TPD][2];
+                layer_prime<2>(stream(k.FQ16, HW / 16, 2), ring2);
+                layer_mm<2>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2);
                 __syncthreads();
                 epi(std::integral_constant<int, 2>{}, acc, [&](int, int, int, int f0, int row, const float (&v)[4]) {
                     const f32x4 bv = ld4(Pk + k.bQ + f0);
@@ -269,18 +305,19 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
             }
             // albedo from rgb1 (image chunks 32..63)
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll 1
-            for (int r = 16 * w; r < 16 * w + 16; ++r) {
+            dots16<3>(smem, w, lane, 32, 32, Pk + k.Wr2, HH, [&](int r, const float (&t)[3]) {
                 float rgb[3];
 #pragma unroll
-                for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf_(wtotal(row_dot(smem, r, 32, 32, Pk + k.Wr2 + c * HH, lane)) + Pk[k.br2 + c]);
+                for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf_(t[c] + Pk[k.br2 + c]);
                 if (lane < 3) ost[r * OST_LD + lane] = __fsub_rn(__fmul_rn(lane == 0 ? rgb[0] : (lane == 1 ? rgb[1] : rgb[2]), 1.002f), 0.001f);
-            }
+            });
             __syncthreads();  // rgb1 read before sun_v 2 overwrites the image's first half
             // sun_v 2 and 3 on image columns 0..255
             for (int l = 0; l < 2; ++l) {
                 f32x16 acc[1][NJ];
-                layer_mm<1>(stream(l == 0 ? k.Fs2_16 : k.Fs3_16, HH / 16, 1), HH / 16, smem, lane, acc);
+                u32x4 ring1[TPD][1];
+                layer_prime<1>(stream(l == 0 ? k.Fs2_16 : k.Fs3_16, HH / 16, 1), ring1);
+                layer_mm<1>(stream(l == 0 ? k.Fs2_16 : k.Fs3_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1);
                 __syncthreads();
                 const int64_t boff = l == 0 ? k.bs2 : k.bs3;
                 epi(std::integral_constant<int, 1>{}, acc, [&](int, int, int, int f0, int row, const float (&v)[4]) {
@@ -294,13 +331,12 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
             }
             // sun visibility and the ray's sky colour
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll 1
-            for (int r = 16 * w; r < 16 * w + 16; ++r) {
-                const float sun = sigmoidf_(wtotal(row_dot(smem, r, 0, 32, Pk + k.ws4, lane)) + Pk[k.bs4]);
+            dots16<1>(smem, w, lane, 0, 32, Pk + k.ws4, 0, [&](int r, const float (&t)[1]) {
+                const float sun = sigmoidf_(t[0] + Pk[k.bs4]);
                 const float sky = lane < 3 ? g.sky[(std::min<int64_t>(p0 + r, g.P - 1) / g.S) * 4 + lane] : 0.f;
                 if (lane == 0) ost[r * OST_LD + 4] = sun;
                 if (lane < 3) ost[r * OST_LD + 5 + lane] = sky;
-            }
+            });
         }
         __syncthreads();
         // the tile's output rows, contiguous in HBM
