@@ -359,6 +359,8 @@ def run_inference(a, c, rank, world, dev):
         "mlp_gemms": gemm_totals(a.steps),
         "finite": bool(torch.isfinite(res["rgb_coarse"]).all()),
     }
+    if a.full_image:
+        out["full_image"] = full_image(rays, sems, model, args, B, rank, world, dev, h, w, c)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or 1024)
     if rank == 0:
@@ -366,6 +368,53 @@ def run_inference(a, c, rank, world, dev):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+@torch.no_grad()
+def full_image(rays, sems, model, args, B, rank, world, dev, h, w, c):
+    """The whole C5 image: every rank renders all rays of its row shard in chunks of B into an
+    HBM-resident [rows·w][4] (rgb, depth) buffer, then the shards are gathered to rank 0 (one
+    all_gather of equal, padded shards; on CPU copies when the group is gloo).  Timed from the
+    first chunk to the gathered image on rank 0, max over ranks."""
+    n = rays.shape[0]
+    shard = torch.empty(n, 4, device=dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i0 in range(0, n, B):
+        i1 = min(n, i0 + B)
+        res = spnerf_amd.render_rays({"coarse": model}, args, rays[i0:i1], None, semantics=sems[i0:i1], mode="test")
+        shard[i0:i1, 0:3] = res["rgb_coarse"]
+        shard[i0:i1, 3] = res["depth_coarse"]
+    torch.cuda.synchronize()
+    t_render = time.perf_counter() - t0
+    if world > 1:
+        rows_max = (h + world - 1) // world
+        pad = torch.zeros(rows_max * w, 4, device=dev)
+        pad[:n] = shard
+        gloo = dist.get_backend() == "gloo"
+        src = pad.cpu() if gloo else pad
+        parts = [torch.empty_like(src) for _ in range(world)]
+        dist.all_gather(parts, src)
+        if rank == 0:
+            image = torch.cat([parts[r][:((r + 1) * h // world - r * h // world) * w] for r in range(world)]).to(dev)
+        else:
+            image = None
+    else:
+        image = shard
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0, t_render], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    info = {"rays": h * w, "height": h, "width": w, "samples_per_ray": c["n_samples"], "seconds": float(t[0]),
+            "render_seconds_max_rank": float(t[1]), "gathered_to_rank0": world > 1,
+            "ray_samples_per_s": h * w * c["n_samples"] / float(t[0])}
+    if rank == 0:
+        img = image.reshape(h, w, 4)
+        info.update({"finite": bool(torch.isfinite(img).all()), "rgb_mean": [float(v) for v in img[..., :3].mean((0, 1))],
+                     "depth_min_max": [float(img[..., 3].min()), float(img[..., 3].max())]})
+    return info
 
 
 def free_port():
@@ -403,6 +452,9 @@ def parse_args(argv=None):
     ap.add_argument("--torch-loss", action="store_true", help="the losses module (plain torch) instead of the fused loss kernels")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-batch", type=int, default=0, help="rays per CPU-baseline step (default: the GPU step's batch)")
+    ap.add_argument("--full-image", action="store_true",
+                    help="C5: after the timed chunks, render every ray of the image (each rank its row shard) and "
+                         "gather rgb + depth to rank 0; reported as full_image")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="replay render+loss+backward as a HIP graph (default)")
     ap.add_argument("--eager", dest="graph", action="store_false", help="launch every kernel from Python")
