@@ -46,7 +46,7 @@ __global__ __launch_bounds__(512) void k_stream(const char* __restrict__ src, in
 // the same walk landing in LDS by global_load_lds_dwordx4 (one 1-KB wave-instruction = 16 rows x
 // 64 B when SEG = 64, 4 rows x 256 B, or one 1-KB row), four slices in flight per wave, no
 // consumer; tiles taken modulo tmod (tmod = 8: a 2 MB footprint, L2-resident)
-template <int SEG>
+template <int SEG, bool BAR = false>
 __global__ __launch_bounds__(512) void k_stream_dma(const char* __restrict__ src, int ntiles, int tmod, u32x4* out) {
     __shared__ __attribute__((aligned(16))) char smem[4 * 32768];
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -69,6 +69,7 @@ __global__ __launch_bounds__(512) void k_stream_dma(const char* __restrict__ src
             if (IPS == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
             else if (IPS == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            if constexpr (BAR) __builtin_amdgcn_s_barrier();  // a GEMM K-loop's per-step block barrier
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -143,6 +144,7 @@ int main() {
         run2(k_stream_dma<64>, "LDS-DMA, 16 rows x 64 B / instr", tmod);
         run2(k_stream_dma<256>, "LDS-DMA, 4 rows x 256 B / instr", tmod);
         run2(k_stream_dma<1024>, "LDS-DMA, 1 row x 1 KB / instr", tmod);
+        run2(k_stream_dma<64, true>, "LDS-DMA 64 B + barrier per slice", tmod);
     }
     for (int grid : {256}) {
         run(k_stream<64>, "slices of 64 B per row", grid);
