@@ -11,7 +11,8 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libspnerf_amd.so")
+# SPNERF_AMD_LIB: another in-tree build of the same sources (A/B runs of compile-time variants)
+LIB_PATH = os.path.join(HERE, os.environ.get("SPNERF_AMD_LIB", "libspnerf_amd.so"))
 
 SPNERF_MLP_SAVE = 1
 SPNERF_MLP_SIGMA_ONLY = 2

@@ -83,36 +83,31 @@ __device__ __forceinline__ void unpack8(u32x4 v, float (&f)[8]) {
     }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 (round to nearest even): one v_cvt_pk_bf16_f32 (converting the
+// scalars separately costs a convert, a shift and an or per pair)
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-    const __bf16 a = (__bf16)lo, b = (__bf16)hi;
-    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
 }
 
 __device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
     return u32x4{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
 }
 
-// sin / cos for bf16 outputs: reduce to [-1/2, 1/2] revolutions, then the hardware
-// v_sin_f32 / v_cos_f32 (argument in revolutions).  Absolute error ~1e-6 for |x| < 1e3,
+// sin / cos for bf16 outputs: reduce to [0, 1) revolutions (v_fract_f32, exact), then the
+// hardware v_sin_f32 / v_cos_f32 (argument in revolutions).  Absolute error ~1e-6 for |x| < 1e3,
 // far below the bf16 rounding of the result (2^-9 relative).
+__device__ __forceinline__ float revs(float x) { return __builtin_amdgcn_fractf(x * 0.15915494309189535f); }
 __device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
-    float r = x * 0.15915494309189535f;
-    r -= __builtin_rintf(r);
+    const float r = revs(x);
     *s = __builtin_amdgcn_sinf(r);
     *c = __builtin_amdgcn_cosf(r);
 }
 
 // the sine / cosine halves of fast_sincos (bit-identical results)
-__device__ __forceinline__ float fast_sin(float x) {
-    float r = x * 0.15915494309189535f;
-    r -= __builtin_rintf(r);
-    return __builtin_amdgcn_sinf(r);
-}
-__device__ __forceinline__ float fast_cos(float x) {
-    float r = x * 0.15915494309189535f;
-    r -= __builtin_rintf(r);
-    return __builtin_amdgcn_cosf(r);
-}
+__device__ __forceinline__ float fast_sin(float x) { return __builtin_amdgcn_sinf(revs(x)); }
+__device__ __forceinline__ float fast_cos(float x) { return __builtin_amdgcn_cosf(revs(x)); }
 
 // The saved pre-activation Z of a bf16 trunk layer is stored as fp16 (11-bit significand: 4x
 // finer than bf16 at the same 2 bytes; hidden-layer |Z| is O(1), far inside fp16's range), and

@@ -30,6 +30,7 @@ namespace spn {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 int g_fused_heads = 1;
+int g_heads_dbg = 0;
 
 namespace {
 constexpr int TM = 128;                 // points per tile
@@ -40,7 +41,9 @@ constexpr int IMG = TM * HW * 2;        // the [128][512] bf16 image
 constexpr int OST_LD = 16;              // output staging row (floats), NO <= 16
 constexpr int OST_OFF = IMG;
 constexpr int PART_OFF = OST_OFF + TM * OST_LD * 4;
-constexpr int LDS = PART_OFF + 8 * TM * 4 * 4;  // semantic partials [wave][point][4]
+constexpr int RQ_OFF = PART_OFF + 8 * TM * 4 * 4;  // semantic partials [wave][point][4]
+constexpr int RQ_RAYS = 4;                         // per-ray Q rows staged for tiles of <= 4 rays
+constexpr int LDS = RQ_OFF + RQ_RAYS * 2 * HH * 4;
 
 __device__ __forceinline__ int img_off(int row, int ch) { return row * 1024 + ((ch ^ (row & 15)) << 4); }
 
@@ -163,6 +166,7 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     float* ost = reinterpret_cast<float*>(smem + OST_OFF);
     float* part = reinterpret_cast<float*>(smem + PART_OFF);
+    float* srq = reinterpret_cast<float*>(smem + RQ_OFF);
     const float* Pk = g.packed;
     const bf16* P16 = reinterpret_cast<const bf16*>(g.packed);
     const bool full = g.mode == 0;
@@ -200,6 +204,13 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
 
     for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TM;
+        // the tile's rays' sun rows of Q into LDS when they are few (one ray per tile at 128
+        // samples per ray): the Q epilogue then reads LDS instead of an L2 round trip per row
+        const int64_t ray0 = p0 / g.S;
+        const int nray = (int)((std::min<int64_t>(p0 + TM, g.P) - 1) / g.S - ray0) + 1;
+        const bool rq_lds = full && nray <= RQ_RAYS && !(g.dbg & 4);  // block-uniform (dbg 4: A/B)
+        if (rq_lds)
+            for (int i = tid; i < nray * 2 * HH; i += 512) srq[i] = g.rbQ[ray0 * (2 * HH) + i];
         // stage H_L (rows past P read a clamped row; their outputs are never stored)
 #pragma unroll
         for (int q0 = 0; q0 < 16; q0 += 8) {
@@ -207,7 +218,8 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int c = tid + 512 * (q0 + q), row = c >> 6, ch = c & 63;
-                v[q] = ldg16(g.HL + std::min<int64_t>(p0 + row, g.P - 1) * HW + ch * 8);
+                const u32x4* src = reinterpret_cast<const u32x4*>(g.HL + std::min<int64_t>(p0 + row, g.P - 1) * HW + ch * 8);
+                v[q] = (g.dbg & 2) ? u32x4{0u, 0u, 0u, 0u} : g.nt ? __builtin_nontemporal_load(src) : *src;  // block-uniform
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -284,10 +296,15 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
                 layer_prime<2>(stream(k.FQ16, HW / 16, 2), ring2);
                 layer_mm<2>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2);
                 __syncthreads();
-                epi(std::integral_constant<int, 2>{}, acc, [&](int, int, int, int f0, int row, const float (&v)[4]) {
+                // each accumulator row's ray, relative to ray0 (P < 2^31: host check)
+                const int er32 = opaque(lane) & 31;
+                int rrel[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) rrel[j] = (int)(std::min<int64_t>(p0 + 32 * j + er32, g.P - 1) / g.S - ray0);
+                epi(std::integral_constant<int, 2>{}, acc, [&](int, int j, int, int f0, int row, const float (&v)[4]) {
                     const f32x4 bv = ld4(Pk + k.bQ + f0);
-                    const int pt = (int)std::min<int64_t>(p0 + row, g.P - 1);   // P < 2^31 (host check)
-                    const f32x4 rv = ld4(g.rbQ + (int64_t)(pt / g.S) * (2 * HH) + f0);
+                    const f32x4 rv = rq_lds ? *reinterpret_cast<const f32x4*>(srq + rrel[j] * (2 * HH) + f0)
+                                            : ld4(g.rbQ + (ray0 + rrel[j]) * (2 * HH) + f0);
                     float y[4];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) y[e] = fast_sin((v[e] + bv[e]) + rv[e]);
@@ -361,8 +378,11 @@ int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, 
             "heads_bf16: weights not packed for the fused heads");
     if (a.P == 0) return SPNERF_OK;
     const int ntiles = (int)((a.P + TM - 1) / TM);
+    HeadsFusedArgs ad = a;
+    ad.nt = (g_trunk_nt >> 1) & 1;
+    ad.dbg = g_heads_dbg;
     ProfScope prof("heads_fused", s, flop, bytes);
-    hipLaunchKernelGGL(k_heads_bf16, dim3(std::min(ntiles, 256)), dim3(512), 0, s, a, k, ntiles);
+    hipLaunchKernelGGL(k_heads_bf16, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, k, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -1581,6 +1581,9 @@ static int* option_slot(const char* name) {
     if (n == "fused_trunk") return &g_fused_trunk;
     if (n == "trunk_tile") return &g_trunk_tile;
     if (n == "trunk_dbg") return &g_trunk_dbg;
+    if (n == "trunk_nt") return &g_trunk_nt;
+    if (n == "trunk_var") return &g_trunk_var;
+    if (n == "heads_dbg") return &g_heads_dbg;
     if (n == "nt_f32_variant") return &g_nt_variant;
     if (n == "tn_f32_variant") return &g_tn_variant;
     if (n == "nt_bf16_variant") return &g_nt16_variant;

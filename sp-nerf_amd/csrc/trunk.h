@@ -40,6 +40,7 @@ struct TrunkArgs {
     int64_t P = 0;
     int S = 1, L = 0, skip = -1, K0p = 0;
     int dbg = 0;  // set from g_trunk_dbg by trunk_bf16
+    int nt = 0;   // set from g_trunk_nt: non-temporal copy-out stores of H
     // layers >= 1 (w0 = 1): H = sin(Z), Z = the pre-activation rounded to fp16; when saving, Ds[i]
     // receives Z as fp16 (consumers recompute cos(Z) and sin(Z)) and Hs[i] may be null
     int zround = 0;
@@ -53,11 +54,19 @@ struct TrunkArgs {
 // Offset (bf16 elements) of W[n][k] of a [512][Kp] layer in MFMA A-fragment order: wave w =
 // n / 64 streams k-steps of 16; per k-step its two 32-feature tiles are 1 KB each, lane
 // (n % 32) + 32·((k / 8) % 2) holding 8 consecutive k.
+#ifndef SPN_TRUNK_KMAJOR
+#define SPN_TRUNK_KMAJOR 0
+#endif
+// With SPN_TRUNK_KMAJOR the 8 waves' 2 KB pieces of one k-step are adjacent (16 KB per k-step)
+// instead of each wave's stream being contiguous.
 __host__ __device__ inline int64_t trunk_frag_off(int n, int k, int Kp) {
     const int nks = Kp >> 4;
-    return ((((int64_t)(n >> 6) * nks + (k >> 4)) * 2 + ((n >> 5) & 1)) * 64 + (n & 31) + 32 * ((k >> 3) & 1)) * 8 +
-           (k & 7);
+    const int64_t blk = SPN_TRUNK_KMAJOR ? (int64_t)(k >> 4) * 8 + (n >> 6) : (int64_t)(n >> 6) * nks + (k >> 4);
+    return ((blk * 2 + ((n >> 5) & 1)) * 64 + (n & 31) + 32 * ((k >> 3) & 1)) * 8 + (k & 7);
 }
+// wave w's stream of a layer with nks k-steps: the first k-step's offset and the k-step stride
+__host__ __device__ inline int64_t trunk_wave_off(int w, int nks) { return SPN_TRUNK_KMAJOR ? w * 1024 : (int64_t)w * nks * 1024; }
+constexpr int kTrunkKStride = SPN_TRUNK_KMAJOR ? 8192 : 1024;
 
 // MFMA A-fragment order for a layer whose waves own NA 32-feature tiles each (NA = 2: the trunk's
 // layout above; NA = 1: 32 features per wave, for 256-wide layers)
@@ -82,6 +91,8 @@ struct HeadsFusedArgs {
     float* out = nullptr;
     int64_t P = 0;
     int S = 1, NO = 8, C = 0, sem_col = 8, mode = 0;  // mode: 0 all heads, 1 σ only
+    int nt = 0;  // non-temporal loads of HL (g_trunk_nt & 2)
+    int dbg = 0;  // profiling ablations (g_heads_dbg; outputs invalid): 2 = no H staging loads
 };
 struct PackedOffs;
 struct Dims;
@@ -89,10 +100,13 @@ bool heads_bf16_shape_ok(const Dims& d);   // the packed layout carries the fuse
 bool heads_bf16_supported(const Dims& d);  // ... and the option is on
 int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes);
 
+extern int g_heads_dbg;    // HeadsFusedArgs::dbg
 extern int g_fused_heads;  // 1 = bf16 inference runs the fused heads where supported (default)
 extern int g_fused_trunk;  // 1 = bf16 forwards use the fused trunk where supported (default)
 extern int g_trunk_tile;   // 0 = tile by mode; 64 / 128 = force
 extern int g_trunk_dbg;    // profiling ablations (outputs invalid): 1 = no HBM copy-outs
+extern int g_trunk_var;    // profiling ablations of the 128-point trunk (outputs invalid)
+extern int g_trunk_nt;     // 1 = trunk H stores non-temporal, 2 = fused heads' H loads non-temporal
 bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 // layer 0 inside the launch (TrunkArgs::X0) for this PE width when saving / not saving
 bool trunk_l0_supported(int K0p, bool save);

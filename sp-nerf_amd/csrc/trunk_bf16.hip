@@ -38,7 +38,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 int g_fused_trunk = 1;
 int g_trunk_tile = 0;  // 0 = by mode (64 when saving, else 128); 64 / 128 force a tiling (A/B runs)
-int g_trunk_dbg = 0;   // profiling ablation, outputs invalid when set: 1 = skip the HBM copy-outs
+int g_trunk_nt = 0;
+int g_trunk_var = 0;  // profiling ablations of the 128-point tiling (k_trunk_bf16 VAR)
+int g_trunk_dbg = 0;   // profiling ablations, outputs invalid when set: 1 = skip the HBM copy-outs,
+                       // (options trunk_var 16 / 32: no MFMAs in the main k-loop / no sine in the
+                       // inference epilogue)
 
 constexpr int TW = 512;  // trunk width of the fused kernel
 
@@ -59,10 +63,15 @@ __device__ __forceinline__ int act_off(int row, int ch) { return row * 1024 + ((
 // lane group on distinct 16-B slots of the bank row
 __device__ __forceinline__ int x0_rel(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 
-template <int TMt>
+// VAR (TMt = 128 only): 0 = the kernel; profiling ablations (outputs invalid; option trunk_var),
+// bits: 16 = no MFMAs in the main k-loop, 32 = no sine in the epilogue, 64 = no weight refills
+// in the k-loop, 128 = no image (B) reads in the k-loop, 256 = no epilogue (464: all of them)
+template <int TMt, int VAR = 0>
 __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     using Geo = TrunkGeo<TMt>;
-    constexpr int NJ = Geo::NJ, TPD = Geo::TPD, IMG = Geo::IMG, CPT = Geo::CPT;
+    constexpr int NJ = Geo::NJ, IMG = Geo::IMG, CPT = Geo::CPT;
+    constexpr int TPD = Geo::TPD;
+    constexpr bool NOMF = VAR & 16, NOSIN = VAR & 32, NOW = VAR & 64, NOB = VAR & 128, NOEPI = VAR & 256;
     __shared__ __attribute__((aligned(16))) char smem[Geo::LDS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     float* sbias = reinterpret_cast<float*>(smem + Geo::BIAS_OFF);
@@ -81,14 +90,16 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
 
     u32x4 ring[TPD][2];
-    // wave w's fragment stream of layer i: k-step ks at + ks * 1024, feature tile a at + 512 * a
-    auto wstream = [&](int i) { return ka->Wf[i] + (int64_t)w * nks_of(i) * 1024 + lane * 8; };
-    auto prime = [&](int i) {
+    // wave w's fragment stream of layer i: k-step ks at + ks * kTrunkKStride, feature tile a at + 512 * a
+    auto wstream = [&](int i) { return ka->Wf[i] + trunk_wave_off(w, nks_of(i)) + lane * 8; };
+    // slots [d0, d1) of layer i's first k-steps
+    auto prime = [&](int i, auto kd0, auto kd1) {
+        constexpr int d0 = decltype(kd0)::value, d1 = decltype(kd1)::value;
         const bf16* src = wstream(i);
 #pragma unroll
-        for (int d = 0; d < TPD; ++d) {
-            ring[d][0] = ldg16(src + d * 1024);
-            ring[d][1] = ldg16(src + d * 1024 + 512);
+        for (int d = d0; d < d1; ++d) {
+            ring[d][0] = ldg16(src + d * kTrunkKStride);
+            ring[d][1] = ldg16(src + d * kTrunkKStride + 512);
         }
     };
     // copy chunks [q0, q0 + n) (per thread) of an image to HBM rows p0 + row
@@ -104,7 +115,11 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 #pragma unroll
         for (int q = 0; q < n; ++q) {
             const int c = ct + 512 * (q0 + q);
-            if (p0 + (c >> 6) < g.P) *reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8) = v[q];
+            if (p0 + (c >> 6) < g.P) {
+                u32x4* o = reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8);
+                if (g.nt) __builtin_nontemporal_store(v[q], o);  // block-uniform
+                else *o = v[q];
+            }
         }
     };
 
@@ -117,7 +132,13 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
-    prime(first);
+    // the ring may be primed in two parts: [0, PH) beside the live accumulators of the
+    // epilogue, the rest after it (an 8-deep ring primed that way measured slower than 4)
+    constexpr int PH = TPD;
+    using I0 = std::integral_constant<int, 0>;
+    using IPH = std::integral_constant<int, PH>;
+    using ITPD = std::integral_constant<int, TPD>;
+    prime(first, I0{}, ITPD{});
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TMt;
         const int st = opaque(tid);
@@ -213,19 +234,26 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                     const int offn = ((2 * (ks + 1) + h) ^ sw) << 4;
                     bf16x8 bn[NJ];
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
+                    for (int j = 0; j < NJ; ++j) bn[j] = NOB ? bc[j] : *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
                     const bf16x8 a0 = __builtin_bit_cast(bf16x8, ring[d][0]);
                     const bf16x8 a1 = __builtin_bit_cast(bf16x8, ring[d][1]);
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
+                        if constexpr (NOMF) {  // ablation: no MFMAs (keep the operands live)
+                            acc[0][j][0] += __builtin_bit_cast(float, a0[0] != bc[j][0] ? 1 : 0);
+                            acc[1][j][0] += __builtin_bit_cast(float, a1[0] != bc[j][0] ? 1 : 0);
+                            continue;
+                        }
                         acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bc[j], acc[0][j], 0, 0, 0);
                         acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bc[j], acc[1][j], 0, 0, 0);
                     }
                     // refill the slot just consumed, right behind its MFMAs (TPD - 1 steps of
                     // cover); past the stream's end: re-read its last step
                     const int kn = std::min(ks + TPD, nks - 1);
-                    ring[d][0] = ldg16(wsrc + kn * 1024);
-                    ring[d][1] = ldg16(wsrc + kn * 1024 + 512);
+                    if constexpr (!NOW) {
+                        ring[d][0] = ldg16(wsrc + kn * kTrunkKStride);
+                        ring[d][1] = ldg16(wsrc + kn * kTrunkKStride + 512);
+                    }
                     // order: (1 image read, 2 MFMAs) x NJ, then the 2 weight loads
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
@@ -265,19 +293,31 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             }
             // the next layer's (or the next tile's layer-1) first k-steps load during the epilogue
             const bool last = i == g.L - 1;
-            if (!last) prime(i + 1);
-            else if (tile + (int)gridDim.x < ntiles) prime(first);
+            const int inext = last ? (tile + (int)gridDim.x < ntiles ? first : -1) : i + 1;
+            if (inext >= 0) prime(inext, I0{}, IPH{});
 
             __syncthreads();  // every wave is done reading the images of layer i
             bf16* Hs = ka->Hs[i];
             bf16* Ds = ka->Ds[i];
             const float* rb = i == 0 ? g.rb0 : (skip ? g.rb_skip : nullptr);
-            const float w0 = i == 0 ? 30.f : 1.f;  // SIREN w0 of fc_net.0 (×1 elsewhere: exact)
-            const bool zr = g.zround && i >= 1;     // block-uniform: Z = fp16(v), the D slot gets Z
+            // block-uniform: Z = fp16(v), the D slot gets Z (saving tiles only: the host keeps
+            // zround off the 128-point tiling)
+            const bool zr = Geo::DIMG && g.zround && i >= 1;
             // kpass 0: cos (or Z) into the image (TMt = 128 when saving: it leaves between two
             // barriers); 1: sin into the image; 2: sin into the image and cos (or Z) into the D image
-            auto epilogue = [&](auto kpass) {
+            // kl0: layer 0 (SIREN w0 = 30 of fc_net.0; ×1 elsewhere, exact, so not multiplied)
+            auto epilogue = [&](auto kpass, auto kl0) {
+                if constexpr (NOEPI) {  // keep the accumulators (and so the MFMAs) live
+                    float t = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) t += acc[a][j][0];
+                    if (t == 1234.5f) *reinterpret_cast<float*>(smem + 4 * tid) = t;
+                    return;
+                }
                 constexpr int pass = decltype(kpass)::value;
+                constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
@@ -301,14 +341,14 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
                                 const float z = zr ? zr16(v[e]) : v[e];
-                                const float x = w0 * z;
+                                const float x = w0 == 1.f ? z : w0 * z;
                                 if (pass == 2) {
                                     fast_sincos(x, &y[e], &c[e]);
-                                    c[e] = zr ? z : w0 * c[e];
+                                    c[e] = zr ? z : (w0 == 1.f ? c[e] : w0 * c[e]);
                                 } else if (pass == 1) {
-                                    y[e] = fast_sin(x);
+                                    y[e] = NOSIN ? x : fast_sin(x);
                                 } else {
-                                    y[e] = zr ? z : w0 * fast_cos(x);
+                                    y[e] = zr ? z : (w0 == 1.f ? fast_cos(x) : w0 * fast_cos(x));
                                 }
                             }
                             // Z (zr: into the D image, or into the image by pass 0) is stored as fp16
@@ -324,9 +364,13 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                         __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
                     }
             };
+            auto epi = [&](auto kpass) {
+                if (i == 0) epilogue(kpass, std::true_type{});  // block-uniform
+                else epilogue(kpass, std::false_type{});
+            };
             if constexpr (Geo::DIMG) {
-                if (Ds) epilogue(std::integral_constant<int, 2>{});  // block-uniform
-                else epilogue(std::integral_constant<int, 1>{});
+                if (Ds) epi(std::integral_constant<int, 2>{});  // block-uniform
+                else epi(std::integral_constant<int, 1>{});
                 if (last) {
                     __syncthreads();
                     copy_all(smem, Hs, p0);
@@ -336,17 +380,20 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 dpend = last ? nullptr : Ds;
             } else {
                 if (Ds) {  // block-uniform
-                    epilogue(std::integral_constant<int, 0>{});
+                    epi(std::integral_constant<int, 0>{});
                     __syncthreads();
                     copy_all(smem, Ds, p0);
                     __syncthreads();  // the sin pass overwrites the image
                 }
-                epilogue(std::integral_constant<int, 1>{});
+                epi(std::integral_constant<int, 1>{});
                 if (last) {
                     __syncthreads();
                     copy_all(smem, Hs, p0);
                 }
                 hpend = last ? nullptr : Hs;
+            }
+            if constexpr (PH < TPD) {
+                if (inext >= 0) prime(inext, IPH{}, ITPD{});
             }
         }
         __syncthreads();  // the next tile restages the image and reuses the bias slots
@@ -373,16 +420,23 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     SPN_ARG(a.P < (1ll << 31) / TW, "trunk_bf16: too many points (%lld)", (long long)a.P);
     bool save = false;
     for (int i = 1; i < a.L; ++i) save |= a.Ds[i] != nullptr;
-    const int tm = trunk_tile(save);
+    const int tm = a.zround ? 64 : trunk_tile(save);  // the 128-point tiling has no fp16-Z path
     SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0 && !save), "trunk_bf16: inline encoding needs z, rs, inference");
     SPN_ARG(!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, save)), "trunk_bf16: layer 0 unsupported for K0p=%d",
             a.K0p);
     TrunkArgs ad = a;
     ad.dbg = g_trunk_dbg;
+    ad.nt = g_trunk_nt & 1;
     const int ntiles = cdiv(a.P, tm);
     ProfScope prof("trunk_bf16", s, flop, bytes);
     if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else hipLaunchKernelGGL(k_trunk_bf16<128>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 64) hipLaunchKernelGGL((k_trunk_bf16<128, 64>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 128) hipLaunchKernelGGL((k_trunk_bf16<128, 128>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 256) hipLaunchKernelGGL((k_trunk_bf16<128, 256>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 464) hipLaunchKernelGGL((k_trunk_bf16<128, 464>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else hipLaunchKernelGGL((k_trunk_bf16<128, 0>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

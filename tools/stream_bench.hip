@@ -101,6 +101,45 @@ __global__ __launch_bounds__(512) void k_stream_mod(const char* __restrict__ src
     if (acc[0] == 0x12345678u) out[tid] = acc;
 }
 
+
+// The fused trunk's weight stream without its MFMAs: every block (one per CU, 8 waves) walks
+// ntl tiles x 8 layers x 32 k-steps; per k-step each wave loads its 2 KB (two 16-B loads per
+// lane) of a 4 MB weight set through a TPD-deep register ring.  Layouts: 0 = each wave's stream
+// contiguous (64 KB per wave per layer), 1 = k-step-major (the 8 waves' pieces of a k-step
+// adjacent), 2 = k-step-major with the k order rotated per block.
+template <int TPD, int LAYOUT>
+__global__ __launch_bounds__(512) void k_wstream(const char* __restrict__ wts, int ntl, u32x4* out) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u32x4 ring[TPD][2];
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const int rot = LAYOUT == 2 ? (blockIdx.x * 5) & 31 : 0;
+    auto addr = [&](int layer, int ks) -> const u32x4* {
+        ks = (ks + rot) & 31;
+        const size_t blk = LAYOUT == 0 ? (size_t)w * 32 + ks : (size_t)ks * 8 + w;
+        return reinterpret_cast<const u32x4*>(wts + (size_t)layer * 524288 + blk * 2048) + lane;
+    };
+    for (int t = 0; t < ntl; ++t)
+        for (int layer = 0; layer < 8; ++layer) {
+#pragma unroll
+            for (int d = 0; d < TPD; ++d) {
+                ring[d][0] = addr(layer, d)[0];
+                ring[d][1] = addr(layer, d)[64];
+            }
+            for (int ks0 = 0; ks0 < 32; ks0 += TPD) {
+#pragma unroll
+                for (int d = 0; d < TPD; ++d) {
+                    acc ^= ring[d][0] ^ ring[d][1];
+                    const int kn = min(ks0 + d + TPD, 31);  // past the end: re-read (as the trunk)
+                    ring[d][0] = addr(layer, kn)[0];
+                    ring[d][1] = addr(layer, kn)[64];
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            __syncthreads();
+        }
+    if (acc[0] == 0x12345678u) out[tid] = acc;
+}
+
 int main() {
     const size_t bytes = (size_t)524288 * 1024;  // 512 MiB: 524 288 rows of 1 KB (bf16 x 512)
     char* src;
@@ -145,6 +184,28 @@ int main() {
         run2(k_stream_dma<256>, "LDS-DMA, 4 rows x 256 B / instr", tmod);
         run2(k_stream_dma<1024>, "LDS-DMA, 1 row x 1 KB / instr", tmod);
         run2(k_stream_dma<64, true>, "LDS-DMA 64 B + barrier per slice", tmod);
+    }
+    {
+        const int ntl = 64;
+        auto runw = [&](auto kern, const char* name) {
+            for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, src, ntl, out);
+            CK(hipEventRecord(a));
+            const int it = 10;
+            for (int i = 0; i < it; ++i) hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, src, ntl, out);
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            const double us = 1e3 * ms / it, per_cu = (double)ntl * 8 * 524288;
+            printf("%-40s %8.1f us  %5.1f B/clk/CU at 2.4 GHz\n", name, us, per_cu / (us * 1e-6) / 2.4e9);
+        };
+        runw(k_wstream<4, 0>, "weights TPD 4, wave-major");
+        runw(k_wstream<4, 1>, "weights TPD 4, k-major");
+        runw(k_wstream<4, 2>, "weights TPD 4, k-major rotated");
+        runw(k_wstream<8, 0>, "weights TPD 8, wave-major");
+        runw(k_wstream<8, 1>, "weights TPD 8, k-major");
+        runw(k_wstream<8, 2>, "weights TPD 8, k-major rotated");
+        runw(k_wstream<16, 1>, "weights TPD 16, k-major");
     }
     for (int grid : {256}) {
         run(k_stream<64>, "slices of 64 B per row", grid);
