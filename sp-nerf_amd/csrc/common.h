@@ -95,10 +95,11 @@ __device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
     return u32x4{pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
 }
 
-// sin / cos for bf16 outputs: reduce to [0, 1) revolutions (v_fract_f32, exact), then the
-// hardware v_sin_f32 / v_cos_f32 (argument in revolutions).  Absolute error ~1e-6 for |x| < 1e3,
-// far below the bf16 rounding of the result (2^-9 relative).
-__device__ __forceinline__ float revs(float x) { return __builtin_amdgcn_fractf(x * 0.15915494309189535f); }
+// sin / cos for bf16 outputs: the hardware v_sin_f32 / v_cos_f32 on the argument in revolutions,
+// as LLVM lowers native sin for gfx9 (whose sine unit reduces the full input range itself: no
+// v_fract, unlike GCN1-3).  Absolute error ~1e-6 for |x| < 1e3, far below the bf16 rounding of
+// the result (2^-9 relative).
+__device__ __forceinline__ float revs(float x) { return x * 0.15915494309189535f; }
 __device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
     const float r = revs(x);
     *s = __builtin_amdgcn_sinf(r);
