@@ -3,13 +3,13 @@
 // resident in LDS from the trunk output to the output row — instead of four GEMMs writing the
 // G / Q / sun_v activations to HBM (≈5 KB per point) and a heads kernel reading them back.
 //
-//   σ        = softplus(w_σ · H + b_σ)                                   (dot products, LDS rows)
+//   σ        = softplus(w_σ · H + b_σ)                (narrow_mm: a 32-row MFMA, hi/lo weight rows)
 //   semh     = sin(W_m1 H + b_m1)          [256]  → logits = W_m2 semh + b_m2 in its epilogue
 //   feat     = W_f H + b_f                 [512]  → the image
 //   [s1 | r1]= sin(W_Q feat + b_Q + sun rows[ray])  [256 | 256] → the image
-//   albedo   = sigmoid(W_r2 r1 + b_r2)·1.002 − 0.001                     (dot products)
+//   albedo   = sigmoid(W_r2 r1 + b_r2)·1.002 − 0.001                     (narrow_mm)
 //   s2, s3   = sin(W_s2 s1 + b), sin(W_s3 s2 + b)   [256] → image columns 0..255
-//   sun      = sigmoid(w_s4 · s3 + b)                                    (dot products)
+//   sun      = sigmoid(w_s4 · s3 + b)                                    (narrow_mm)
 //   sky      = the ray's sky colour (per-ray rows)
 //
 // The GEMM layers use the fused trunk's formulation (trunk_bf16.hip): weights are the MFMA A
@@ -17,9 +17,11 @@
 // [128][512] bf16 activation image (16-B chunks XOR-swizzled by row) the B operand, a
 // 32x32x16 accumulator holds 4 runs of 4 consecutive features of one point; 8 waves own 64
 // (512-wide layers) or 32 (256-wide layers) output features each.  Activations round to bf16
-// like the layer-by-layer path's GEMM outputs; the narrow heads' dot products run in fp32 on
-// the bf16 rows (other summation order than k_heads_fwd_v: not bit-identical, within bf16
-// rounding).
+// like the layer-by-layer path's GEMM outputs.  The narrow heads (σ, albedo, sun: 1–3 outputs)
+// are 32-row MFMA tiles whose rows are the bf16 hi and lo halves of the fp32 weight rows, K split
+// over the 8 waves and the partials summed in wave order (other summation order than
+// k_heads_fwd_v: not bit-identical, within bf16 rounding); as per-point dot products with wave
+// reductions they took a quarter of the kernel.
 #include <algorithm>
 
 #include "mlp_layout.h"
@@ -104,59 +106,43 @@ __device__ __forceinline__ void layer_mm(const bf16* __restrict__ wsrc, int nks,
     }
 }
 
-// Sum over the wavefront (DPP row adds + 4 readlanes), returned to every lane
-template <int CTRL>
-__device__ __forceinline__ float dppf(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float wtotal(float v) {
-    v += dppf<0xb1>(v);
-    v += dppf<0x4e>(v);
-    v += dppf<0x124>(v);
-    v += dppf<0x128>(v);
-    const int b = __float_as_int(v);
-    return (__int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16))) +
-           (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
-}
-
-// lane-partial dot of one 16-B image chunk with 8 fp32 weights held in registers
-__device__ __forceinline__ float dot8(u32x4 x, f32x4 w0, f32x4 w1) {
-    float f[8];
-    unpack8(x, f);
-    return ((f[0] * w0[0] + f[1] * w0[1]) + (f[2] * w0[2] + f[3] * w0[3])) +
-           ((f[4] * w1[0] + f[5] * w1[1]) + (f[6] * w1[2] + f[7] * w1[3]));
-}
-
-// the narrow heads' dot products for the 16 points of wave w, four points at a time: each lane
-// owns chunk ch0 + lane (lanes >= nch contribute 0), its NDOT weight octets loaded once per tile;
-// fn(r, t[NDOT]) receives every point's wave totals (the same per-lane expression and wave sum
-// as one point at a time: bit-identical)
-template <int NDOT, typename F>
-__device__ __forceinline__ void dots16(const char* smem, int w, int lane_, int ch0, int nch, const float* __restrict__ wp,
-                                       int wstride, F fn) {
-    const int lane = opaque(lane_);
-    const bool on = lane < nch;
-    f32x4 w0[NDOT], w1[NDOT];
+// A narrow head on MFMA: the [32][K] hi/lo-row A operand a (PackedOffs::Fnar16, fragment order,
+// 32 features per wave-tile) times the image columns from k-step kb, K split over the 8 waves
+// (wave w takes k-steps [w·KPER, (w+1)·KPER)) for all 128 points.  Row pairs (0, 1), (2, 3) and
+// (8, 9) are the hi and lo halves of up to three weight rows; their sums are this wave's partial
+// outputs, written to part[w][point][0..2] (summed over the waves in wave order by the caller).
+template <int KPER>
+__device__ __forceinline__ void narrow_mm(const bf16* __restrict__ a, int kb, const char* smem, int lane_, int w,
+                                          float* part) {
+    const int lane = opaque(lane_), r32 = lane & 31, h = lane >> 5, sw = r32 & 15;
+    u32x4 af[KPER];
 #pragma unroll
-    for (int c = 0; c < NDOT; ++c) {
-        w0[c] = on ? ld4(wp + c * wstride + 8 * lane) : f32x4{0.f, 0.f, 0.f, 0.f};
-        w1[c] = on ? ld4(wp + c * wstride + 8 * lane + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int d = 0; d < KPER; ++d) af[d] = ldg16(a + (w * KPER + d) * 512 + lane * 8);
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const char* brow = smem + r32 * 1024;
+#pragma unroll
+    for (int d = 0; d < KPER; ++d) {
+        const int off = ((2 * (kb + w * KPER + d) + h) ^ sw) << 4;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const bf16x8 b = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + off);
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[d]), b, acc[j], 0, 0, 0);
+        }
     }
-#pragma unroll 1
-    for (int r0 = 16 * w; r0 < 16 * w + 16; r0 += 4) {
-        u32x4 x[4];
+    // rows 0..3 are elements 0..3 and rows 8, 9 elements 4, 5 of lanes 0..31 (point = lane)
+    if (h == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            x[q] = *reinterpret_cast<const u32x4*>(smem + img_off(r0 + q, ch0 + (on ? lane : 0)));
-        float t[4][NDOT];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int c = 0; c < NDOT; ++c) t[q][c] = wtotal(on ? dot8(x[q], w0[c], w1[c]) : 0.f);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) fn(r0 + q, t[q]);
+        for (int j = 0; j < NJ; ++j)
+            *reinterpret_cast<f32x4*>(part + (w * TM + 32 * j + r32) * 4) =
+                f32x4{acc[j][0] + acc[j][1], acc[j][2] + acc[j][3], acc[j][4] + acc[j][5], 0.f};
     }
-    __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ int64_t narrow_off(int head) {  // σ, albedo, sun within Fnar16
+    return head == 0 ? 0 : head == 1 ? (int64_t)32 * HW : (int64_t)32 * (HW + HH);
 }
 
 }  // namespace
@@ -229,11 +215,15 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
         }
         __syncthreads();
 
-        // σ: wave w takes points 16w .. 16w + 15 (loops of dot products stay rolled and fenced:
-        // unrolled, their hoisted LDS reads stayed live into the GEMM phases and spilled)
-        dots16<1>(smem, w, lane, 0, 64, Pk + k.wsig, 0, [&](int r, const float (&t)[1]) {
-            if (lane == 0) ost[r * OST_LD + 3] = softplusf_(t[0] + Pk[k.bsig]);
-        });
+        // σ on MFMA (narrow_mm), the 8 waves' partials summed in wave order
+        narrow_mm<HW / 16 / 8>(P16 + k.Fnar16 + narrow_off(0), 0, smem, lane, w, part);
+        __syncthreads();
+        if (tid < TM) {
+            float t = 0.f;
+            for (int v = 0; v < 8; ++v) t += part[(v * TM + tid) * 4];
+            ost[tid * OST_LD + 3] = softplusf_(t + Pk[k.bsig]);
+        }
+        __syncthreads();  // the semantic epilogue reuses part
         if (full) {
             // semantic hidden (256) → logits through W_m2 in the epilogue
             if (C > 0) {
@@ -320,15 +310,18 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
                 for (int v = 0; v < 8; ++v) s += part[(v * TM + r) * 4 + c];
                 ost[r * OST_LD + g.sem_col + c] = s + Pk[k.bm2 + c];
             }
-            // albedo from rgb1 (image chunks 32..63)
-            __builtin_amdgcn_sched_barrier(0);
-            dots16<3>(smem, w, lane, 32, 32, Pk + k.Wr2, HH, [&](int r, const float (&t)[3]) {
-                float rgb[3];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) rgb[c] = sigmoidf_(t[c] + Pk[k.br2 + c]);
-                if (lane < 3) ost[r * OST_LD + lane] = __fsub_rn(__fmul_rn(lane == 0 ? rgb[0] : (lane == 1 ? rgb[1] : rgb[2]), 1.002f), 0.001f);
-            });
+            // albedo from rgb1 (image k-steps 16..31) on MFMA
+            __syncthreads();  // the logits are read from part
+            narrow_mm<HH / 16 / 8>(P16 + k.Fnar16 + narrow_off(1), HH / 16, smem, lane, w, part);
             __syncthreads();  // rgb1 read before sun_v 2 overwrites the image's first half
+            if (tid < TM) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    float t = 0.f;
+                    for (int v = 0; v < 8; ++v) t += part[(v * TM + tid) * 4 + c];
+                    ost[tid * OST_LD + c] = __fsub_rn(__fmul_rn(sigmoidf_(t + Pk[k.br2 + c]), 1.002f), 0.001f);
+                }
+            }
             // sun_v 2 and 3 on image columns 0..255
             for (int l = 0; l < 2; ++l) {
                 f32x16 acc[1][NJ];
@@ -346,14 +339,18 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
                 });
                 __syncthreads();
             }
-            // sun visibility and the ray's sky colour
-            __builtin_amdgcn_sched_barrier(0);
-            dots16<1>(smem, w, lane, 0, 32, Pk + k.ws4, 0, [&](int r, const float (&t)[1]) {
-                const float sun = sigmoidf_(t[0] + Pk[k.bs4]);
-                const float sky = lane < 3 ? g.sky[(std::min<int64_t>(p0 + r, g.P - 1) / g.S) * 4 + lane] : 0.f;
-                if (lane == 0) ost[r * OST_LD + 4] = sun;
-                if (lane < 3) ost[r * OST_LD + 5 + lane] = sky;
-            });
+            // sun visibility (MFMA) and the ray's sky colour; part's albedo partials were read
+            // before the sun_v layers' barriers
+            narrow_mm<HH / 16 / 8>(P16 + k.Fnar16 + narrow_off(2), 0, smem, lane, w, part);
+            __syncthreads();
+            if (tid < TM) {
+                float t = 0.f;
+                for (int v = 0; v < 8; ++v) t += part[(v * TM + tid) * 4];
+                ost[tid * OST_LD + 4] = sigmoidf_(t + Pk[k.bs4]);
+                const float* sk = g.sky + (std::min<int64_t>(p0 + tid, g.P - 1) / g.S) * 4;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) ost[tid * OST_LD + 5 + c] = sk[c];
+            }
         }
         __syncthreads();
         // the tile's output rows, contiguous in HBM
@@ -374,6 +371,7 @@ bool heads_bf16_supported(const Dims& d) { return g_fused_heads && heads_bf16_sh
 
 int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes) {
     SPN_ARG(a.P >= 0 && a.S > 0 && a.NO <= OST_LD && a.C <= 4, "heads_bf16: bad sizes");
+    SPN_ARG(k.Fnar16 >= 0, "heads_bf16: narrow heads not packed");
     SPN_ARG(a.mode == 1 || (k.Ffeat16 >= 0 && k.FQ16 >= 0 && k.Fs2_16 >= 0 && k.Fs3_16 >= 0 && (a.C == 0 || k.Fsem16 >= 0)),
             "heads_bf16: weights not packed for the fused heads");
     if (a.P == 0) return SPNERF_OK;

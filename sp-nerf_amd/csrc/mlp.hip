@@ -33,9 +33,11 @@ struct PackPiece {
     // order (trunk_frag_off, dst_ld = the layer's padded K); 5 = the same for 32 features per
     // wave (frag_off NA = 1: the fused heads' 256-wide layers); 3 = split into bf16 planes
     // [hi | hi | lo | lo] of width dst_ld / 4 each (hi = bf16(v), lo = bf16(v − hi)); 4 = the
-    // same planes in the fused trunk's fragment order (dst_ld = 4·K0p)
+    // same planes in the fused trunk's fragment order (dst_ld = 4·K0p); 6 = a narrow head's
+    // [32][cols] hi/lo-row A operand (PackedOffs::Fnar16; rows = 32, nsrc source rows)
     int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;
     int64_t dst;
+    int nsrc = 0;  // bf = 6: source rows
 };
 constexpr int kMaxPieces = 64;
 constexpr int kPackTR = 32, kPackTC = 64;  // a block re-lays one 32 x 64 tile of a piece
@@ -83,6 +85,17 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     for (int e = 0; e < 8; ++e) {
         const int r = r0 + (tid >> 6) + 4 * e, c = c0 + (tid & 63);
         if (r >= pc.rows || c >= pc.cols) continue;
+        if (pc.bf == 6) {  // destination row r: source row sr's hi (r even) or lo (r odd) plane
+            const int sr = r < 2 ? 0 : r < 4 ? 1 : (r == 8 || r == 9) ? 2 : -1;
+            bf16 o = (bf16)0.f;
+            if (sr >= 0 && sr < pc.nsrc) {
+                const float v = pc.src[(int64_t)sr * pc.src_ld + pc.src_c0 + c];
+                const bf16 hi = (bf16)v;
+                o = (r & 1) ? (bf16)(v - (float)hi) : hi;
+            }
+            reinterpret_cast<bf16*>(a.packed)[pc.dst + frag_off(r, c, pc.dst_ld, 1)] = o;
+            continue;
+        }
         const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
         if (pc.bf == 3 || pc.bf == 4) {
             bf16* dst = reinterpret_cast<bf16*>(a.packed) + pc.dst;
@@ -942,6 +955,14 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
             SPN_TRY(piece(x.r1W, 0, H, W, k.FQ16 + (int64_t)H * W, W, 0, 2));  // rows H.. of Q (64-row waves)
             SPN_TRY(piece(x.s2W, 0, H, H, k.Fs2_16, H, 0, 5));
             SPN_TRY(piece(x.s3W, 0, H, H, k.Fs3_16, H, 0, 5));
+            auto narrow = [&](int pi, int nsrc, int K, int64_t dst) {
+                SPN_TRY(piece(pi, 0, 32, K, dst, K, 0, 6));
+                v.back().nsrc = nsrc;
+                return SPNERF_OK;
+            };
+            SPN_TRY(narrow(x.sigW, 1, W, k.Fnar16));
+            SPN_TRY(narrow(x.r2W, 3, H, k.Fnar16 + (int64_t)32 * W));
+            SPN_TRY(narrow(x.s4W, 1, H, k.Fnar16 + (int64_t)32 * (W + H)));
         }
     }
     return launch_pack(v, packed, s);

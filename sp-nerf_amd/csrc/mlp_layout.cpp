@@ -169,6 +169,7 @@ Packed packed_layout(const Dims& d) {
             k.FQ16 = take16((int64_t)2 * H * W);
             k.Fs2_16 = take16((int64_t)H * H);
             k.Fs3_16 = take16((int64_t)H * H);
+            k.Fnar16 = take16((int64_t)32 * (W + 2 * H));
         }
     }
     k.total = off;
