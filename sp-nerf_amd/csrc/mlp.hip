@@ -30,7 +30,7 @@ namespace spn {
 struct PackPiece {
     const float* src;
     // bf: 1 = bf16 destination (dst in bf16 units); 2 = bf16 in the fused trunk's MFMA fragment
-    // order (trunk_frag_off, dst_ld = the layer's padded K); 5 = the same for 32 features per
+    // order (trunk_frag_off, dst_ld = the layer's padded K; transposed: element [c][r]); 5 = the same for 32 features per
     // wave (frag_off NA = 1: the fused heads' 256-wide layers); 3 = split into bf16 planes
     // [hi | hi | lo | lo] of width dst_ld / 4 each (hi = bf16(v), lo = bf16(v − hi)); 4 = the
     // same planes in the fused trunk's fragment order (dst_ld = 4·K0p); 6 = a narrow head's
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
     const int tcols = (pc.cols + kPackTC - 1) / kPackTC;
     const int r0 = (t / tcols) * kPackTR, c0 = (t % tcols) * kPackTC;
     const int tid = threadIdx.x;
-    if (pc.transpose && pc.bf <= 1) {
+    if (pc.transpose && pc.bf <= 2) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const int rr = (tid >> 6) + 4 * e, cc = tid & 63;
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             const int rr = tid & 31, cc = (tid >> 5) + 8 * e;
             const int r = r0 + rr, c = c0 + cc;
             if (r < pc.rows && c < pc.cols) {
-                const int64_t o = pc.dst + (int64_t)c * pc.dst_ld + r;
+                const int64_t o = pc.dst + (pc.bf == 2 ? trunk_frag_off(c, r, pc.dst_ld) : (int64_t)c * pc.dst_ld + r);
                 if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)tileT[cc][rr];
                 else a.packed[o] = tileT[cc][rr];
             }
@@ -929,6 +929,7 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
             SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wt16[i], k.Kp[i], 0, 1));
             SPN_TRY(piece(x.fcW[i], 0, W, W, k.WTt16[i], W, 1, 1));
             if (k.Wf16[i] >= 0) SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wf16[i], k.Kp[i], 0, 2));
+            if (k.Wb16[i] >= 0) SPN_TRY(piece(x.fcW[i], 0, W, W, k.Wb16[i], W, 1, 2));
         }
         if (d.sem) {
             SPN_TRY(piece(x.m1W, 0, H, W, k.WG16 + (int64_t)W * W, W, 0, 1));
@@ -1489,22 +1490,45 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     }
     // 6. trunk, top to bottom
     const T* X0 = BF ? buf(c.w.X0b) : buf(c.w.X0);
-    for (int i = d.L - 1; i >= 0; --i) {
-        // dZ (buffer cur) holds dL/d(pre-activation of layer i); the side stream has it.  The
-        // input of layer i >= 2 is saved as Z (option zsave): staged as sin(Z) by the TN
+    // layer i's weight gradient (and the per-ray sums of its dZ at layer 0 / the skip layer)
+    auto layer_grads = [&](int i, const T* dZi) -> int32_t {
+        // dZi holds dL/d(pre-activation of layer i).  The input of layer i >= 2 is saved as Z
+        // (option zsave): staged as sin(Z) by the TN
         const bool zin = zs && i >= 2;
         const T* In = i == 0 ? X0 : buf(zin ? c.w.Db[i - 1] : c.w.Hb[i - 1]);
         const int ldin = i == 0 ? d.K0p : W;
         const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
         if (i == d.skip)
-            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, W, X0, d.K0p, W, W + d.K0p, s2,
+            SPN_TRY(tn_grad<T>(c, dZi, W, W, In, W, X0, d.K0p, W, W + d.K0p, s2,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
         else
-            SPN_TRY(tn_grad<T>(c, dZ, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s2,
+            SPN_TRY(tn_grad<T>(c, dZi, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s2,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
-        if (d.sem && (i == 0 || i == d.skip)) {
-            SPN_TRY(ray_rowsum<T>(dZ, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
+        if (d.sem && (i == 0 || i == d.skip))
+            SPN_TRY(ray_rowsum<T>(dZi, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
+        return SPNERF_OK;
+    };
+    if (BF && !zs && g_fused_bwd && !c.k.Wb16.empty() && c.k.Wb16[1] >= 0) {
+        // the whole dX chain in one launch (k_trunk_bwd_bf16): dZ_{i-1} overwrites D_{i-1} in
+        // place (the workspace serves one backward: spnerf_mlp_backward consumes it), then the
+        // weight gradients of every layer
+        TrunkBwdArgs a;
+        a.dZtop = reinterpret_cast<const bf16*>(dZ);
+        for (int i = 1; i < d.L; ++i) {
+            a.Wb[i] = c.pk16(c.k.Wb16[i]);
+            a.D[i - 1] = c.hb(c.w.Db[i - 1]);
+            a.dZ[i - 1] = c.hb(c.w.Db[i - 1]);
         }
+        a.P = P; a.L = d.L;
+        // algorithmic HBM bytes: dZ_{L-1} in, per layer D_{i-1} in and dZ_{i-1} out
+        SPN_TRY(trunk_bwd_bf16(a, s, 2.0 * P * W * W * (d.L - 1), 2.0 * P * W * (1.0 + 2.0 * (d.L - 1))));
+        SPN_TRY(stream_dep(sd, s, s2));
+        for (int i = d.L - 1; i >= 0; --i) SPN_TRY(layer_grads(i, i == d.L - 1 ? dZ : buf(c.w.Db[i])));
+        return SPNERF_OK;
+    }
+    for (int i = d.L - 1; i >= 0; --i) {
+        // dZ (buffer cur) holds dL/d(pre-activation of layer i); the side stream has it
+        SPN_TRY(layer_grads(i, dZ));
         if (sd && s2 != s) {   // this layer's reads of buffer `cur` are issued on s2
             tn_done[i] = sd->ev[sd->next];
             sd->next = (sd->next + 1) % 64;
@@ -1621,6 +1645,7 @@ static int* option_slot(const char* name) {
     if (n == "zsave") return &g_zsave;
     if (n == "pe_inline") return &g_pe_inline;
     if (n == "tn_split_tail") return &g_tn_split_tail;
+    if (n == "fused_bwd") return &g_fused_bwd;
     return nullptr;
 }
 

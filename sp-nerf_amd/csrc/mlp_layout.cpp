@@ -153,6 +153,7 @@ Packed packed_layout(const Dims& d) {
             k.Wt16.push_back(i == 0 ? -1 : take16((int64_t)W * k.Kp[i]));
             k.WTt16.push_back(i == 0 ? -1 : take16((int64_t)W * W));
             k.Wf16.push_back(!fused ? -1 : take16((int64_t)W * (i == 0 ? 4 * k.Kp[0] : k.Kp[i])));
+            k.Wb16.push_back(!fused || i == 0 ? -1 : take16((int64_t)W * W));
         }
         k.WG16 = take16((int64_t)d.NG * W);
         k.WGT16 = take16((int64_t)W * d.NG);

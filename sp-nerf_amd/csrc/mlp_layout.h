@@ -71,6 +71,8 @@ struct Packed : PackedOffs {
     std::vector<int64_t> Wt16, WTt16;   // bf16 trunk layers 1.. (bf16 units), -1 for layer 0
     std::vector<int64_t> Wf16;          // the same in MFMA fragment order for the fused trunk (-1: none);
                                         // layer 0: the split planes [hi | hi | lo | lo], K = 4·K0p
+    std::vector<int64_t> Wb16;          // W_i[:, :W]ᵀ in fragment order (Kp = W) for the fused backward
+                                        // dX chain (k_trunk_bwd_bf16); -1 for layer 0 / none
 };
 Packed packed_layout(const Dims& d);
 

@@ -51,6 +51,22 @@ struct TrunkArgs {
     int rs = 0, dir_off = 0, n_freq = 0, K0 = 0;
 };
 
+// Backward dX chain of the bf16 trunk in one persistent launch (k_trunk_bwd_bf16): from
+// dZ_{L-1} (dL/d pre-activation of the last trunk layer, [P][512] bf16) down to dZ_0, each
+// dZ_{i-1} = (dZ_i · W_i[:, :512]) ⊙ D_{i-1} with the point tile's dZ resident in LDS between
+// layers (models/spnerf.py:323-330 differentiated; the skip layer's PE columns get no gradient).
+// Wb[i] = W_i[:, :512]ᵀ in the forward trunk's fragment order (trunk_frag_off, Kp = 512).
+// dZ[i] may alias D[i] (a tile reads its D rows before it writes its dZ rows).
+struct TrunkBwdArgs {
+    const bf16* dZtop = nullptr;
+    const bf16* Wb[kTrunkMaxL] = {};
+    const bf16* D[kTrunkMaxL] = {};
+    bf16* dZ[kTrunkMaxL] = {};
+    int64_t P = 0;
+    int L = 0;
+    int dbg = 0;  // g_trunk_dbg (profiling ablations, outputs invalid): 1 = no dZ copy-outs, 2 = no D loads
+};
+
 // Offset (bf16 elements) of W[n][k] of a [512][Kp] layer in MFMA A-fragment order: wave w =
 // n / 64 streams k-steps of 16; per k-step its two 32-feature tiles are 1 KB each, lane
 // (n % 32) + 32·((k / 8) % 2) holding 8 consecutive k.
@@ -111,5 +127,7 @@ bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 // layer 0 inside the launch (TrunkArgs::X0) for this PE width when saving / not saving
 bool trunk_l0_supported(int K0p, bool save);
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes);
+int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes);
+extern int g_fused_bwd;  // 1 = the bf16 training backward runs its dX chain in k_trunk_bwd_bf16
 
 }  // namespace spn

@@ -400,6 +400,196 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     }
 }
 
+// Backward dX chain (TrunkBwdArgs): the 64-point tiling of the training forward run top to
+// bottom.  The LDS image holds the tile's dZ_i (B operand); the weights Wb[i] = W_iᵀ stream from
+// L2 as the A operand through the same register ring; the epilogue multiplies the fp32
+// accumulator by D_{i-1} and rounds to bf16 — the ×Dmul epilogue of the layer-by-layer dX GEMMs
+// over the same k order, so dZ_{i-1} equals theirs bit for bit.  The tile's D_{i-1} rows load
+// (coalesced 1-KB rows, in registers) while layer i's k-loop runs and land in a second LDS image
+// before the epilogue; dZ_i leaves for HBM (the weight gradients read it) behind the NEXT
+// layer's MFMAs, which read the same image.  Per point and layer: 1 KB of D in, 1 KB of dZ out
+// (the layer-by-layer GEMM also re-reads dZ_i: 3 KB).
+__global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntiles) {
+    using Geo = TrunkGeo<64>;
+    constexpr int TMt = 64, NJ = Geo::NJ, IMG = Geo::IMG, CPT = Geo::CPT, TPD = Geo::TPD;
+    constexpr int nks = TW / 16;
+    __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
+    const int sw = r32 & 15;
+    typedef const __attribute__((address_space(4))) TrunkBwdArgs* KArgs;
+    const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+
+    u32x4 ring[TPD][2];
+    auto wstream = [&](int i) { return ka->Wb[i] + trunk_wave_off(w, nks) + lane * 8; };
+    auto prime = [&](int i) {
+        const bf16* src = wstream(i);
+#pragma unroll
+        for (int d = 0; d < TPD; ++d) {
+            ring[d][0] = ldg16(src + d * kTrunkKStride);
+            ring[d][1] = ldg16(src + d * kTrunkKStride + 512);
+        }
+    };
+    auto copy_out = [&](bf16* dst, int64_t p0, int q0, auto kn) {
+        constexpr int n = decltype(kn)::value;
+        const int ct = opaque(tid);
+        u32x4 v[n];
+#pragma unroll
+        for (int q = 0; q < n; ++q) {
+            const int c = ct + 512 * (q0 + q);
+            v[q] = *reinterpret_cast<const u32x4*>(smem + act_off(c >> 6, c & 63));
+        }
+#pragma unroll
+        for (int q = 0; q < n; ++q) {
+            const int c = ct + 512 * (q0 + q);
+            if (p0 + (c >> 6) < g.P) *reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8) = v[q];
+        }
+    };
+
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    if (tile >= ntiles) return;  // block-uniform
+    prime(g.L - 1);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t p0 = (int64_t)tile * TMt;
+        {
+            const int st = opaque(tid);
+#pragma unroll
+            for (int q0 = 0; q0 < CPT; q0 += 8) {
+                u32x4 v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int c = st + 512 * (q0 + q);
+                    v[q] = ldg16(g.dZtop + std::min<int64_t>(p0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int c = st + 512 * (q0 + q);
+                    *reinterpret_cast<u32x4*>(smem + act_off(c >> 6, c & 63)) = v[q];
+                }
+            }
+        }
+        // this tile's D_{l} rows (rows past P: a clamped row), in registers until the k-loop of
+        // layer l + 1 has run.  They are issued BEFORE the epilogue that precedes that k-loop:
+        // vmcnt retires in order, so the weight refills issued after them are only usable once
+        // the D rows are in — the epilogue plus TPD k-steps cover that HBM latency
+        u32x4 dv[CPT];
+        auto load_d = [&](int l) {
+            const int st = opaque(tid);
+            const bf16* dsrc = ka->D[l];
+            if (g.dbg & 2) return;
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                const int c = st + 512 * q;
+                dv[q] = ldg16(dsrc + std::min<int64_t>(p0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
+            }
+        };
+        load_d(g.L - 2);
+        bf16* pend = nullptr;  // dZ_i of the layer whose k-loop runs: copied out during it
+        for (int i = g.L - 1; i >= 1; --i) {
+            const bf16* wsrc = wstream(i);
+            f32x16 acc[2][NJ];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[a][j][r] = 0.f;
+            __syncthreads();  // the dZ_i image is complete; the D image is free
+            const char* brow = smem + r32 * 1024;
+            bf16x8 bc[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
+#pragma unroll 1
+            for (int ks0 = 0; ks0 < nks; ks0 += TPD) {
+#pragma unroll
+                for (int d = 0; d < TPD; ++d) {
+                    const int ks = ks0 + d;
+                    const int offn = ((2 * (ks + 1) + h) ^ sw) << 4;
+                    bf16x8 bn[NJ];
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
+                    const bf16x8 a0 = __builtin_bit_cast(bf16x8, ring[d][0]);
+                    const bf16x8 a1 = __builtin_bit_cast(bf16x8, ring[d][1]);
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bc[j], acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bc[j], acc[1][j], 0, 0, 0);
+                    }
+                    const int kn = std::min(ks + TPD, nks - 1);
+                    ring[d][0] = ldg16(wsrc + kn * kTrunkKStride);
+                    ring[d][1] = ldg16(wsrc + kn * kTrunkKStride + 512);
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) bc[j] = bn[j];
+                }
+                constexpr int per = CPT / (nks / TPD);
+                static_assert(per * (nks / TPD) == CPT && per >= 1, "copy slices");
+                if (pend && !(g.dbg & 1)) copy_out(pend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+            }
+            {
+                const int st = opaque(tid);
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) {
+                    const int c = st + 512 * q;
+                    *reinterpret_cast<u32x4*>(smem + IMG + act_off(c >> 6, c & 63)) = dv[q];
+                }
+            }
+            // the next layer's (or the next tile's top layer's) first k-steps load during the epilogue
+            const int inext = i > 1 ? i - 1 : (tile + (int)gridDim.x < ntiles ? g.L - 1 : -1);
+            if (inext >= 0) prime(inext);
+            if (i > 1) load_d(i - 2);  // block-uniform
+            __syncthreads();  // every wave is done reading dZ_i; the D image is complete
+            {
+                const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) {
+                            const int row = 32 * j + er32;
+                            const int o = act_off(row, f0 >> 3) + 8 * eh;
+                            const f32x4 dm = ld4(reinterpret_cast<const bf16*>(smem + IMG + o));
+                            float v[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] * dm[e];
+                            *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+            }
+            pend = ka->dZ[i - 1];
+        }
+        __syncthreads();  // dZ_0 is complete
+#pragma unroll
+        for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(pend, p0, q0, std::integral_constant<int, 4>{});
+        __syncthreads();  // the next tile restages the image
+    }
+}
+
+int g_fused_bwd = 1;
+
+int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes) {
+    SPN_ARG(a.P >= 0 && a.L >= 2 && a.L <= kTrunkMaxL, "trunk_bwd_bf16: bad sizes (P=%lld L=%d)", (long long)a.P, a.L);
+    if (a.P == 0) return SPNERF_OK;
+    SPN_ARG(a.P < (1ll << 31) / TW, "trunk_bwd_bf16: too many points (%lld)", (long long)a.P);
+    SPN_ARG(a.dZtop != nullptr, "trunk_bwd_bf16: NULL dZ_{L-1}");
+    for (int i = 1; i < a.L; ++i)
+        SPN_ARG(a.Wb[i] && a.D[i - 1] && a.dZ[i - 1], "trunk_bwd_bf16: NULL pointer at layer %d", i);
+    const int ntiles = cdiv(a.P, 64);
+    TrunkBwdArgs ad = a;
+    ad.dbg = g_trunk_dbg;
+    ProfScope prof("trunk_bwd_bf16", s, flop, bytes);
+    hipLaunchKernelGGL(k_trunk_bwd_bf16, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
 bool trunk_bf16_supported(int W, int L, int skip, int K0p) {
     return W == TW && L >= 2 && L <= kTrunkMaxL && K0p <= 64 && K0p % 16 == 0 && skip < L;
 }

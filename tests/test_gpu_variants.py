@@ -58,12 +58,12 @@ def test_fp32_gemm_variants_bitwise_equal(opts):
         assert torch.equal(g0[k], g1[k]), (opts, k)
 
 
-def _render_bf16(opts, n=300):
+def _render_bf16(opts, n=300, ns=64):
     old = {k: _lib.get_option(k) for k in opts}
     for k, v in opts.items():
         _lib.set_option(k, v)
     try:
-        args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+        args = gu.args_of({"args": dict(n_samples=ns, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
                                         sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
         rays = torch.tensor(gu_rays(n, 22), device=DEV)
         g = torch.Generator(device="cpu").manual_seed(5)
@@ -114,3 +114,18 @@ def test_bf16_skip_layer_tail_split_agrees():
     for k in g1:
         scale = g1[k].abs().max().item()
         assert (g1[k] - g2[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
+
+
+@pytest.mark.parametrize("n,ns", [(300, 64), (301, 40)])
+def test_bf16_fused_backward_bitwise_equal(n, ns):
+    """The fused backward dX chain (k_trunk_bwd_bf16, option fused_bwd) multiplies each layer's
+    fp32 accumulator by D over the same k order as the layer-by-layer x Dmul GEMMs: every dZ, so
+    every gradient, is bit-identical.  301 x 80 points leave a ragged last 64-point tile."""
+    r0, g0 = _render_bf16({"fused_bwd": 0}, n=n, ns=ns)
+    r1, g1 = _render_bf16({"fused_bwd": 1}, n=n, ns=ns)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    assert sorted(g0) == sorted(g1)
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        assert torch.equal(g0[k], g1[k]), k
