@@ -1,5 +1,9 @@
+# C4 at a small global batch (default 512 rays: the per-rank work of 8 GPUs) under library
+# options, pairs in one call:  GB=512 bash tools/ab512.sh "fused_bwd=0" "fused_bwd=1" ...
 cd $GRAFT_REPO_ROOT
-for o in "fused_bwd=0" "fused_bwd=1"; do
-r=$(timeout -k 10 200 python bench.py --config c4 --global-batch 512 --steps 30 --warmup 5 --no-cpu-baseline --no-secondary --option $o 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernels', {}); print(round(d['ms_per_step'],3), {c: (round(v['ms_per_step'],3), v['launches']) for c, v in k.items()})")
-echo "c4@512 [$o] $r"
+GB=${GB:-512}
+for o in "$@"; do
+args=""; for kv in $o; do args="$args --option $kv"; done
+r=$(timeout -k 10 200 python bench.py --config c4 --global-batch $GB --steps 30 --warmup 5 --no-cpu-baseline --no-secondary $args 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernels', {}); print(round(d['ms_per_step'],3), {c: (round(v['ms_per_step'],3), v['launches']) for c, v in k.items() if v['ms_per_step'] > 0.05})")
+echo "c4@$GB [$o] $r"
 done
