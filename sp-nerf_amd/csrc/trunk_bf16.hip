@@ -132,13 +132,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
-    // the ring may be primed in two parts: [0, PH) beside the live accumulators of the
-    // epilogue, the rest after it (an 8-deep ring primed that way measured slower than 4)
-    constexpr int PH = TPD;
-    using I0 = std::integral_constant<int, 0>;
-    using IPH = std::integral_constant<int, PH>;
-    using ITPD = std::integral_constant<int, TPD>;
-    prime(first, I0{}, ITPD{});
+    prime(first, std::integral_constant<int, 0>{}, std::integral_constant<int, TPD>{});
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TMt;
         const int st = opaque(tid);
@@ -207,6 +201,14 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             const bool skip = i == g.skip;
             const bf16* wsrc = wstream(i);
             const int nks = nks_of(i);
+            // the ring runs on into the next layer's (or the next tile's first layer's) stream:
+            // once slot d has served this layer's last k-step in it, it loads the next layer's
+            // k-step d (past the last tile: this layer's step d again, unused).  Priming after the
+            // k-loop instead reloaded registers whose refills were still in flight, and hipcc
+            // drained vmcnt(0) — every refill and H / D copy-out store — before each epilogue
+            const bool last = i == g.L - 1;
+            const int inext = last ? (tile + (int)gridDim.x < ntiles ? first : -1) : i + 1;
+            const bf16* wnxt = inext >= 0 ? wstream(inext) : wsrc;
             const int nkm = i == 0 ? nk0 : nmain;  // k-steps over the image
             float* sb = sbias + (i & 1) * TW;  // slot (i-1)&1 may still be read by the previous epilogue
             sb[tid] = ka->bias[i][tid];
@@ -249,10 +251,10 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                     }
                     // refill the slot just consumed, right behind its MFMAs (TPD - 1 steps of
                     // cover); past the stream's end: re-read its last step
-                    const int kn = std::min(ks + TPD, nks - 1);
                     if constexpr (!NOW) {
-                        ring[d][0] = ldg16(wsrc + kn * kTrunkKStride);
-                        ring[d][1] = ldg16(wsrc + kn * kTrunkKStride + 512);
+                        const bf16* src = ks + TPD < nks ? wsrc + (ks + TPD) * kTrunkKStride : wnxt + d * kTrunkKStride;
+                        ring[d][0] = ldg16(src);
+                        ring[d][1] = ldg16(src + 512);
                     }
                     // order: (1 image read, 2 MFMAs) x NJ, then the 2 weight loads
 #pragma unroll
@@ -288,13 +290,11 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                             acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[j], acc[0][j], 0, 0, 0);
                             acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[j], acc[1][j], 0, 0, 0);
                         }
+                        ring[d][0] = ldg16(wnxt + d * kTrunkKStride);  // ks + TPD >= nks here
+                        ring[d][1] = ldg16(wnxt + d * kTrunkKStride + 512);
                     }
                 }
             }
-            // the next layer's (or the next tile's layer-1) first k-steps load during the epilogue
-            const bool last = i == g.L - 1;
-            const int inext = last ? (tile + (int)gridDim.x < ntiles ? first : -1) : i + 1;
-            if (inext >= 0) prime(inext, I0{}, IPH{});
 
             __syncthreads();  // every wave is done reading the images of layer i
             bf16* Hs = ka->Hs[i];
@@ -392,9 +392,6 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 }
                 hpend = last ? nullptr : Hs;
             }
-            if constexpr (PH < TPD) {
-                if (inext >= 0) prime(inext, IPH{}, ITPD{});
-            }
         }
         __syncthreads();  // the next tile restages the image and reuses the bias slots
     }
@@ -486,6 +483,9 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
         bf16* pend = nullptr;  // dZ_i of the layer whose k-loop runs: copied out during it
         for (int i = g.L - 1; i >= 1; --i) {
             const bf16* wsrc = wstream(i);
+            // the next layer's (or the next tile's top layer's) stream: the ring runs on into it
+            // during this k-loop's last TPD steps
+            const int inext = i > 1 ? i - 1 : (tile + (int)gridDim.x < ntiles ? g.L - 1 : -1);
             f32x16 acc[2][NJ];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -500,6 +500,13 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
             for (int j = 0; j < NJ; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
 #pragma unroll 1
             for (int ks0 = 0; ks0 < nks; ks0 += TPD) {
+                // refill source of this slice's slots (block-uniform): k-steps ks0 + TPD + d of this
+                // layer, past its end the next layer's k-steps d (after the last tile: this
+                // layer's last slice again, unused).  A refill issued after the k-loop instead
+                // (into registers whose previous loads were still in flight) made hipcc drain
+                // vmcnt(0) — every weight refill and dZ store of the layer — before each epilogue
+                const bf16* rsrc = ks0 + TPD < nks ? wsrc + (ks0 + TPD) * kTrunkKStride
+                                                   : (inext >= 0 ? wstream(inext) : wsrc + (nks - TPD) * kTrunkKStride);
 #pragma unroll
                 for (int d = 0; d < TPD; ++d) {
                     const int ks = ks0 + d;
@@ -514,9 +521,8 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
                         acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bc[j], acc[0][j], 0, 0, 0);
                         acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bc[j], acc[1][j], 0, 0, 0);
                     }
-                    const int kn = std::min(ks + TPD, nks - 1);
-                    ring[d][0] = ldg16(wsrc + kn * kTrunkKStride);
-                    ring[d][1] = ldg16(wsrc + kn * kTrunkKStride + 512);
+                    ring[d][0] = ldg16(rsrc + d * kTrunkKStride);
+                    ring[d][1] = ldg16(rsrc + d * kTrunkKStride + 512);
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -538,9 +544,6 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
                     *reinterpret_cast<u32x4*>(smem + IMG + act_off(c >> 6, c & 63)) = dv[q];
                 }
             }
-            // the next layer's (or the next tile's top layer's) first k-steps load during the epilogue
-            const int inext = i > 1 ? i - 1 : (tile + (int)gridDim.x < ntiles ? g.L - 1 : -1);
-            if (inext >= 0) prime(inext);
             if (i > 1) load_d(i - 2);  // block-uniform
             __syncthreads();  // every wave is done reading dZ_i; the D image is complete
             {
