@@ -11,8 +11,9 @@
 //    second image for D = cos, the [TMt][K0p] PE tile of the skip layer, two bias slots.
 //  * Weights stream from L2 (every CU walks the same 512 KB per layer), packed by
 //    spnerf_pack_params in MFMA fragment order (trunk_frag_off): wave w's A fragments of k-step
-//    ks are one contiguous 2 KB, loaded TPD k-steps ahead into a register ring.  The next
-//    layer's first k-steps load during the current layer's epilogue.
+//    ks are one contiguous 2 KB, loaded TPD k-steps ahead into a register ring that runs on
+//    from one layer's stream into the next one's (and into the next tile's first layer), so the
+//    next layer's first k-steps are in flight through the epilogue.
 //  * 8 waves; wave w owns output features [64w, 64w + 64) of all TMt points (2 x TMt/32 tiles).
 //  * Epilogue = the unfused k_gemm_nt_bf16 arithmetic (fp32 accumulator + bias (+ the per-ray
 //    semantic rows at the skip layer), fast_sincos, bf16 rounding) over the same k-order, so the
