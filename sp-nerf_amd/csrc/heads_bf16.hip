@@ -291,15 +291,22 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
                 int rrel[NJ];
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) rrel[j] = (int)(std::min<int64_t>(p0 + 32 * j + er32, g.P - 1) / g.S - ray0);
-                epi(std::integral_constant<int, 2>{}, acc, [&](int, int j, int, int f0, int row, const float (&v)[4]) {
-                    const f32x4 bv = ld4(Pk + k.bQ + f0);
-                    const f32x4 rv = rq_lds ? *reinterpret_cast<const f32x4*>(srq + rrel[j] * (2 * HH) + f0)
-                                            : ld4(g.rbQ + (ray0 + rrel[j]) * (2 * HH) + f0);
-                    float y[4];
+                // two instances of the epilogue (block-uniform choice): one select between the LDS
+                // and the global row made hipcc emit a flat load, waited with vmcnt(0) lgkmcnt(0)
+                // per 4 outputs
+                auto qepi = [&](auto klds) {
+                    epi(std::integral_constant<int, 2>{}, acc, [&](int, int j, int, int f0, int row, const float (&v)[4]) {
+                        const f32x4 bv = ld4(Pk + k.bQ + f0);
+                        const f32x4 rv = decltype(klds)::value ? *reinterpret_cast<const f32x4*>(srq + rrel[j] * (2 * HH) + f0)
+                                                               : ld4(g.rbQ + (ray0 + rrel[j]) * (2 * HH) + f0);
+                        float y[4];
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) y[e] = fast_sin((v[e] + bv[e]) + rv[e]);
-                    put4(row, f0, y);
-                });
+                        for (int e = 0; e < 4; ++e) y[e] = fast_sin((v[e] + bv[e]) + rv[e]);
+                        put4(row, f0, y);
+                    });
+                };
+                if (rq_lds) qepi(std::true_type{});
+                else qepi(std::false_type{});
                 __syncthreads();
             }
             // semantic logits: the 8 waves' partials in wave order
