@@ -77,7 +77,9 @@ int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed,
                            void* workspace, float* out, void* stream);
 /* Gradients of sum(d_out * out) w.r.t. every parameter, written (overwritten, or added with
  * SPNERF_MLP_ACCUMULATE in `flags`) into `grad_flat` (canonical order, torch shapes,
- * contiguous) and w.r.t. t_emb (n_rays, t_dim, overwritten). */
+ * contiguous) and w.r.t. t_emb (n_rays, t_dim, overwritten).  The workspace of a SAVE forward
+ * serves ONE backward: the bf16 MLP's fused dX chain (option fused_bwd) writes the trunk's
+ * pre-activation gradients over the saved derivatives. */
 int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed,
                             const float* rays, int32_t ray_stride, int64_t n_rays, int32_t n_samples,
                             const int64_t* labels, const float* t_emb, int32_t flags,
