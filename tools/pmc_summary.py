@@ -9,15 +9,20 @@ import sys
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc16"
 data, meta = collections.defaultdict(dict), {}
 for f in sorted(glob.glob(os.path.join(root, "p*", "p_counter_collection.csv"))):
+    # each pass is its own run of the same command (same dispatch sequence): a counter's value sums
+    # its per-instance rows within one pass; counters another pass collected already are not re-added
+    have = {d: set(c) for d, c in data.items()}
     for r in csv.DictReader(open(f)):
         d = int(r["Dispatch_Id"])
+        if r["Counter_Name"] in have.get(d, ()):
+            continue
         data[d][r["Counter_Name"]] = data[d].get(r["Counter_Name"], 0) + float(r["Counter_Value"])
-        meta[d] = (r["Kernel_Name"], int(r["Grid_Size"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        meta.setdefault(d, (r["Kernel_Name"], int(r["Grid_Size"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
 seen = set()
 for d in sorted(data):
     name, grid, dur = meta[d]
     short = name.split("(")[0].replace("void spn::", "").replace("spn::", "")
-    if "gemm" not in short or grid < 100000 or (short, grid) in seen:
+    if not ("gemm" in short or "trunk" in short) or grid < 100000 or (short, grid) in seen:
         continue
     seen.add((short, grid))
     c = data[d]
