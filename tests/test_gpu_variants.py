@@ -116,11 +116,12 @@ def test_bf16_skip_layer_tail_split_agrees():
         assert (g1[k] - g2[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
 
 
-@pytest.mark.parametrize("n,ns", [(300, 64), (301, 40)])
+@pytest.mark.parametrize("n,ns", [(300, 64), (301, 40), (1, 16)])
 def test_bf16_fused_backward_bitwise_equal(n, ns):
     """The fused backward dX chain (k_trunk_bwd_bf16, option fused_bwd) multiplies each layer's
     fp32 accumulator by D over the same k order as the layer-by-layer x Dmul GEMMs: every dZ, so
-    every gradient, is bit-identical.  301 x 80 points leave a ragged last 64-point tile."""
+    every gradient, is bit-identical.  301 x 80 points leave a ragged last 64-point tile; one ray of
+    32 points is a single, half-empty tile."""
     r0, g0 = _render_bf16({"fused_bwd": 0}, n=n, ns=ns)
     r1, g1 = _render_bf16({"fused_bwd": 1}, n=n, ns=ns)
     for k in r0:
