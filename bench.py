@@ -50,7 +50,9 @@ GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt_w (fp32 MFMA, 256x128 persistent tile
                 "gemm_nt_bf16": ("k_gemm_nt_bf16d (bf16 MFMA, 256x256 persistent tiles, LDS-DMA ring across tiles)",
                                  BF16_MFMA_PEAK_TFLOPS),
                 "gemm_tn_bf16": ("k_gemm_tn_bf16d (bf16 MFMA, weight gradients, LDS-DMA)", BF16_MFMA_PEAK_TFLOPS),
-                "trunk_bf16": ("k_trunk_bf16 (fused bf16 trunk, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
+                "trunk_bf16": ("k_trunk_bf16<128> (fused bf16 trunk, inference tiles, LDS-resident activations)",
+                               BF16_MFMA_PEAK_TFLOPS),
+                "trunk_bf16_train": ("k_trunk_bf16<64> (fused bf16 trunk, training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
                 "trunk_bwd_bf16": ("k_trunk_bwd_bf16 (fused bf16 backward dX chain, LDS-resident dZ)", BF16_MFMA_PEAK_TFLOPS),
                 "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS)}
 
@@ -642,7 +644,7 @@ def run_train(a, config, rank, world, dev, secondary=False):
     _lib.prof_enable(False)
 
     kernels = {}
-    for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "trunk_bf16", "trunk_bwd_bf16", "tn_skinny", "encode", "heads_fwd",
+    for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "trunk_bf16", "trunk_bf16_train", "trunk_bwd_bf16", "tn_skinny", "encode", "heads_fwd",
               "heads_bwd", "heads_fused", "composite_fwd", "composite_bwd", "sample_guided", "render_loss", "pack", "adam"):
         s = _lib.prof_read(k)
         if s["launches"]:

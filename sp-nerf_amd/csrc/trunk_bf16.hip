@@ -622,7 +622,9 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     ad.dbg = g_trunk_dbg;
     ad.nt = g_trunk_nt & 1;
     const int ntiles = cdiv(a.P, tm);
-    ProfScope prof("trunk_bf16", s, flop, bytes);
+    // the saving 64-point tiling (training) is its own profiling class: its roofline (HBM-heavy,
+    // H and D of every layer out) is not the inference tiling's (MFMA-bound)
+    ProfScope prof(tm == 64 ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
     if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);

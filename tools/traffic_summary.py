@@ -13,7 +13,7 @@ src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_bench"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r02"
 CFGS = sys.argv[3:] or ["c4", "c5"]
 CLASSES = {"k_gemm_nt<": "gemm_nt_f32", "k_gemm_nt_w<": "gemm_nt_f32", "k_gemm_tn<": "gemm_tn_f32",
-           "k_gemm_nt_bf16": "gemm_nt_bf16", "k_gemm_tn_bf16": "gemm_tn_bf16", "k_trunk_bf16": "trunk_bf16",
+           "k_gemm_nt_bf16": "gemm_nt_bf16", "k_gemm_tn_bf16": "gemm_tn_bf16", "k_trunk_bf16<128": "trunk_bf16", "k_trunk_bf16<64": "trunk_bf16_train",
            "k_trunk_bwd_bf16": "trunk_bwd_bf16",
            "k_heads_bf16": "heads_fused", "k_composite_fwd": "composite_fwd"}
 for cfg in CFGS:

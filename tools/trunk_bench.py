@@ -42,7 +42,7 @@ def main():
     rays[:, 9] = 1.0
     z = torch.sort(torch.rand(B, S, device=dev), 1)[0].contiguous()
     lab = torch.randint(0, 3, (B,), device=dev)
-    classes = ["trunk_bf16", "gemm_nt_bf16", "gemm_nt_f32", "heads_fwd", "heads_fused", "encode"]
+    classes = ["trunk_bf16", "trunk_bf16_train", "gemm_nt_bf16", "gemm_nt_f32", "heads_fwd", "heads_fused", "encode"]
     for mode in ("save", "nosave", "sigma"):
         for fused in ((1,) if a.option else (1, 0)):
             _lib.set_option("fused_trunk", fused)
