@@ -514,6 +514,7 @@ def run_train(a, config, rank, world, dev, secondary=False):
     torch.manual_seed(0)
     model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"],
                               precision=c["precision"]).to(dev)
+    model.use_flat_grads()   # backward adds into one flat buffer: the .grads are its views (one all-reduce)
     params = list(model.parameters())
     if a.torch_adam:
         opt = torch.optim.Adam(params, lr=5e-4, fused=True)

@@ -10,6 +10,11 @@
 //   semantic SemanticLoss         λ_ss · Σ_{label ≠ -100} nll / n_valid            :162-183
 // Data parallelism (no reference counterpart): the CE mean runs over the GLOBAL batch's valid
 // labels (denominator n_valid_global / world), so the ranks' losses average to the global one.
+// Labels: -100 is ignored; any other label outside [0, C) — where torch's CrossEntropyLoss raises
+// (a device-side assert on the GPU) — makes the loss, its CE term and that ray's logit gradients
+// NaN (no host synchronisation; a graph-captured step cannot raise).  A global batch without a
+// valid label gives a NaN CE term as torch's mean over zero elements does, and zero logit
+// gradients.
 //
 // k_loss_rays: one wavefront per ray (S ≤ 256 samples, 4 per lane), a block of 4 waves walks a
 // fixed ray range and writes its partial sums — fixed order, deterministic.  k_loss_final: one
@@ -45,16 +50,16 @@ struct LossArgs {
 };
 
 constexpr int kLossWaves = 4;
-constexpr int kLossParts = 5;  // colour, sc2, sc3, depth, nll sum
+constexpr int kLossParts = 6;  // colour, sc2, sc3, depth, nll sum, out-of-range labels
 
 // per-ray quantities shared by the loss and its gradient
 struct RayLoss {
-    float col, sc2, sc3, dep, nll;
+    float col, sc2, sc3, dep, nll, bad;
     bool apply;
 };
 
 __device__ __forceinline__ RayLoss ray_loss(const LossArgs& a, int64_t r, int lane, float* sm_logit) {
-    RayLoss o{0.f, 0.f, 0.f, 0.f, 0.f, false};
+    RayLoss o{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, false};
     if (a.rgb) {
         float c = 0.f;
         if (lane < 3) {
@@ -89,6 +94,7 @@ __device__ __forceinline__ RayLoss ray_loss(const LossArgs& a, int64_t r, int la
     }
     if (a.logits) {
         const int64_t lab = a.labels[r];
+        if (lab != -100 && (lab < 0 || lab >= a.C)) o.bad = 1.f;
         if (lab != -100) {
             // log-softmax over C classes (lane c holds logit c; C ≤ 64)
             const float x = lane < a.C ? a.logits[r * a.C + lane] : -INFINITY;
@@ -108,10 +114,10 @@ __global__ __launch_bounds__(64 * kLossWaves) void k_loss_rays(LossArgs a) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t per = (a.B + a.nblocks - 1) / a.nblocks;
     const int64_t r0 = blockIdx.x * per, r1 = min(a.B, r0 + per);
-    float acc[kLossParts] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float acc[kLossParts] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int64_t r = r0 + wv; r < r1; r += kLossWaves) {
         const RayLoss o = ray_loss(a, r, lane, nullptr);
-        acc[0] += o.col; acc[1] += o.sc2; acc[2] += o.sc3; acc[3] += o.dep; acc[4] += o.nll;
+        acc[0] += o.col; acc[1] += o.sc2; acc[2] += o.sc3; acc[3] += o.dep; acc[4] += o.nll; acc[5] += o.bad;
     }
     if (lane == 0)
         for (int k = 0; k < kLossParts; ++k) part[wv][k] = acc[k];
@@ -126,7 +132,7 @@ __global__ __launch_bounds__(64 * kLossWaves) void k_loss_rays(LossArgs a) {
 __global__ __launch_bounds__(256) void k_loss_final(LossArgs a) {
     __shared__ float red[kLossParts + 1][256];
     const int t = threadIdx.x;
-    float s[kLossParts] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float s[kLossParts] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int b = t; b < a.nblocks; b += 256)
         for (int k = 0; k < kLossParts; ++k) s[k] += a.partial[b * 8 + k];
     float nv = 0.f;
@@ -148,7 +154,8 @@ __global__ __launch_bounds__(256) void k_loss_final(LossArgs a) {
         const float dep = a.lambda_ds > 0.f ? a.lambda_ds / 3.f * red[3][0] / B : 0.f;
         // CE mean over the global batch's valid labels, per rank: Σ nll / (n_valid_global / world)
         const float den = red[kLossParts][0] / (float)a.world;
-        const float ce = (a.logits && den > 0.f) ? a.lambda_ss * (red[4][0] / den) : 0.f;
+        float ce = 0.f;
+        if (a.logits) ce = (den > 0.f && red[5][0] == 0.f) ? a.lambda_ss * (red[4][0] / den) : NAN;
         a.result[1] = col; a.result[2] = sc2; a.result[3] = sc3; a.result[4] = dep; a.result[5] = ce;
         a.result[6] = den;
         a.result[0] = (((col + sc2) + sc3) + dep) + ce;
@@ -178,7 +185,8 @@ __global__ __launch_bounds__(64 * kLossWaves) void k_loss_grad(LossArgs a) {
         const int64_t lab = a.labels[r];
         const float den = a.result[6];
         float d = 0.f;
-        if (lab != -100 && den > 0.f) d = g * a.lambda_ss * (sm - (lane == lab ? 1.f : 0.f)) / den;
+        if (o.bad != 0.f) d = NAN;
+        else if (lab != -100 && den > 0.f) d = g * a.lambda_ss * (sm - (lane == lab ? 1.f : 0.f)) / den;
         a.d_logits[r * a.C + lane] = d;
     }
 }

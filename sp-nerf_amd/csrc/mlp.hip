@@ -1646,6 +1646,8 @@ static int* option_slot(const char* name) {
     if (n == "pe_inline") return &g_pe_inline;
     if (n == "tn_split_tail") return &g_tn_split_tail;
     if (n == "fused_bwd") return &g_fused_bwd;
+    if (n == "trunk2") return &g_trunk2;
+    if (n == "trunk2_tile") return &g_trunk2_tile;
     return nullptr;
 }
 

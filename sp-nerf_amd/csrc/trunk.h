@@ -127,6 +127,11 @@ bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 // layer 0 inside the launch (TrunkArgs::X0) for this PE width when saving / not saving
 bool trunk_l0_supported(int K0p, bool save);
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes);
+// the two-workgroups-per-CU tiling (trunk2_bf16.hip): D stored from the registers, 76 KB of LDS
+extern int g_trunk2;       // 0 = off, 1 = saving (training) launches, 2 = every launch
+extern int g_trunk2_tile;  // 64 or 128 points per tile
+bool trunk2_supported(const TrunkArgs& a, bool save);
+int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, double bytes);
 int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes);
 extern int g_fused_bwd;  // 1 = the bf16 training backward runs its dX chain in k_trunk_bwd_bf16
 

@@ -614,6 +614,8 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     SPN_ARG(a.P < (1ll << 31) / TW, "trunk_bf16: too many points (%lld)", (long long)a.P);
     bool save = false;
     for (int i = 1; i < a.L; ++i) save |= a.Ds[i] != nullptr;
+    SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0 && !save), "trunk_bf16: inline encoding needs z, rs, inference");
+    if (trunk2_supported(a, save)) return trunk2_bf16(a, s, save, flop, bytes);
     const int tm = a.zround ? 64 : trunk_tile(save);  // the 128-point tiling has no fp16-Z path
     SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0 && !save), "trunk_bf16: inline encoding needs z, rs, inference");
     SPN_ARG(!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, save)), "trunk_bf16: layer 0 unsupported for K0p=%d",

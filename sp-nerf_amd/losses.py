@@ -112,11 +112,14 @@ class DepthLoss(torch.nn.Module):
         if target_valid_depth is None:
             target_valid_depth = torch.ones(pd.shape[0], device=pd.device)
         B = float(target_valid_depth.shape[0])
-        pstd = (((z - pd.unsqueeze(-1)).pow(2) * pw).sum(-1)).sqrt()
+        var = ((z - pd.unsqueeze(-1)).pow(2) * pw).sum(-1)
         with torch.no_grad():
-            apply = (target_valid_depth > 0) & self.is_not_in_expected_distribution(pd, pstd, target_depth, target_std)
+            apply = (target_valid_depth > 0) & self.is_not_in_expected_distribution(pd, var.sqrt(), target_depth, target_std)
             m = apply.to(pd.dtype)
         if self.GNLL:
+            # σ_pred only on the applied rays (metrics.py:90-102 computes it for those alone): a
+            # ray left out with zero spread must not put sqrt'(0) = inf · 0 = NaN into the gradient
+            pstd = torch.where(apply, var, torch.ones_like(var)).sqrt()
             term = _gaussian_nll(pd, target_depth, torch.where(apply, pstd, torch.ones_like(pstd)))
         else:
             term = target_weight * (pd - target_depth) ** 2
@@ -246,6 +249,8 @@ class FusedRenderLoss(torch.nn.Module):
         if self.lambda_sc > 0:
             sun = inputs["sun_sc_coarse"]
             S = sun.shape[1]
+            if self.lambda_ds > 0 and inputs["z_vals_coarse"].shape[1] != S:
+                raise ValueError(f"FusedRenderLoss: sun_sc has {S} samples per ray, z_vals {inputs['z_vals_coarse'].shape[1]}")
             if sun.stride(1) != sun.stride(0) // S or sun.stride(0) % S:
                 sun = sun.contiguous()
             cfg.update(S=S, lambda_sc=self.lambda_sc, ld_sun=sun.stride(1), T_sc=f32(inputs["transparency_sc_coarse"]),
@@ -256,6 +261,8 @@ class FusedRenderLoss(torch.nn.Module):
             td = target_depths.float()
             if td.dim() != 2 or td.stride(1) != 1:
                 td = td.contiguous()
+            if target_valid_depth is None:   # metrics.py:83-86: every ray has a prior
+                target_valid_depth = torch.ones(B, dtype=torch.int64, device=dev)
             cfg.update(S=z.shape[1], lambda_ds=self.lambda_ds, z=z, w=f32(inputs["weights_coarse"].detach()), td=td,
                        tw=td[:, 1:], ld_td=td.stride(0), valid=target_valid_depth.reshape(-1).long().contiguous(),
                        tstd=f32(target_std.reshape(-1)))

@@ -132,6 +132,7 @@ class SPNeRF(torch.nn.Module):
         self._packed = None
         self._pack_pool = []
         self._flat_grad = None
+        self.flat_grads = False  # opt-in direct gradient path (use_flat_grads)
 
     # ---------------------------------------------------------------- library plumbing
     def cfg(self) -> _lib.ModelCfg:
@@ -212,12 +213,25 @@ class SPNeRF(torch.nn.Module):
         if buf is not None and buf is not self._packed and len(self._pack_pool) < 4:
             self._pack_pool.append(buf)
 
+    def use_flat_grads(self, on: bool = True) -> "SPNeRF":
+        """Opt in to the direct gradient path (the training loop's ``loss.backward()`` into
+        leaf ``.grad``s, as bench.py and dp do): the MLP backward then adds every parameter's
+        gradient straight into one flat buffer whose views ARE the ``.grad``s (no per-parameter
+        autograd accumulation, no flatten for the all-reduce), bypassing autograd's gradient
+        return — so per-parameter hooks do not fire and ``torch.autograd.grad`` must not be
+        used on the parameters.  Off by default: gradients go back through autograd."""
+        self.flat_grads = bool(on)
+        return self
+
     def flat_grad_target(self, params):
-        """Where the MLP backward accumulates parameter gradients directly (no per-parameter
-        autograd accumulation, no flatten for the all-reduce): the model's flat gradient buffer,
-        when every parameter's ``.grad`` is its view — or, when every ``.grad`` is None, the
-        buffer zeroed, with its views installed as the ``.grad``s.  None otherwise (the
-        gradients then go back through autograd)."""
+        """Where the MLP backward accumulates parameter gradients directly: with
+        ``use_flat_grads`` on and EVERY canonical parameter requiring grad, the model's flat
+        gradient buffer, when every parameter's ``.grad`` is its view — or, when every
+        ``.grad`` is None, the buffer zeroed, with its views installed as the ``.grad``s.  None
+        otherwise (the gradients then go back through autograd; a frozen parameter never gets
+        a ``.grad`` here)."""
+        if not self.flat_grads or not all(p.requires_grad for p in params):
+            return None
         fb = self._flat_grad
         if all(p.grad is None for p in params):
             total = sum(p.numel() for p in params)
@@ -291,7 +305,11 @@ class WeightPack:
     def done(self):
         self.pending -= 1
         if self.pending == 0 and self.owned:
-            self.model.release_packed(self.buf)
+            # a buffer captured into a HIP graph is re-packed by every replay: it never returns
+            # to the free list, where a later eager forward could take it while a replay's
+            # backward still reads it
+            if not torch.cuda.is_current_stream_capturing():
+                self.model.release_packed(self.buf)
             self.buf = None
 
 

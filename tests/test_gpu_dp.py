@@ -63,6 +63,7 @@ def step_grads(rank, world, precision):
     tables = [torch.rand(GLOBAL_B, S, generator=g) for _ in range(3)]
     torch.manual_seed(0)
     model = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True, precision=precision).to(dev)
+    model.use_flat_grads(world > 1)   # the ranks all-reduce the flat buffer in place; one process: autograd
     args = types.SimpleNamespace(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
                                  sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)
     R = scene

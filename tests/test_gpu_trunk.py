@@ -24,10 +24,14 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5  # norm-relative
 
 
-def _render(fused: bool, dims: ModelDims, n_rays: int, guided: bool, sc: float, seed: int = 0):
-    _lib.set_option("fused_trunk", int(fused))
+def _render(fused: bool, dims: ModelDims, n_rays: int, guided: bool, sc: float, seed: int = 0, n_samples: int = 64,
+            options: dict | None = None):
+    opts = {"fused_trunk": int(fused), **(options or {})}
+    saved = {k: _lib.get_option(k) for k in opts}
+    for k, v in opts.items():
+        _lib.set_option(k, v)
     try:
-        args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=guided,
+        args = gu.args_of({"args": dict(n_samples=n_samples, n_importance=0, model="sp-nerf", beta=False, guidedsample=guided,
                                         sc_lambda=sc, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
         rays = torch.tensor(gu_rays(n_rays, 9 + seed), device=DEV)
         g = torch.Generator(device="cpu").manual_seed(seed)
@@ -48,7 +52,18 @@ def _render(fused: bool, dims: ModelDims, n_rays: int, guided: bool, sc: float, 
         return ({k: v.detach().cpu() for k, v in res.items()},
                 {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None})
     finally:
-        _lib.set_option("fused_trunk", 1)
+        for k, v in saved.items():
+            _lib.set_option(k, v)
+
+
+def _assert_bitwise(a, b):
+    (r1, g1), (r0, g0) = a, b
+    assert sorted(r1) == sorted(r0) and sorted(g1) == sorted(g0)
+    for k in r0:
+        assert torch.isfinite(r1[k]).all(), k
+        assert torch.equal(r1[k], r0[k]), (k, gu.rel_err(r1[k].numpy(), r0[k].numpy()))
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), (n, gu.rel_err(g1[n].numpy(), g0[n].numpy()))
 
 
 @pytest.mark.parametrize("dims,n_rays,guided,sc", [
@@ -108,3 +123,20 @@ def test_fused_trunk_point_network_bitwise_vs_layerwise():
             _lib.set_option("fused_trunk", 1)
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("dims,n_rays,guided,sc,n_samples", [
+    (ModelDims(width=512, sem=True), 257, True, 0.1, 64),   # C3 flags: semantic rows at the skip layer
+    (ModelDims(width=512), 33, False, 0.1, 32),             # 33·32 points: the last 64-point tile half full
+    (ModelDims(width=512, sem=True), 96, False, 0.0, 128),  # C5-like sampling, semantic rows
+])
+def test_two_workgroup_trunk_bitwise(dims, n_rays, guided, sc, n_samples):
+    """k_trunk2_bf16 (D stored from the registers, trunk2_bf16.hip; 128-point tiles, or 64-point
+    tiles two workgroups per CU) against the one-workgroup kernels with the D image: training
+    (trunk2=1, the default) and inference too (trunk2=2, layer 0 and the inline encoding in the
+    launch) equal trunk2=0 bit for bit."""
+    base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk2": 0})
+    for tile in (128, 64):
+        for t2 in (1, 2):
+            _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples,
+                                    options={"trunk2": t2, "trunk2_tile": tile}), base)

@@ -26,11 +26,15 @@ def main():
     ap.add_argument("--samples", type=int, default=128)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE")
+    ap.add_argument("--modes", default="save,nosave,sigma")
     a = ap.parse_args()
     for o in a.option:
         k, v = o.split("=")
         _lib.set_option(k, int(v))
     dev = torch.device("cuda", 0)
+    torch.zeros(1, device=dev)
+    print("trunk2 resident workgroups per CU (save, inference):", _lib.lib().spnerf_debug_trunk2_occupancy(1),
+          _lib.lib().spnerf_debug_trunk2_occupancy(0), flush=True)
     torch.manual_seed(0)
     m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True, precision="bf16").to(dev)
     B, S = a.rays, a.samples
@@ -43,7 +47,7 @@ def main():
     z = torch.sort(torch.rand(B, S, device=dev), 1)[0].contiguous()
     lab = torch.randint(0, 3, (B,), device=dev)
     classes = ["trunk_bf16", "trunk_bf16_train", "gemm_nt_bf16", "gemm_nt_f32", "heads_fwd", "heads_fused", "encode"]
-    for mode in ("save", "nosave", "sigma"):
+    for mode in a.modes.split(","):
         for fused in ((1,) if a.option else (1, 0)):
             _lib.set_option("fused_trunk", fused)
 
