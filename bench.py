@@ -45,16 +45,31 @@ from spnerf_amd.scene import synthetic_scene  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec
 BF16_MFMA_PEAK_TFLOPS = 2516.6    # dense bf16 = 16 x the f32 MFMA rate (MI355X_MICROARCH.md "Peak BF16", ~2.5 PF)
 HBM_PEAK_GBS = 8000.0
-GEMM_CLASSES = {"gemm_nt_f32": ("k_gemm_nt_w (fp32 MFMA, 256x128 persistent tiles, 2 blocks/CU, LDS-DMA)", FP32_MFMA_PEAK_TFLOPS),
-                "gemm_tn_f32": ("k_gemm_tn (fp32 MFMA, weight gradients)", FP32_MFMA_PEAK_TFLOPS),
-                "gemm_nt_bf16": ("k_gemm_nt_bf16d (bf16 MFMA, 256x256 persistent tiles, LDS-DMA ring across tiles)",
-                                 BF16_MFMA_PEAK_TFLOPS),
-                "gemm_tn_bf16": ("k_gemm_tn_bf16d (bf16 MFMA, weight gradients, LDS-DMA)", BF16_MFMA_PEAK_TFLOPS),
-                "trunk_bf16": ("k_trunk_bf16<128> (fused bf16 trunk, inference tiles, LDS-resident activations)",
-                               BF16_MFMA_PEAK_TFLOPS),
-                "trunk_bf16_train": ("k_trunk_bf16<64> (fused bf16 trunk, training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
-                "trunk_bwd_bf16": ("k_trunk_bwd_bf16 (fused bf16 backward dX chain, LDS-resident dZ)", BF16_MFMA_PEAK_TFLOPS),
-                "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS)}
+# The library's profiling classes: ONE class per kernel function (rocprofv3 name in the text).
+# MFMA kernels carry the peak of their arithmetic; the rest are HBM kernels.
+GEMM_CLASSES = {
+    "gemm_nt_f32": ("k_gemm_nt_w<256,128,2,2,3> (fp32 MFMA NT GEMM, persistent 256x128 tiles, LDS-DMA)", FP32_MFMA_PEAK_TFLOPS),
+    "gemm_tn_f32": ("k_gemm_tn<3> (fp32 MFMA weight-gradient GEMM)", FP32_MFMA_PEAK_TFLOPS),
+    "gemm_nt_bf16d": ("k_gemm_nt_bf16d<false,2> (bf16 MFMA NT GEMM, 256x256 persistent tiles, LDS-DMA ring; "
+                      "bias / sin / D epilogue: head layers and layer 0)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_nt_bf16d_dmul": ("k_gemm_nt_bf16d<true,2> (bf16 MFMA dX GEMM with the x D epilogue)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_nt_bf16w": ("k_gemm_nt_bf16w (bf16 MFMA NT GEMM, register-staged)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_nt_bf16": ("k_gemm_nt_bf16 (bf16 MFMA NT GEMM, 128x128 tiles)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_tn_bf16d": ("k_gemm_tn_bf16d<2> (bf16 MFMA weight-gradient GEMM, 256x256 tiles, LDS-DMA)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_tn_bf16w": ("k_gemm_tn_bf16w (bf16 MFMA weight-gradient GEMM, 256x256 register-staged)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA weight-gradient GEMM, 128x128 tiles)", BF16_MFMA_PEAK_TFLOPS),
+    "trunk_bf16": ("k_trunk_bf16<128> (fused bf16 trunk, inference tiles, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
+    "trunk_bf16_train": ("k_trunk_bf16<64> (fused bf16 trunk, training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
+    "trunk_bwd_bf16": ("k_trunk_bwd_bf16 (fused bf16 backward dX chain, LDS-resident dZ)", BF16_MFMA_PEAK_TFLOPS),
+    "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS)}
+HBM_CLASSES = {"tn_skinny": "k_tn_skinny (narrow-head / per-ray weight gradients)",
+               "reduce_slabs": "k_reduce_slabs (fixed-order weight-gradient split reduction)",
+               "encode": "k_encode (positional encoding)", "heads_fwd": "k_heads_fwd_v (narrow heads)",
+               "heads_bwd": "k_heads_bwd_v (narrow-head backward)", "composite_fwd": "k_composite_fwd",
+               "composite_bwd": "k_composite_bwd", "sample_guided": "k_guided", "render_loss": "k_loss_*",
+               "pack": "k_pack (weight re-layout)", "adam": "k_adam", "ray_rowsum": "k_ray_rowsum*",
+               "ray_terms": "k_ray_fwd / k_ray_bwd / k_class_sum", "zero": "k_zero"}
+MFMA_TARGET = 0.40   # BASELINE.json north star: >= 40% MFMA utilisation on the MLP
 
 CONFIGS = {
     "c2": dict(workload="C2: JAX_214-shape scene (3 JAX_269 RPC cameras, GPU-generated rays), img_downscale=4, "
@@ -113,10 +128,12 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(c, seconds: float, batch: int):
+def cpu_baseline(c, seconds: float, batch: int, min_steps: int = 3):
     """The parity-pinned CPU restatement (oracle/ref_cpu.py) of the same train step on the host
-    cores: batches of the GPU step's size (``batch`` rays) of the same workload, repeated until
-    ~``seconds`` have passed (at least one timed step), after one small warm-up step."""
+    cores — render, the trainer's whole loss sum (colour + solar terms + subset depth + semantic
+    CE, ``ref_cpu.train_loss`` = main.py:143-174, so the backward runs through the solar pass as
+    on the GPU), backward, Adam — on ``batch``-ray batches of the same workload, at least
+    ``min_steps`` steps and until ~``seconds`` have passed, after one small warm-up step."""
     import numpy as np
     from oracle import ref_cpu
     from oracle.weights import ModelDims, make_weights
@@ -142,7 +159,9 @@ def cpu_baseline(c, seconds: float, batch: int):
                 ref_cpu.render_rays(p, dims, args, scene.rays[idx], None, scene.sems[idx] if c["sem"] else None, "test")
             return
         res = ref_cpu.render_rays(p, dims, args, scene.rays[idx], None, scene.sems[idx] if c["sem"] else None, "train", **kw)
-        loss = torch.mean((res["rgb_coarse"] - scene.rgbs[idx]) ** 2)
+        loss = ref_cpu.train_loss(res, scene.rgbs[idx], scene.depths[idx], scene.valid_depth[idx], scene.depth_std[idx],
+                                  scene.sems[idx] if c["sem"] else None, c["sc_lambda"], 1.0 if c["depth"] else 0.0,
+                                  1.0 if c["sem"] else 0.0)
         opt.zero_grad()
         loss.backward()
         opt.step()
@@ -153,14 +172,15 @@ def cpu_baseline(c, seconds: float, batch: int):
     while True:
         one()
         n += 1
-        if time.perf_counter() - t0 >= seconds or n >= 200:
+        if (time.perf_counter() - t0 >= seconds and n >= min_steps) or n >= 200:
             break
     dt = time.perf_counter() - t0
     what = "inference renders" if c.get("inference") else "train steps"
     return {"value": B * s_final * n / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
             "host_cpus_reported": os.cpu_count(), "cpu_model": cpu_model(),
-            "sample": f"{n} {what} of {B} rays x {s_final} samples, the GPU step's batch (oracle/ref_cpu.py, torch "
-                      f"CPU, fp32, {threads} threads = the CPUs this job may use)"}
+            "sample": f"{n} {what} of {B} rays x {s_final} samples of the same workload (oracle/ref_cpu.py render + "
+                      f"ref_cpu.train_loss = the GPU step's loss sum + Adam; torch CPU, fp32, {threads} threads = the "
+                      f"CPUs this job may use)"}
 
 
 def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int = 3, dev="cuda:0",
@@ -243,38 +263,50 @@ def ref_cpu_replay(draws):
     return draw
 
 
-def measured_traffic(config, kernel_class):
-    """HBM bytes per launch of ``kernel_class`` from the committed PMC profile of this workload
-    (tools/pmc_bench.sh + tools/traffic_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
-    bytes = 2*FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md's gfx950 correction).  PMC
-    counters cannot be read from inside the bench process, hence the profile file."""
-    for rnd in ("r02", "r01"):
-        path = os.path.join(ROOT, "profiles", rnd, f"traffic_{config}.json")
+def measured_traffic(config, rays_per_rank, kernel_class):
+    """HBM bytes per launch of ``kernel_class`` from the committed PMC profile of THIS workload at
+    THIS batch (rays per rank) — tools/pmc_bench.sh + tools/traffic_summary.py: separate
+    FETCH_SIZE / WRITE_SIZE passes, bytes = 2*FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md's
+    gfx950 correction.  None when no profile of that (config, rays per rank) is committed (PMC
+    counters cannot be read from inside the bench process, hence the profile file)."""
+    for rnd in ("r03",):
+        rel = f"profiles/{rnd}/traffic_{config}_rays{rays_per_rank}.json"
         try:
-            with open(path) as f:
+            with open(os.path.join(ROOT, rel)) as f:
                 t = json.load(f)[kernel_class]
-            return t["hbm_bytes_per_launch"], f"profiles/{rnd}/traffic_{config}.json ({t['launches']} launches)"
+            if t.get("rays_per_rank") != rays_per_rank:
+                continue
+            return t["hbm_bytes_per_launch"], f"{rel} ({t['launches']} launches)"
         except (OSError, KeyError, ValueError):
             continue
     return None, None
 
 
 
+def dominant_class():
+    """The kernel function (profiling class) with the most time in the profiled steps."""
+    classes = _lib.prof_classes()
+    return max(classes, key=lambda k: _lib.prof_read(k)["ms"]) if classes else None
+
+
 def roofline_of(dom, nt, traffic=None, traffic_src=None):
-    """Roofline of the dominant kernel class: the bound is the one its algorithmic intensity
-    (FLOP per algorithmic HBM byte, both counted per launch by the library) sits under — MFMA
-    when it is above the ridge peak_flops / 8 TB/s (fp32: 19.7 FLOP/B, bf16: 315), HBM below it
-    (the bf16 GEMMs at K = 512: ≈127 FLOP/B for a sine layer, reading 2 B and writing 4 B per
-    output).  Both fractions are reported; ``frac`` is the binding one."""
-    dom_name, peak = GEMM_CLASSES[dom]
+    """Roofline of the dominant kernel: the bound is the one its algorithmic intensity (FLOP per
+    algorithmic HBM byte, both counted per launch by the library) sits under — MFMA when it is
+    above the ridge peak_flops / 8 TB/s (fp32: 19.7 FLOP/B, bf16: 315), HBM below it (the bf16
+    GEMMs at K = 512: ≈127 FLOP/B for a sine layer, reading 2 B and writing 4 B per output); a
+    kernel without MFMAs is HBM-bound.  Both fractions are reported; ``frac`` is the binding one."""
+    if dom in GEMM_CLASSES:
+        dom_name, peak = GEMM_CLASSES[dom]
+    else:
+        dom_name, peak = HBM_CLASSES.get(dom, dom), None
     secs = nt["ms"] * 1e-3
     tflops = nt["flop"] / secs / 1e12 if secs else 0.0
     gbs = nt["bytes"] / secs / 1e9 if secs else 0.0
-    ridge = peak * 1e3 / HBM_PEAK_GBS  # FLOP per byte
-    intensity = nt["flop"] / nt["bytes"] if nt["bytes"] else float("inf")
+    ridge = peak * 1e3 / HBM_PEAK_GBS if peak else None  # FLOP per byte
+    intensity = nt["flop"] / nt["bytes"] if nt["bytes"] else (float("inf") if nt["flop"] else 0.0)
     r = {"kernel": f"{dom} ({dom_name})", "intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge,
-         "mfma_frac": tflops / peak, "hbm_frac": gbs / HBM_PEAK_GBS}
-    if intensity >= ridge:
+         "mfma_frac": tflops / peak if peak else None, "hbm_frac": gbs / HBM_PEAK_GBS}
+    if peak and intensity >= ridge:
         r.update(bound="mfma", achieved=tflops, peak=peak, unit="TFLOP/s", frac=tflops / peak)
     else:
         r.update(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=gbs / HBM_PEAK_GBS)
@@ -284,8 +316,9 @@ def roofline_of(dom, nt, traffic=None, traffic_src=None):
     return r
 
 def gemm_totals(steps):
-    """All MFMA GEMM launches of the timed steps: counted FLOP / summed kernel time, against the
-    peak of each launch's dtype (time-weighted) — the MLP's MFMA utilisation."""
+    """Every MFMA launch of the profiled steps (GEMMs and fused trunk / heads kernels): counted
+    FLOP / summed kernel time, against the peak of each launch's dtype (time-weighted) — the
+    MLP's MFMA utilisation, BASELINE.json's north-star figure (target >= 0.40)."""
     flop = ms = peak_ms = 0.0
     for k, (_, peak) in GEMM_CLASSES.items():
         r = _lib.prof_read(k)
@@ -296,7 +329,20 @@ def gemm_totals(steps):
         return None
     tf = flop / (ms * 1e-3) / 1e12
     peak = peak_ms / ms
-    return {"tflops": tf, "peak": peak, "frac": tf / peak, "ms_per_step": ms / steps}
+    return {"tflops": tf, "peak": peak, "frac": tf / peak, "ms_per_step": ms / steps, "target": MFMA_TARGET}
+
+
+def kernel_table(steps):
+    """Per kernel function of the profiled steps: launches, ms per step, average launch, achieved
+    TFLOP/s and algorithmic GB/s."""
+    out = {}
+    for k in _lib.prof_classes():
+        s = _lib.prof_read(k)
+        if s["launches"]:
+            out[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / steps, "avg_us": 1e3 * s["ms"] / s["launches"],
+                      "tflops": s["flop"] / (s["ms"] * 1e-3) / 1e12 if s["flop"] else None,
+                      "gbs": s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["bytes"] else None}
+    return dict(sorted(out.items(), key=lambda kv: -kv[1]["ms_per_step"]))
 
 
 def run_inference(a, c, rank, world, dev):
@@ -317,7 +363,7 @@ def run_inference(a, c, rank, world, dev):
     model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"],
                               precision=c["precision"]).to(dev)
     args = make_args(c)
-    B, n = c["batch"], rays.shape[0]
+    B, n = a.global_batch or c["batch"], rays.shape[0]
     pos = [0]
 
     @torch.no_grad()
@@ -346,7 +392,7 @@ def run_inference(a, c, rank, world, dev):
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    dom = max(GEMM_CLASSES, key=lambda k: _lib.prof_read(k)["ms"])
+    dom = dominant_class()
     nt = _lib.prof_read(dom)
     total = world * B * c["n_samples"] * a.steps
     value = total / elapsed
@@ -358,8 +404,9 @@ def run_inference(a, c, rank, world, dev):
         "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": c["n_samples"],
                    "parallelism": f"ray-shard{world}", "image_rays": h * w},
         "image_seconds_projected": h * w * c["n_samples"] / value,
-        "roofline": roofline_of(dom, nt, *measured_traffic(a.config, dom)),
-        "mlp_gemms": gemm_totals(a.steps),
+        "roofline": roofline_of(dom, nt, *measured_traffic(a.config, B, dom)),
+        "mlp_mfma_utilisation": gemm_totals(a.steps),
+        "kernels": kernel_table(a.steps),
         "finite": bool(torch.isfinite(res["rgb_coarse"]).all()),
     }
     if a.full_image:
@@ -454,7 +501,8 @@ def parse_args(argv=None):
     ap.add_argument("--torch-adam", action="store_true", help="torch.optim.Adam(fused=True) instead of spnerf_amd.optim.Adam")
     ap.add_argument("--torch-loss", action="store_true", help="the losses module (plain torch) instead of the fused loss kernels")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-batch", type=int, default=0, help="rays per CPU-baseline step (default: the GPU step's batch)")
+    ap.add_argument("--cpu-batch", type=int, default=0,
+                    help="rays per CPU-baseline step (default: the GPU step's batch, at most 512)")
     ap.add_argument("--full-image", action="store_true",
                     help="C5: after the timed chunks, render every ray of the image (each rank its row shard) and "
                          "gather rgb + depth to rank 0; reported as full_image")
@@ -493,7 +541,8 @@ def main():
     if rank == 0 and world == 1 and a.config == "c4" and not a.no_secondary:
         # configs[1] (C2, fp32) beside the headline, same process and GPU, no CPU leg
         sec = run_train(a, "c2", rank, world, dev, secondary=True)
-        out["secondary"] = {"c2": {k: sec[k] for k in ("value", "unit", "ms_per_step", "dtype", "config", "roofline")}}
+        out["secondary"] = {"c2": {k: sec[k] for k in ("value", "unit", "ms_per_step", "dtype", "config", "roofline",
+                                                          "mlp_mfma_utilisation")}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -566,8 +615,20 @@ def run_train(a, config, rank, world, dev, secondary=False):
         loss.backward()
         return loss.detach()   # no autograd graph outlives the step (captured nodes would pin their stream)
 
+    # all-reduce time per timed step, from HIP events on the current stream around the call (the
+    # collective's completion is ordered before the end event); summed after the timed region
+    ar_events = []
+    ar_timing = [False]
+
     def finish():
-        dp.allreduce_grads(params, world)   # one RCCL all-reduce of the flat gradient (N > 1)
+        if world > 1 and ar_timing[0]:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dp.allreduce_grads(params, world)   # one RCCL all-reduce of the flat gradient (N > 1)
+            e1.record()
+            ar_events.append((e0, e1))
+        else:
+            dp.allreduce_grads(params, world)
         opt.step()
         args.noise_std *= 0.9               # main.py:155
 
@@ -620,6 +681,7 @@ def run_train(a, config, rank, world, dev, secondary=False):
         _lib.prof_reset()
         _lib.prof_enable(True)
     torch.cuda.synchronize()
+    ar_timing[0] = True
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
@@ -627,6 +689,8 @@ def run_train(a, config, rank, world, dev, secondary=False):
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    ar_timing[0] = False
+    allreduce_ms = sum(e0.elapsed_time(e1) for e0, e1 in ar_events) / a.steps if ar_events else None
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -644,19 +708,11 @@ def run_train(a, config, rank, world, dev, secondary=False):
         torch.cuda.synchronize()
     _lib.prof_enable(False)
 
-    kernels = {}
-    for k in ("gemm_nt_f32", "gemm_tn_f32", "gemm_nt_bf16", "gemm_tn_bf16", "trunk_bf16", "trunk_bf16_train", "trunk_bwd_bf16", "tn_skinny", "encode", "heads_fwd",
-              "heads_bwd", "heads_fused", "composite_fwd", "composite_bwd", "sample_guided", "render_loss", "pack", "adam"):
-        s = _lib.prof_read(k)
-        if s["launches"]:
-            kernels[k] = {"launches": s["launches"], "ms_per_step": s["ms"] / prof_steps,
-                          "avg_us": 1e3 * s["ms"] / s["launches"],
-                          "tflops": s["flop"] / (s["ms"] * 1e-3) / 1e12 if s["flop"] else None,
-                          "gbs": s["bytes"] / (s["ms"] * 1e-3) / 1e9 if s["bytes"] else None}
-    # dominant kernel = the GEMM class with the most time in the timed steps
-    dom = max(GEMM_CLASSES, key=lambda k: _lib.prof_read(k)["ms"])
+    kernels = kernel_table(prof_steps)
+    # dominant kernel = the kernel function with the most time in the profiled steps
+    dom = dominant_class()
     nt = _lib.prof_read(dom)
-    traffic, traffic_src = measured_traffic(config, dom)
+    traffic, traffic_src = measured_traffic(config, B, dom)
     total = world * B * s_final * a.steps
     out = {
         "metric": "ray-samples/sec (train step)",
@@ -675,7 +731,8 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "config": {"workload": c["workload"], "global_batch": B * world, "rays_per_rank": B,
                    "samples_per_ray": s_final, "parallelism": f"dp{world}"},
         "roofline": roofline_of(dom, nt, traffic, traffic_src),
-        "mlp_gemms": gemm_totals(prof_steps),
+        "mlp_mfma_utilisation": gemm_totals(prof_steps),
+        "allreduce_ms_per_step": allreduce_ms,
         "kernels": kernels,
         "final_loss": final_loss,
         "execution": ("hip graph of render+loss+backward per step, eager all-reduce + fused Adam; kernel timings "
@@ -683,7 +740,7 @@ def run_train(a, config, rank, world, dev, secondary=False):
     }
     del graph
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not secondary:
-        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or B)
+        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or min(B, 512))
         if config in ("c2", "c4"):
             out["psnr_parity"] = {p: psnr_parity(dev=dev, precision=p) for p in ("fp32", "bf16")}
     return out

@@ -202,10 +202,13 @@ int32_t spnerf_adam_step(int32_t n, void* const* params, const void* const* grad
 /* ---- in-library kernel timing (HIP events on the launch stream) ------------------------- */
 int32_t spnerf_prof_enable(int32_t on);
 int32_t spnerf_prof_reset(void);
-/* Totals over the recorded launches of one kernel class ("gemm_nt_f32", "gemm_tn_f32",
- * "composite_fwd", ...).  Synchronises the recorded events. */
+/* Totals over the recorded launches of one kernel class ("gemm_nt_f32", "gemm_tn_bf16d",
+ * "composite_fwd", ...: one class per kernel function, the DMA NT GEMM's x Dmul instance as
+ * "gemm_nt_bf16d_dmul").  Synchronises the recorded events. */
 int32_t spnerf_prof_read(const char* kernel_class, int64_t* launches, double* total_ms, double* total_flop,
                          double* total_bytes);
+/* The names of the classes recorded since the last reset, comma-separated, into buf (cap bytes). */
+int32_t spnerf_prof_classes(char* buf, int32_t cap);
 
 #ifdef __cplusplus
 }

@@ -78,6 +78,7 @@ SIGNATURES = {
     "spnerf_prof_enable": (c_int32, [c_int32]),
     "spnerf_prof_reset": (c_int32, []),
     "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
+    "spnerf_prof_classes": (c_int32, [c_char_p, c_int32]),
 }
 
 _lib = None
@@ -143,6 +144,12 @@ def prof_enable(on: bool = True) -> None:
 
 def prof_reset() -> None:
     check(lib().spnerf_prof_reset(), "prof_reset")
+
+
+def prof_classes() -> list:
+    buf = ctypes.create_string_buffer(8192)
+    check(lib().spnerf_prof_classes(buf, len(buf)), "prof_classes")
+    return [c for c in buf.value.decode().split(",") if c]
 
 
 def prof_read(kernel_class: str) -> dict:

@@ -103,6 +103,16 @@ extern "C" int32_t spnerf_prof_reset(void) {
     return SPNERF_OK;
 }
 
+extern "C" int32_t spnerf_prof_classes(char* buf, int32_t cap) {
+    SPN_ARG(buf != nullptr && cap > 0, "prof_classes: NULL buffer");
+    std::lock_guard<std::mutex> lk(g_mu);
+    std::string names;
+    for (auto& kv : g_stats) names += (names.empty() ? "" : ",") + kv.first;
+    SPN_ARG((int64_t)names.size() < cap, "prof_classes: buffer of %d bytes too small (%zu)", cap, names.size() + 1);
+    snprintf(buf, cap, "%s", names.c_str());
+    return SPNERF_OK;
+}
+
 extern "C" int32_t spnerf_prof_read(const char* cls, int64_t* launches, double* total_ms, double* total_flop,
                                     double* total_bytes) {
     SPN_ARG(cls != nullptr, "prof_read: NULL class");

@@ -1235,16 +1235,18 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     const int ntiles = cdiv(a.M, HB) * cdiv(a.N, HB);
     // algorithmic bytes: A and B once, C, the derivative of the sine columns, the Dmul read
     const double dcols = (a.Dout && a.act == 1) ? (double)(a.N - std::min(a.n_lin, a.N)) : 0.0;
-    ProfScope prof("gemm_nt_bf16", s, 2.0 * a.M * a.N * (a.k_alg > 0 ? a.k_alg : a.K),
-                   2.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N * (1.0 + (a.Dmul ? 1.0 : 0.0)) +
-                          (double)a.M * dcols));
     // variants: 1 / 2 = one block per tile, prefetch depth 1 / 2; 3 / 4 = persistent grid of
     // two blocks per CU (the LDS limit), depth 1 / 2
     int v = variant > 0 ? variant : g_nt16_variant;
     if (v == 8 && (a.K % ND_K != 0 || (a.K1 != a.K && a.K1 % ND_K != 0))) v = 5;  // DMA needs whole 32-wide K-steps
+    const bool dm = a.Dmul && !a.bias && !a.rowbias && !a.r1_a && a.act == 0 && !a.Dout;
+    // one profiling class per kernel function: the DMA kernel's two epilogue instances apart
+    ProfScope prof(v == 8 ? (dm ? "gemm_nt_bf16d_dmul" : "gemm_nt_bf16d") : v >= 5 ? "gemm_nt_bf16w" : "gemm_nt_bf16", s,
+                   2.0 * a.M * a.N * (a.k_alg > 0 ? a.k_alg : a.K),
+                   2.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N * (1.0 + (a.Dmul ? 1.0 : 0.0)) +
+                          (double)a.M * dcols));
     if (v == 8) {
         const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
-        const bool dm = a.Dmul && !a.bias && !a.rowbias && !a.r1_a && a.act == 0 && !a.Dout;
         const int ip = (a.dbg & 64) ? 2 : (a.dbg & 32) ? 1 : g_nt16_ip;
         if (dm && ip == 2) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
         else if (dm && ip == 1) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
@@ -1299,12 +1301,13 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     int pps = cdiv(a.P, splits);
     pps = (pps + 63) / 64 * 64;
     a.p_per_split = pps < 64 ? 64 : pps;
-    ProfScope prof("gemm_tn_bf16", s, 2.0 * a.P * a.N * a.K,
+    const bool wide = tn_wide(a.N, a.K, -1);
+    const bool dma = wide && g_tn16_variant == 3 && a.P % TD_STEP == 0 && !a.b_sin;  // DMA: whole 32-point steps
+    ProfScope prof(dma ? "gemm_tn_bf16d" : wide ? "gemm_tn_bf16w" : "gemm_tn_bf16", s, 2.0 * a.P * a.N * a.K,
                    2.0 * (double)a.P * (a.N + a.K) + 4.0 * splits * (double)a.N * a.K);
-    if (tn_wide(a.N, a.K, -1)) {
+    if (wide) {
         const int nb = cdiv(a.N, TW) * cdiv(a.K, TW);
-        const int v = g_tn16_variant;
-        if (v == 3 && a.P % TD_STEP == 0 && !a.b_sin)  // DMA: whole 32-point steps, B staged as is
+        if (dma)  // B staged as is
         {
             const int ip = (a.dbg & 4) ? 2 : (a.dbg & 2) ? 1 : g_tn16_ip;
             if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, dim3(nb * splits), dim3(512), 0, s, a);

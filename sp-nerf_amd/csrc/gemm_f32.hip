@@ -1004,6 +1004,7 @@ int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s, int variant) {
 int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s) {
     if (a.nrows <= 0) return SPNERF_OK;
     const int cols = a.ncols + 1;
+    ProfScope prof("reduce_slabs", s, 0.0, 4.0 * (double)a.nrows * cols * (a.splits + (a.accumulate ? 2.0 : 1.0)));
     hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(cols, 256), a.nrows), dim3(256), 0, s, a);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;

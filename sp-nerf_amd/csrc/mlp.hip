@@ -1290,6 +1290,7 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
             a.d.td = 0;
         }
         if (d.sem || mode != 1) {
+            ProfScope prof("ray_terms", s, 0.0, 0.0);
             hipLaunchKernelGGL(k_ray_fwd, dim3((unsigned)n_rays), dim3(256), 0, s, a);
             SPN_HIP(hipGetLastError());
         }
@@ -1357,6 +1358,7 @@ __global__ void k_zero(float* __restrict__ p, int64_t n) {
 
 static int32_t zero_fill(float* p, int64_t n, hipStream_t s) {
     if (n <= 0) return SPNERF_OK;
+    ProfScope prof("zero", s, 0.0, 4.0 * n);
     hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0, s, p, n);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
@@ -1365,6 +1367,7 @@ static int32_t zero_fill(float* p, int64_t n, hipStream_t s) {
 // per-ray sums of a point-major buffer (see k_ray_rowsum)
 template <typename T>
 static int32_t ray_rowsum(const T* in, int ld, int c0, int N, int S, int64_t n_rays, float* out, int ldo, hipStream_t s) {
+    ProfScope prof("ray_rowsum", s, 0.0, (double)n_rays * (S * (double)N * sizeof(T) + 4.0 * N));
     if constexpr (std::is_same<T, bf16>::value) {
         if (N % 8 == 0 && N <= 2048 && ld % 8 == 0 && c0 % 8 == 0) {
             hipLaunchKernelGGL(k_ray_rowsum16, dim3((unsigned)n_rays), dim3(256), 0, s, in, ld, c0, N, S, out, ldo);
@@ -1580,6 +1583,7 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
     {
         const int sky_on = mode == 0;
         if (sky_on) {
+            ProfScope prof("ray_rowsum", s, 0.0, 0.0);
             hipLaunchKernelGGL(k_ray_rowsum<float>, dim3(1, (unsigned)n_rays), dim3(256), 0, s, d_out, d.NO, 5, 3, S,
                                c.at(c.w.dsky), 4);
             SPN_HIP(hipGetLastError());
@@ -1587,8 +1591,11 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
         RayBwdArgs a{packed, c.k, d, c.at(c.w.sky), c.at(c.w.skyh), c.at(c.w.dsky), c.at(c.w.R0), c.at(c.w.R4),
                      c.at(c.w.RQ), labels, c.at(c.w.skyd), c.at(c.w.skydh), c.at(c.w.gemb), c.at(c.w.embr), grad_t,
                      d.sem ? 1 : 0, (d.beta && mode == 0) ? 1 : 0, sky_on};
-        hipLaunchKernelGGL(k_ray_bwd, dim3((unsigned)n_rays), dim3(256), 0, s, a);
-        SPN_HIP(hipGetLastError());
+        {
+            ProfScope prof("ray_terms", s, 0.0, 0.0);
+            hipLaunchKernelGGL(k_ray_bwd, dim3((unsigned)n_rays), dim3(256), 0, s, a);
+            SPN_HIP(hipGetLastError());
+        }
         const float* sun = rays + 8;
         const int64_t B = n_rays;
         // sun_v_net.0 sun-direction columns: dW[n][W+j] = Σ_ray RQ[ray][n] sun[ray][j]
@@ -1605,6 +1612,7 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
                            nullptr, nullptr, s));
             SPN_TRY(skinny(c, B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R4), W, W, gp(x.fcW[d.skip]) + W + d.K0,
                            ld(x.fcW[d.skip]), 1, nullptr, nullptr, s));
+            ProfScope prof("ray_terms", s, 0.0, 0.0);
             hipLaunchKernelGGL(k_class_sum, dim3((d.C + 1) * d.sd), dim3(256), 0, s, n_rays, c.at(c.w.gemb), d.sd, labels,
                                d.C, gp(x.emb), c.acc);
             SPN_HIP(hipGetLastError());

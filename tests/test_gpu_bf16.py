@@ -7,7 +7,9 @@ runs on bf16 hi/lo planes, (x_hi + x_lo)·(w_hi + w_lo) with fp32 accumulation (
 per product: the near-fp32 input precision SURVEY §8 hard part 1 asks for, at bf16 MFMA rates).
 It cannot meet the 1e-4 fp32 bar by construction, so it is held to mixed-precision tolerances
 against the SAME reference fixtures the fp32 path matches to 1e-4:
-  * outputs: norm-relative error  ||bf16 - ref|| / ||ref|| <= OUT_TOL per key;
+  * outputs: norm-relative error  ||bf16 - ref|| / ||ref|| <= OUT_TOL_KEY[key], about 3x the
+    worst value measured on MI355X over CASES (tools/bf16_errors.py; the measurements are in the
+    comments), so that a real regression fails;
   * gradients: norm-relative error of the whole flat gradient <= GRAD_TOL_ALL, and per parameter
     tensor of >= 64 elements <= GRAD_TOL (full-gradient fixtures; W=512 fixtures through the
     fixed random projections, error / ||grad||).  Scalar-sized gradients (σ / sun / β output
@@ -26,10 +28,34 @@ from test_gpu_parity import DEV, make_model, run_case
 
 pytestmark = pytest.mark.gpu
 
-OUT_TOL = 2e-2       # measured worst 4e-3 (sem_logits, C3 size); most outputs 1e-4..5e-4
-GRAD_TOL = 8e-2      # per tensor; measured worst 5.1e-2 (sun_v_net.0.bias projection, c3_w512)
-GRAD_TOL_ALL = 2e-2  # whole flat gradient; measured 0.5-1.4e-2 over CASES
-CASES = ["c1_w512", "c3_w512", "c3_w64", "beta_w64", "nomap_w64", "c3_test_w64", "c5_w512"]
+# per output key (suffixes _coarse / _fine / _sc dropped): the worst norm-relative error measured
+# over CASES on MI355X (round 3), and the bound at ~3x it
+OUT_TOL_KEY = {
+    "rgb": 1.5e-3,            # 5.6e-4 (nomap_w64)
+    "depth": 5e-4,            # 1.4e-4 (nomap_w64)
+    "weights": 1e-3,          # 2.9e-4 (fine_sc_guided_w64)
+    "transparency": 5e-4,     # 1.6e-4 (nomap_w64)
+    "albedo": 1.8e-3,         # 5.7e-4 (fine_sc_guided_w64)
+    "sun": 2e-3,              # 6.6e-4 (fine_w64)
+    "sky": 1e-6,              # 7.6e-8: the per-ray sky MLP stays fp32
+    "z_vals": 6e-4,           # 1.7e-4 (guided / fine depths follow the bf16 weights)
+    "z_vals_unsort": 6e-4,    # 9.5e-5
+    "beta": 2.2e-3,           # 7.2e-4 (beta_w64)
+    "sem_logits": 1.5e-2,     # 4.8e-3 (fine_w64)
+}
+OUT_TOL = 2e-2       # the point-network check below (no per-key measurement)
+GRAD_TOL = 8e-2      # per tensor; measured worst 4.6e-2 (sun_v_net.2.bias projection, c3_w512)
+GRAD_TOL_ALL = 2e-2  # whole flat gradient; measured 0.4-1.6e-2 over CASES (worst fine_sc_guided_w64)
+CASES = ["c1_w512", "c3_w512", "c3_w64", "beta_w64", "nomap_w64", "c3_test_w64", "c5_w512", "fine_w64",
+         "fine_sc_guided_w64"]
+
+
+def out_tol(key: str) -> float:
+    stem = key
+    for suf in ("_coarse", "_fine"):
+        stem = stem[:-len(suf)] if stem.endswith(suf) else stem
+    stem = stem[:-3] if stem.endswith("_sc") else stem
+    return OUT_TOL_KEY[stem]
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -45,7 +71,7 @@ def test_bf16_render_close_to_reference(name):
             gu.assert_close(f"{name}:{k}", got, ref, rtol=1e-6, atol_frac=1e-7)
         worst[k] = gu.rel_err(got, ref)
     print(name, {k: f"{v:.2e}" for k, v in worst.items()})
-    bad = {k: v for k, v in worst.items() if v > OUT_TOL}
+    bad = {k: (v, out_tol(k)) for k, v in worst.items() if v > out_tol(k)}
     assert not bad, bad
 
 
@@ -129,7 +155,7 @@ def test_bf16_full_size_gradients_agree_with_fp32():
     for k in ("rgb_coarse", "depth_coarse", "sem_logits_coarse", "sun_sc_coarse"):
         e = gu.rel_err(r16[k].numpy(), r32[k].numpy())
         print(k, f"{e:.2e}")
-        assert e < OUT_TOL, (k, e)
+        assert e < out_tol(k), (k, e)
     errs = {n: gu.rel_err(g16[n].numpy(), g32[n].numpy()) for n in g32 if g32[n].abs().sum() > 0}
     print("worst grads", sorted(errs.items(), key=lambda kv: -kv[1])[:6])
     assert max(errs.values()) < GRAD_TOL, errs

@@ -82,3 +82,27 @@ def test_fused_loss_deterministic():
     a = L.FusedRenderLoss(0.1, 1.0, 1.0)(r, tgt, td, valid, tstd, labels)[0]
     b = L.FusedRenderLoss(0.1, 1.0, 1.0)(r, tgt, td, valid, tstd, labels)[0]
     assert torch.equal(a, b)
+
+
+def test_fused_loss_label_errors_are_nan_not_silent():
+    """Labels outside [0, C) other than -100 (torch raises there) make the loss and those rays'
+    logit gradients NaN; a batch with no valid label gives a NaN CE term (torch's mean over
+    nothing) and zero logit gradients; target_valid_depth=None means every ray has a prior."""
+    r, out, tgt, td, valid, tstd, labels = inputs(B=64, S=32)
+    bad = labels.clone()
+    bad[5] = 3
+    loss, terms = L.FusedRenderLoss(0.1, 1.0, 1.0)(r, tgt, td, valid, tstd, bad)
+    loss.backward()
+    assert torch.isnan(loss) and torch.isnan(terms["coarse_ss"])
+    g = r["sem_logits_coarse"].grad
+    assert torch.isnan(g[5]).all() and torch.isfinite(torch.cat([g[:5], g[6:]])).all()
+    r, out, tgt, td, valid, tstd, labels = inputs(B=64, S=32)
+    loss, terms = L.FusedRenderLoss(0.1, 1.0, 1.0)(r, tgt, td, valid, tstd, torch.full_like(labels, -100))
+    loss.backward()
+    ref = L.SemanticLoss(1.0)(r, torch.full_like(labels, -100))[0]
+    assert torch.isnan(terms["coarse_ss"]) and torch.isnan(ref)
+    assert float(r["sem_logits_coarse"].grad.abs().sum()) == 0.0
+    r, out, tgt, td, valid, tstd, labels = inputs(B=64, S=32)
+    a = L.FusedRenderLoss(0.0, 1.0, 0.0)(r, tgt, td, None, tstd)[0]
+    b = L.FusedRenderLoss(0.0, 1.0, 0.0)(r, tgt, td, torch.ones_like(valid), tstd)[0]
+    assert float(a) == float(b)

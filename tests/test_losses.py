@@ -95,3 +95,32 @@ def test_depth_loss_empty_selections_are_zero():
     assert float(got) == 0.0
     got, _ = L.DepthLoss(usealldepth=False)(res, td, tw, valid, torch.full_like(ts, 1e3))  # all inside
     assert float(got) == 0.0
+
+
+def test_gnll_ray_left_out_with_zero_spread_keeps_gradient_finite():
+    """A ray with one-hot weights (zero predicted spread) that the subset rule leaves out — no
+    depth prior — puts no NaN into the GNLL gradient (the reference computes σ_pred only on the
+    applied rays, metrics.py:90-102)."""
+    S = 8
+    w = torch.zeros(2, S)
+    w[0, 3] = 1.0                      # zero spread, invalid prior → left out
+    w[1] = torch.full((S,), 1.0 / S)   # spread out, applied
+    w.requires_grad_(True)
+    z = torch.linspace(0.1, 0.9, S).repeat(2, 1)
+    depth = (w * z).sum(1)
+    res = {"weights_coarse": w, "z_vals_coarse": z, "depth_coarse": depth}
+    loss, _ = L.DepthLoss(1.0, GNLL=True, usealldepth=False)(res, torch.tensor([0.5, 0.2]), torch.ones(2),
+                                                             torch.tensor([0, 1]), torch.tensor([0.01, 0.01]))
+    loss.backward()
+    assert torch.isfinite(loss) and torch.isfinite(w.grad).all()
+    assert float(w.grad[0].abs().sum()) == 0.0
+
+
+def test_oracle_train_loss_is_the_reference_sum():
+    """oracle/ref_cpu.train_loss (the CPU baseline's loss: main.py:143-174) = the reference's
+    SNerfLoss(0.1) + DepthLoss(1.0, subset) + SemanticLoss(0.04) values on the same inputs."""
+    x = {k: torch.tensor(D["in_" + k]) for k in CO}
+    depths = torch.stack([T("depth_t"), T("depth_w")], 1)
+    got = ref_cpu.train_loss(x, T("targets"), depths, T("valid"), T("dstd"), T("labels"), 0.1, 1.0, 0.04)
+    want = float(D["snerf_sc|loss"]) + float(D["depth_subset|loss"]) + float(D["sem|loss"])
+    np.testing.assert_allclose(float(got), want, rtol=1e-5, atol=1e-8)

@@ -5,6 +5,6 @@ cd $GRAFT_REPO_ROOT
 CONFIG=${CONFIG:-c4}
 for o in "$@"; do
 args=""; lib=libspnerf_amd.so; for kv in $o; do case $kv in lib=*) lib=${kv#lib=};; *) args="$args --option $kv";; esac; done
-r=$(SPNERF_AMD_LIB=$lib timeout -k 10 200 python bench.py --config $CONFIG --steps 20 --warmup 5 --no-cpu-baseline --no-secondary $args 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernels', {}); print(round(d['ms_per_step'],3), round(d['value']/1e6,2), {c: round(v['ms_per_step'],2) for c, v in k.items() if v['ms_per_step'] > 0.2}, 'frac', round(d['roofline']['frac'],3), 'mlp', round(d.get('mlp_gemms', {}).get('frac', 0),3))")
+r=$(SPNERF_AMD_LIB=$lib timeout -k 10 200 python bench.py --config $CONFIG --steps 20 --warmup 5 --no-cpu-baseline --no-secondary $args 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernels', {}); print(round(d['ms_per_step'],3), round(d['value']/1e6,2), {c: round(v['ms_per_step'],2) for c, v in k.items() if v['ms_per_step'] > 0.2}, 'frac', round(d['roofline']['frac'],3), 'mlp', round((d.get('mlp_mfma_utilisation') or {}).get('frac', 0),3))")
 echo "$CONFIG [$o] ms,Msps=$r"
 done
