@@ -252,6 +252,67 @@ def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int
                      "JAX_269 cameras at img_downscale 4 (JAX_214 absent); CPU side = oracle/ref_cpu.py (fp32)"}
 
 
+def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: int = 3, dev="cuda:0"):
+    """Long-horizon training parity (BASELINE.json "PSNR vs ref", north star |Δ| <= 0.05 dB):
+    the bf16 MLP (configs 3-5) against the fp32 HIP path — itself pinned to the reference at
+    1e-4 per step (tests/test_gpu_parity.py) — trained side by side for ``steps`` steps with the
+    C3 flags (64 + 64 guided samples, solar pass, depth + semantic heads, W=512; the trainer's
+    loss sum and Adam lr 5e-4, main.py:97,125-186) on the JAX_269 cameras at img_downscale 4
+    against the REAL JAX_269 images, from the same init, on the same batches, with the same
+    on-device draws (PhiloxRandom, same seed); then both render the same held-out rays."""
+    import numpy as np
+    from spnerf_amd import PhiloxRandom, random_source
+
+    c = CONFIGS["c3"]
+    args = make_args(c)
+    scene = synthetic_scene(4.0, seed=0, device=dev)
+    R = scene
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(R.rays.shape[0])
+    held, pool = torch.as_tensor(perm[:n_eval], device=dev), perm[n_eval:]
+    models, opts, srcs, curves = {}, {}, {}, {}
+    for prec in ("fp32", "bf16"):
+        torch.manual_seed(seed)
+        models[prec] = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True,
+                                         sem=True, precision=prec).to(dev).use_flat_grads()
+        opts[prec] = spnerf_amd.optim.Adam(list(models[prec].parameters()), lr=5e-4)
+        srcs[prec] = PhiloxRandom(seed=seed)
+        curves[prec] = []
+    floss = FusedRenderLoss(c["sc_lambda"], 1.0, 1.0)
+    t0 = time.perf_counter()
+    for step in range(steps):
+        idx = torch.as_tensor(rng.choice(pool, batch, replace=False), device=dev)
+        for prec in ("fp32", "bf16"):
+            m = models[prec]
+            opts[prec].zero_grad(set_to_none=True)
+            with random_source(srcs[prec]):
+                res = spnerf_amd.render_rays({"coarse": m}, args, R.rays[idx], None, semantics=R.sems[idx], mode="train",
+                                             valid_depth=R.valid_depth[idx], target_depths=R.depths[idx],
+                                             target_std=R.depth_std[idx])
+            loss, _ = floss(res, R.rgbs[idx], R.depths[idx], R.valid_depth[idx], R.depth_std[idx], R.sems[idx])
+            loss.backward()
+            opts[prec].step()
+            if step % max(1, steps // 20) == 0 or step == steps - 1:
+                curves[prec].append((step, float(loss.detach())))
+    train_s = time.perf_counter() - t0
+    psnr = {}
+    for prec in ("fp32", "bf16"):
+        rgb = []
+        with torch.no_grad(), random_source(PhiloxRandom(seed=seed + 1)):
+            for i0 in range(0, n_eval, 2048):
+                ii = held[i0:i0 + 2048]
+                rgb.append(spnerf_amd.render_rays({"coarse": models[prec]}, args, R.rays[ii], None, semantics=R.sems[ii],
+                                                  mode="test")["rgb_coarse"])
+        mse = float(torch.mean((torch.cat(rgb) - R.rgbs[held]) ** 2))
+        psnr[prec] = float(-10.0 * np.log10(mse))
+    return {"psnr_bf16_db": psnr["bf16"], "psnr_fp32_hip_db": psnr["fp32"], "delta_db": psnr["bf16"] - psnr["fp32"],
+            "steps": steps, "batch_rays": batch, "held_out_rays": n_eval, "train_seconds": train_s,
+            "loss_curve": curves, "targets": scene.rgb_source,
+            "setup": "C3 flags (64+64 guided, solar pass, depth + semantic heads, W=512) at img_downscale 4 on the "
+                     "JAX_269 cameras (JAX_214 absent), trainer's loss sum, Adam lr 5e-4, same init / batches / "
+                     "on-device Philox draws for both; the fp32 HIP path is the reference-pinned one (1e-4 per step)"}
+
+
 def ref_cpu_replay(draws):
     """The oracle's draw(kind, shape) callable over a recorded list of draws."""
     it = iter(draws)
@@ -501,6 +562,8 @@ def parse_args(argv=None):
     ap.add_argument("--torch-adam", action="store_true", help="torch.optim.Adam(fused=True) instead of spnerf_amd.optim.Adam")
     ap.add_argument("--torch-loss", action="store_true", help="the losses module (plain torch) instead of the fused loss kernels")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--psnr-steps", type=int, default=2000,
+                    help="steps of the long bf16-vs-fp32 training parity run in the default line (0 = skip)")
     ap.add_argument("--cpu-batch", type=int, default=0,
                     help="rays per CPU-baseline step (default: the GPU step's batch, at most 512)")
     ap.add_argument("--full-image", action="store_true",
@@ -580,6 +643,12 @@ def run_train(a, config, rank, world, dev, secondary=False):
     semloss = SemanticLoss(lambda_ss=1.0) if c["sem"] else None
     floss = None if a.torch_loss else FusedRenderLoss(c["sc_lambda"], 1.0 if c["depth"] else 0.0, 1.0 if c["sem"] else 0.0)
     s_final = c["n_samples"] * (2 if c["guided"] else 1)
+
+    # The production random source: draws generated inside the sampling / compositing kernels,
+    # keyed by (seed, step, GLOBAL ray id) — rank r's rays are rows r·B.. of the global batch, so
+    # an N-rank step draws what one process rendering the whole batch draws (no RNG launches)
+    from spnerf_amd import PhiloxRandom, set_random_source
+    set_random_source(PhiloxRandom(seed=0, ray_offset=rank * B))
 
     # Batch indices live in static buffers so that the captured step reads each new batch.
     idx_s = torch.empty(B, dtype=torch.int64, device=dev)
@@ -737,12 +806,17 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "final_loss": final_loss,
         "execution": ("hip graph of render+loss+backward per step, eager all-reduce + fused Adam; kernel timings "
                       f"from {prof_steps} eager steps right after the timed region") if a.graph else "eager",
+        "random_draws": "on-device Philox keyed by (seed, step, global ray id, slot) inside the sampling / "
+                        "compositing kernels (spnerf_amd.PhiloxRandom)",
     }
     del graph
+    set_random_source(None)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not secondary:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or min(B, 512))
         if config in ("c2", "c4"):
             out["psnr_parity"] = {p: psnr_parity(dev=dev, precision=p) for p in ("fp32", "bf16")}
+            if a.psnr_steps > 0 and c["precision"] == "bf16":
+                out["psnr_long"] = psnr_long(steps=a.psnr_steps, dev=dev)
     return out
 
 

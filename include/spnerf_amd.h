@@ -42,6 +42,23 @@ typedef struct spnerf_model_cfg {
     int32_t reserved[7];
 } spnerf_model_cfg;
 
+/* ---- on-device random draws (counter-based Philox keyed by seed, step and ray)
+ * The render path's draws — stratified jitter (rendering.py:143), the guided windows'
+ * uniforms (:35 via :87, :113), sample_pdf's uniforms (:35) and the sigma noise (spnerf.py:122) —
+ * are generated inside the kernels that consume them when a key is passed instead of a draw
+ * buffer: draw `i` of ray `r` in slot `s` = Philox4x32-10(counter = (ray0 + r, s << 16 | i,
+ * step), key = seed) with state = {seed, step} read from DEVICE memory (so a captured HIP graph
+ * replays with the step its caller advanced).  Uniforms take 24 bits, [0, 1) like torch's
+ * float uniform; normals are Box–Muller of two of the four words.  A draw depends only on
+ * (seed, step, ray0 + r, slot, i): data-parallel ranks that pass ray0 = their first global
+ * ray reproduce the single-process draws bit for bit. */
+typedef struct spnerf_rng {
+    const int64_t* state;  /* device {seed, step}                                             */
+    int64_t ray0;          /* global id of ray 0 of this call                                 */
+    int32_t slot;          /* draw stream (the guided sampler uses slot and slot + 1)         */
+    int32_t reserved;
+} spnerf_rng;
+
 /* mlp flags */
 #define SPNERF_MLP_SAVE 1        /* keep activations for spnerf_mlp_backward (training)      */
 #define SPNERF_MLP_SIGMA_ONLY 2  /* trunk + sigma head only (pass 1 of guided sampling)      */
@@ -87,17 +104,19 @@ int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed,
                             void* stream);
 
 /* ---- compositing: inference() (spnerf.py:109-157) --------------------------------------- */
+/* noise (n_rays, n_samples) N(0,1) draws scaled by noise_std, or NULL with rng set: drawn on the
+ * device (the backward must get the same rng) */
 int32_t spnerf_composite_forward(int64_t n_rays, int32_t n_samples, const float* z, const float* out,
                                  int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
                                  int32_t n_sem, int32_t flags, float* rgb, float* depth, float* weights,
-                                 float* transparency, float* sem_logits, void* stream);
+                                 float* transparency, float* sem_logits, const spnerf_rng* rng, void* stream);
 /* d_out (P, n_out) receives the gradient w.r.t. out (sigma, albedo, sun, sky, sem columns;
  * other columns are zeroed).  Any upstream gradient pointer may be NULL (= zero). */
 int32_t spnerf_composite_backward(int64_t n_rays, int32_t n_samples, const float* z, const float* out,
                                   int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
                                   int32_t n_sem, int32_t flags, const float* g_rgb, const float* g_depth,
                                   const float* g_weights, const float* g_transparency, const float* g_sem,
-                                  float* d_out, void* stream);
+                                  float* d_out, const spnerf_rng* rng, void* stream);
 
 /* ---- training losses (modules/metrics.py as main.py:125-174 combines them) ------------------
  * loss = SNerfLoss colour MSE (rgb, target (B,3); rgb NULL = off)                  metrics.py:27-45
@@ -130,9 +149,10 @@ int32_t spnerf_render_loss_backward(int64_t n_rays, int32_t n_samples, int32_t n
                                     float* d_rgb, float* d_sun_sc, float* d_depth, float* d_logits, void* stream);
 
 /* ---- sample generation (rendering.py) --------------------------------------------------- */
-/* stratified jittered depths, perturb = 1 (rendering.py:131-144); u (n_rays, n) in [0,1) */
+/* stratified jittered depths, perturb = 1 (rendering.py:131-144); u (n_rays, n) in [0,1), or
+ * NULL with rng set (drawn on the device) */
 int32_t spnerf_sample_stratified(int64_t n_rays, int32_t n_samples, const float* rays, int32_t ray_stride,
-                                 const float* u, float* z, void* stream);
+                                 const float* u, float* z, const spnerf_rng* rng, void* stream);
 /* GenerateGuidedSamples + sort + merge (rendering.py:92-116,165-167): 3-sigma window around
  * the pass-1 depth, replaced by the GT window on rays with valid_depth > 0 (valid_depth may be
  * NULL = test mode), clamped to clamp_nf[0..1] (device; the chunk's first-ray near/far,
@@ -142,11 +162,12 @@ int32_t spnerf_sample_guided(int64_t n_rays, int32_t n_samples, const float* z, 
                              const float* weights, const float* clamp_nf, const int64_t* valid_depth,
                              const float* target_depths, int32_t td_stride, const float* target_std,
                              const float* u_pred, const float* u_gt, float* z_sorted, float* z_unsort,
-                             void* stream);
+                             const spnerf_rng* rng, void* stream);
 /* sample_pdf (rendering.py:14-55): bins (n_rays, n_bins+1), weights (n_rays, n_bins),
  * u (n_rays, n_imp) → samples (n_rays, n_imp). n_bins+1 <= 256, n_imp <= 256. */
 int32_t spnerf_sample_pdf(int64_t n_rays, int32_t n_bins, const float* bins, const float* weights,
-                          int32_t n_imp, const float* u, float eps, float* samples, void* stream);
+                          int32_t n_imp, const float* u, float eps, float* samples, const spnerf_rng* rng,
+                          void* stream);
 /* sample_3sigma (rendering.py:58-73): low/high (n_rays), u (n_rays, n) → (n_rays, n) */
 int32_t spnerf_sample_3sigma(int64_t n_rays, int32_t n, const float* low, const float* high,
                              const float* clamp_nf, const float* u, float* out, void* stream);

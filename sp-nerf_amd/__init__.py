@@ -15,7 +15,7 @@ from .rendering import (GenerateGuidedSamples, compute_samples_around_depth, ren
                         sample_pdf, stratified)
 from . import optim  # noqa: F401  (optim.Adam: the library's one-launch Adam step)
 from . import dsm  # noqa: F401  (DSM extraction: satellite_scene.py:475-568 on the GPU)
-from .rng import ReplayRandom, TorchRandom, current_random_source, random_source, set_random_source  # noqa: F401
+from .rng import PhiloxRandom, ReplayRandom, TorchRandom, current_random_source, random_source, set_random_source  # noqa: F401
 from .spnerf import (SPNeRF, Mapping, Siren, first_layer_sine_init, inference, inference_rays, run_mlp,  # noqa: F401
                      sine_init)
 

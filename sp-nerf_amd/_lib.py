@@ -31,6 +31,17 @@ class ModelCfg(ctypes.Structure):
         return tuple(getattr(self, f) for f, _ in self._fields_[:-1])
 
 
+class Rng(ctypes.Structure):
+    """spnerf_rng (include/spnerf_amd.h): on-device Philox draws keyed by the device state
+    {seed, step}, the call's first global ray id and a draw slot."""
+    _fields_ = [("state", c_void_p), ("ray0", c_int64), ("slot", c_int32), ("reserved", c_int32)]
+
+
+def rng_ref(r):
+    """ctypes argument for an optional spnerf_rng (None = NULL)."""
+    return None if r is None else ctypes.byref(r)
+
+
 # name → (restype, argtypes); the exact export list of include/spnerf_amd.h
 SIGNATURES = {
     "spnerf_last_error": (c_char_p, []),
@@ -45,10 +56,11 @@ SIGNATURES = {
     "spnerf_mlp_backward": (c_int32, [POINTER(ModelCfg), c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p,
                                       c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "spnerf_composite_forward": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_int32,
-                                           c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                           c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           POINTER(Rng), c_void_p]),
     "spnerf_composite_backward": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_int32,
                                             c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                            c_void_p]),
+                                            POINTER(Rng), c_void_p]),
     "spnerf_render_loss_workspace_bytes": (c_int64, [c_int64]),
     "spnerf_render_loss_forward": (c_int32, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_float, c_void_p, c_int32,
                                              c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -58,10 +70,11 @@ SIGNATURES = {
                                               c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_int32, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "spnerf_sample_stratified": (c_int32, [c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "spnerf_sample_stratified": (c_int32, [c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, POINTER(Rng), c_void_p]),
     "spnerf_sample_guided": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                       c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "spnerf_sample_pdf": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_void_p, c_void_p]),
+                                       c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, POINTER(Rng), c_void_p]),
+    "spnerf_sample_pdf": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_void_p,
+                                    POINTER(Rng), c_void_p]),
     "spnerf_sample_3sigma": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "spnerf_sort_rows": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     "spnerf_rpc_rays": (c_int32, [POINTER(c_double), c_double, c_double, c_double, c_int32, c_int32, c_int32, c_int32,

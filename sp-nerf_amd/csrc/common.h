@@ -162,6 +162,43 @@ __device__ __forceinline__ int xcd_remap(int id, int nb) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// ---- on-device draws: Philox4x32-10 keyed by (seed, step, ray, slot, index) (spnerf_rng) ----
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], const uint32_t (&k)[2]) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+    const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k[0], n2 = hi0 ^ c[3] ^ k[1];
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+}
+// the four 32-bit words of draw `idx` of ray `ray` in `slot`
+__device__ __forceinline__ void philox_words(const spnerf_rng& r, int64_t ray, int idx, uint32_t (&c)[4]) {
+    const uint64_t seed = (uint64_t)r.state[0], step = (uint64_t)r.state[1];
+    const uint64_t id = (uint64_t)(r.ray0 + ray);
+    c[0] = (uint32_t)id; c[1] = (uint32_t)(id >> 32);
+    c[2] = ((uint32_t)r.slot << 16) | (uint32_t)idx; c[3] = (uint32_t)step;
+    uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(step >> 32)};
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        philox_round(c, k);
+        k[0] += 0x9E3779B9u;
+        k[1] += 0xBB67AE85u;
+    }
+}
+// uniform in [0, 1) with 24 random bits (torch's float uniform resolution)
+__device__ __forceinline__ float rng_uniform(const spnerf_rng& r, int64_t ray, int idx) {
+    uint32_t c[4];
+    philox_words(r, ray, idx, c);
+    return (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+}
+// standard normal (Box–Muller of two words; u1 in (0, 1])
+__device__ __forceinline__ float rng_normal(const spnerf_rng& r, int64_t ray, int idx) {
+    uint32_t c[4];
+    philox_words(r, ray, idx, c);
+    const float u1 = (float)((c[1] >> 8) + 1u) * (1.0f / 16777216.0f);
+    const float u2 = (float)(c[2] >> 8) * (1.0f / 16777216.0f);
+    return sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795865f * u2);
+}
+
 // torch-compatible elementwise pieces (ATen CPU formulas)
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float softplusf_(float x) { return x > 20.0f ? x : log1pf(expf(x)); }

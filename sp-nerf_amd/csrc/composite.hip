@@ -21,6 +21,7 @@ struct CompArgs {
     int S, NO, sem_col, n_sem, weights_only;
     const float *z, *out, *noise;
     float noise_std;
+    spnerf_rng rng;   // noise drawn on the device when rng.state is set (and noise is null)
     float *rgb, *depth, *w, *T, *sem;
     const float *g_rgb, *g_depth, *g_w, *g_T, *g_sem;
     float* d_out;
@@ -51,6 +52,7 @@ __device__ __forceinline__ void march(const CompArgs& a, int64_t ray, int lane, 
             const int64_t p = ray * S + e;
             float sg = rows[e * a.NO + 3];
             if (a.noise) sg = sg + a.noise[p] * a.noise_std;
+            else if (a.rng.state) sg = sg + rng_normal(a.rng, ray, e) * a.noise_std;
             const float zn = j + 1 < EPL ? st.z[j + 1] : zn0;
             const float dl = e == S - 1 ? 1e10f : zn - st.z[j];
             const float r = relu_t(sg);
@@ -327,7 +329,7 @@ using namespace spn;
 extern "C" int32_t spnerf_composite_forward(int64_t n_rays, int32_t n_samples, const float* z, const float* out,
                                             int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
                                             int32_t n_sem, int32_t flags, float* rgb, float* depth, float* weights,
-                                            float* transparency, float* sem_logits, void* stream) {
+                                            float* transparency, float* sem_logits, const spnerf_rng* rng, void* stream) {
     const bool wo = flags & SPNERF_COMP_WEIGHTS_ONLY;
     SPN_ARG(z && out && depth && weights && transparency, "composite_forward: NULL pointer");
     SPN_ARG(wo || rgb, "composite_forward: rgb is NULL");
@@ -335,6 +337,7 @@ extern "C" int32_t spnerf_composite_forward(int64_t n_rays, int32_t n_samples, c
     CompArgs a{};
     a.B = n_rays; a.S = n_samples; a.NO = n_out; a.sem_col = sem_col; a.n_sem = wo ? 0 : n_sem; a.weights_only = wo;
     a.z = z; a.out = out; a.noise = noise; a.noise_std = noise_std;
+    if (!noise && rng && noise_std != 0.f) a.rng = *rng;
     a.rgb = rgb; a.depth = depth; a.w = weights; a.T = transparency; a.sem = sem_logits;
     return run_comp(a, true, (hipStream_t)stream);
 }
@@ -343,12 +346,13 @@ extern "C" int32_t spnerf_composite_backward(int64_t n_rays, int32_t n_samples, 
                                              int32_t n_out, const float* noise, float noise_std, int32_t sem_col,
                                              int32_t n_sem, int32_t flags, const float* g_rgb, const float* g_depth,
                                              const float* g_weights, const float* g_transparency, const float* g_sem,
-                                             float* d_out, void* stream) {
+                                             float* d_out, const spnerf_rng* rng, void* stream) {
     const bool wo = flags & SPNERF_COMP_WEIGHTS_ONLY;
     SPN_ARG(z && out && d_out, "composite_backward: NULL pointer");
     CompArgs a{};
     a.B = n_rays; a.S = n_samples; a.NO = n_out; a.sem_col = sem_col; a.n_sem = wo ? 0 : n_sem; a.weights_only = wo;
     a.z = z; a.out = out; a.noise = noise; a.noise_std = noise_std;
+    if (!noise && rng && noise_std != 0.f) a.rng = *rng;
     a.g_rgb = g_rgb; a.g_depth = g_depth; a.g_w = g_weights; a.g_T = g_transparency; a.g_sem = g_sem;
     a.d_out = d_out;
     return run_comp(a, false, (hipStream_t)stream);

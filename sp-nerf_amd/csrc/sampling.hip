@@ -13,8 +13,9 @@
 
 namespace spn {
 
+// u: the draws, or null: drawn on the device from rng (spnerf_rng)
 __global__ void k_stratified(int64_t B, int S, const float* __restrict__ rays, int rs, const float* __restrict__ u,
-                             float* __restrict__ z) {
+                             float* __restrict__ z, spnerf_rng rng) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= B * S) return;
     const int64_t ray = i / S;
@@ -27,7 +28,8 @@ __global__ void k_stratified(int64_t B, int S, const float* __restrict__ rays, i
     const float zc = zl(k);
     const float hi = k < S - 1 ? __fmul_rn(0.5f, __fadd_rn(zc, zl(k + 1))) : zc;
     const float lo = k > 0 ? __fmul_rn(0.5f, __fadd_rn(zl(k - 1), zc)) : zc;
-    z[i] = __fadd_rn(lo, __fmul_rn(__fsub_rn(hi, lo), u[i]));
+    const float ui = u ? u[i] : rng_uniform(rng, ray, k);
+    z[i] = __fadd_rn(lo, __fmul_rn(__fsub_rn(hi, lo), ui));
 }
 
 struct WaveLds {
@@ -119,8 +121,9 @@ struct GuidedArgs {
     const int64_t* valid;
     const float *tdepth, *tstd;
     int td_stride;
-    const float *u_pred, *u_gt;
+    const float *u_pred, *u_gt;   // or null: drawn from rng, slots rng.slot (pred) / rng.slot + 1 (GT)
     float *z_sorted, *z_unsort;
+    spnerf_rng rng;
 };
 
 template <int EPL>
@@ -145,12 +148,15 @@ __global__ __launch_bounds__(256) void k_guided(GuidedArgs a) {
     }
     const float sd = sqrtf(wave_sum(s));
     float low = dep - 3.f * sd, high = dep + 3.f * sd;
-    const float* u = a.u_pred + rr * N;
+    const bool dev_rng = a.u_pred == nullptr;
+    const float* u = dev_rng ? nullptr : a.u_pred + rr * N;
+    spnerf_rng rk = a.rng;
     if (a.valid && a.valid[rr] > 0) {  // GT window replaces the predicted one (:98-114)
         const float gt = a.tdepth[rr * a.td_stride], gs = a.tstd[rr];
         low = gt - 3.f * gs;
         high = gt + 3.f * gs;
-        u = a.u_gt + rr * N;
+        if (dev_rng) rk.slot += 1;
+        else u = a.u_gt + rr * N;
     }
     const float nr = a.clamp_nf[0], fr = a.clamp_nf[1];
     float w[EPL];
@@ -160,7 +166,8 @@ __global__ __launch_bounds__(256) void k_guided(GuidedArgs a) {
     // 2N slots: [0,N) guided samples (sorted first, rendering.py:165), [N,2N) stratified
     int n2 = 1;
     while (n2 < 2 * N) n2 <<= 1;
-    for (int e = lane; e < n2; e += 64) L.buf[e] = e < N ? invert_cdf(L, N - 1, u[e], 1e-5f) : INFINITY;
+    for (int e = lane; e < n2; e += 64)
+        L.buf[e] = e < N ? invert_cdf(L, N - 1, dev_rng ? rng_uniform(rk, rr, e) : u[e], 1e-5f) : INFINITY;
     __syncthreads();
     int n1 = 1;
     while (n1 < N) n1 <<= 1;
@@ -189,10 +196,11 @@ __global__ __launch_bounds__(256) void k_guided(GuidedArgs a) {
 struct PdfArgs {
     int64_t B;
     int nb, n_imp;
-    const float *bins, *w, *u;
+    const float *bins, *w, *u;   // u null: drawn from rng
     float eps;
     float* out;
     const float *low, *high, *clamp_nf;  // sample_3sigma mode when low != nullptr
+    spnerf_rng rng;
 };
 
 template <int EPL>
@@ -219,7 +227,7 @@ __global__ __launch_bounds__(256) void k_sample_pdf(PdfArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (int e = lane; e < a.n_imp; e += 64)
-        a.out[ray * a.n_imp + e] = invert_cdf(L, nb, a.u[ray * a.n_imp + e], a.eps);
+        a.out[ray * a.n_imp + e] = invert_cdf(L, nb, a.u ? a.u[ray * a.n_imp + e] : rng_uniform(a.rng, ray, e), a.eps);
 }
 
 __global__ __launch_bounds__(256) void k_sort_rows(int64_t B, int n, const float* __restrict__ in, float* __restrict__ out) {
@@ -240,14 +248,16 @@ __global__ __launch_bounds__(256) void k_sort_rows(int64_t B, int n, const float
 
 using namespace spn;
 
+static spnerf_rng rng_or_null(const spnerf_rng* r) { return r ? *r : spnerf_rng{nullptr, 0, 0, 0}; }
+
 extern "C" int32_t spnerf_sample_stratified(int64_t n_rays, int32_t n_samples, const float* rays, int32_t ray_stride,
-                                            const float* u, float* z, void* stream) {
-    SPN_ARG(rays && u && z, "sample_stratified: NULL pointer");
+                                            const float* u, float* z, const spnerf_rng* rng, void* stream) {
+    SPN_ARG(rays && z && (u || (rng && rng->state)), "sample_stratified: NULL pointer");
     SPN_ARG(n_samples >= 2 && ray_stride >= 8 && n_rays >= 0, "sample_stratified: bad sizes");
     const int64_t n = n_rays * n_samples;
     if (n == 0) return SPNERF_OK;
     hipLaunchKernelGGL(k_stratified, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n_rays,
-                       n_samples, rays, ray_stride, u, z);
+                       n_samples, rays, ray_stride, u, z, rng_or_null(rng));
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
@@ -256,13 +266,15 @@ extern "C" int32_t spnerf_sample_guided(int64_t n_rays, int32_t n_samples, const
                                         const float* weights, const float* clamp_nf, const int64_t* valid_depth,
                                         const float* target_depths, int32_t td_stride, const float* target_std,
                                         const float* u_pred, const float* u_gt, float* z_sorted, float* z_unsort,
-                                        void* stream) {
-    SPN_ARG(z && depth && weights && clamp_nf && u_pred && z_sorted && z_unsort, "sample_guided: NULL pointer");
-    SPN_ARG(!valid_depth || (target_depths && target_std && u_gt), "sample_guided: train mode needs GT inputs");
+                                        const spnerf_rng* rng, void* stream) {
+    const bool dev_rng = u_pred == nullptr;
+    SPN_ARG(z && depth && weights && clamp_nf && z_sorted && z_unsort && (!dev_rng || (rng && rng->state)),
+            "sample_guided: NULL pointer");
+    SPN_ARG(!valid_depth || (target_depths && target_std && (u_gt || dev_rng)), "sample_guided: train mode needs GT inputs");
     SPN_ARG(n_samples >= 2 && n_samples <= 128, "sample_guided: n_samples %d must be in [2, 128]", n_samples);
     if (n_rays == 0) return SPNERF_OK;
     GuidedArgs a{n_rays, n_samples, z, depth, weights, clamp_nf, valid_depth, target_depths, target_std, td_stride,
-                 u_pred, u_gt, z_sorted, z_unsort};
+                 u_pred, dev_rng ? nullptr : u_gt, z_sorted, z_unsort, rng_or_null(rng)};
     const dim3 g((unsigned)((n_rays + 3) / 4)), b(256);
     ProfScope prof("sample_guided", (hipStream_t)stream, 0.0, (double)n_rays * n_samples * 4.0 * 7.0);
     if (n_samples <= 64) hipLaunchKernelGGL(k_guided<1>, g, b, 0, (hipStream_t)stream, a);
@@ -281,11 +293,12 @@ static int32_t launch_pdf(const PdfArgs& a, int nbins, hipStream_t s) {
 }
 
 extern "C" int32_t spnerf_sample_pdf(int64_t n_rays, int32_t n_bins, const float* bins, const float* weights,
-                                     int32_t n_imp, const float* u, float eps, float* samples, void* stream) {
-    SPN_ARG(bins && weights && u && samples, "sample_pdf: NULL pointer");
+                                     int32_t n_imp, const float* u, float eps, float* samples, const spnerf_rng* rng,
+                                     void* stream) {
+    SPN_ARG(bins && weights && samples && (u || (rng && rng->state)), "sample_pdf: NULL pointer");
     SPN_ARG(n_bins >= 1 && n_bins + 1 <= 256 && n_imp >= 1, "sample_pdf: n_bins %d / n_imp %d out of range", n_bins, n_imp);
     if (n_rays == 0) return SPNERF_OK;
-    PdfArgs a{n_rays, n_bins, n_imp, bins, weights, u, eps, samples, nullptr, nullptr, nullptr};
+    PdfArgs a{n_rays, n_bins, n_imp, bins, weights, u, eps, samples, nullptr, nullptr, nullptr, rng_or_null(rng)};
     return launch_pdf(a, n_bins, (hipStream_t)stream);
 }
 
@@ -294,7 +307,7 @@ extern "C" int32_t spnerf_sample_3sigma(int64_t n_rays, int32_t n, const float* 
     SPN_ARG(low && high && clamp_nf && u && out, "sample_3sigma: NULL pointer");
     SPN_ARG(n >= 2 && n <= 256, "sample_3sigma: n %d out of range", n);
     if (n_rays == 0) return SPNERF_OK;
-    PdfArgs a{n_rays, n - 1, n, nullptr, nullptr, u, 1e-5f, out, low, high, clamp_nf};
+    PdfArgs a{n_rays, n - 1, n, nullptr, nullptr, u, 1e-5f, out, low, high, clamp_nf, spnerf_rng{nullptr, 0, 0, 0}};
     return launch_pdf(a, n, (hipStream_t)stream);
 }
 

@@ -22,18 +22,20 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .rng import current_random_source
+from .rng import begin_render, current_random_source, device_key
 from .spnerf import inference_rays, pack_for_render
 
 
-def stratified(rays: torch.Tensor, n_samples: int, u: torch.Tensor) -> torch.Tensor:
-    """z = lower + (upper - lower)·u over [near, far] (rendering.py:131-144, perturb = 1)."""
+def stratified(rays: torch.Tensor, n_samples: int, u: torch.Tensor = None, rng=None) -> torch.Tensor:
+    """z = lower + (upper - lower)·u over [near, far] (rendering.py:131-144, perturb = 1); with
+    ``rng`` (an spnerf_rng) instead of ``u`` the jitter is drawn on the device."""
     _lib.require_device(rays, u)
     rays = rays.contiguous().float()
-    u = u.contiguous().float()
+    u = None if u is None else u.contiguous().float()
     z = torch.empty(rays.shape[0], n_samples, device=rays.device)
     _lib.check(_lib.lib().spnerf_sample_stratified(rays.shape[0], n_samples, _lib.ptr(rays), rays.stride(0), _lib.ptr(u),
-                                                   _lib.ptr(z), _lib.stream_of(rays)), "sample_stratified")
+                                                   _lib.ptr(z), _lib.rng_ref(rng), _lib.stream_of(rays)),
+               "sample_stratified")
     return z
 
 
@@ -42,14 +44,17 @@ def sample_pdf(bins, weights, N_importance, det=False, eps=1e-5):
     CDF in searchsorted — here it uses the intended ``linspace(0,1,N)`` for every ray.)"""
     _lib.require_device(bins, weights)
     B, nb = weights.shape
+    key = keep = None
     if det:
         u = torch.linspace(0, 1, N_importance, device=bins.device).expand(B, N_importance).contiguous()
     else:
-        u = current_random_source().rand((B, N_importance), bins.device)
+        key, keep = device_key(bins.device)
+        u = None if key is not None else current_random_source().rand((B, N_importance), bins.device)
     out = torch.empty(B, N_importance, device=bins.device)
-    b, w, uu = bins.contiguous().float(), weights.contiguous().float(), u.contiguous().float()
+    b, w = bins.contiguous().float(), weights.contiguous().float()
+    uu = None if u is None else u.contiguous().float()
     _lib.check(_lib.lib().spnerf_sample_pdf(B, nb, _lib.ptr(b), _lib.ptr(w), N_importance, _lib.ptr(uu), float(eps),
-                                            _lib.ptr(out), _lib.stream_of(bins)), "sample_pdf")
+                                            _lib.ptr(out), _lib.rng_ref(key), _lib.stream_of(bins)), "sample_pdf")
     return out
 
 
@@ -97,7 +102,8 @@ def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std, 
     B = z_vals.shape[0]
     dev = z_vals.device
     src = current_random_source()
-    u_pred = src.rand((B, n), dev).contiguous().float()                     # rendering.py:35 via :87
+    key, keep = device_key(dev, 2)   # on-device draws: slots key.slot (pred) and key.slot + 1 (GT)
+    u_pred = None if key is not None else src.rand((B, n), dev).contiguous().float()   # rendering.py:35 via :87
     valid = tdep = tstd = u_gt = None
     td_stride = 2
     if mode == "train":
@@ -106,7 +112,8 @@ def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std, 
         tdep = target_depths.to(device=dev, dtype=torch.float32).contiguous()
         td_stride = tdep.stride(0)
         tstd = target_std.reshape(-1).to(device=dev, dtype=torch.float32).contiguous()
-        u_gt = src.gt_uniform(valid, n, dev).contiguous().float()             # rendering.py:113
+        if key is None:
+            u_gt = src.gt_uniform(valid, n, dev).contiguous().float()         # rendering.py:113
     z_sorted = torch.empty(B, 2 * n, device=dev)
     z_unsort = torch.empty(B, 2 * n, device=dev)
     if clamp_nf is None:
@@ -115,8 +122,8 @@ def _guided(res, z_vals, n, rays, mode, valid_depth, target_depths, target_std, 
     _lib.check(_lib.lib().spnerf_sample_guided(B, n, _lib.ptr(z_vals), _lib.ptr(depth),
                                                _lib.ptr(weights), _lib.ptr(clamp_nf), _lib.ptr(valid),
                                                _lib.ptr(tdep), td_stride, _lib.ptr(tstd), _lib.ptr(u_pred), _lib.ptr(u_gt),
-                                               _lib.ptr(z_sorted), _lib.ptr(z_unsort), _lib.stream_of(z_vals)),
-               "sample_guided")
+                                               _lib.ptr(z_sorted), _lib.ptr(z_unsort), _lib.rng_ref(key),
+                                               _lib.stream_of(z_vals)), "sample_guided")
     return z_sorted, z_unsort
 
 
@@ -156,8 +163,12 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
     _lib.require_device(rays)
     rays = rays.contiguous().float()
     B = rays.shape[0]
-    src = current_random_source()
-    z_vals = stratified(rays, N_samples, src.rand((B, N_samples), rays.device))   # rendering.py:143
+    begin_render(rays.device)         # a keyed on-device random source starts a new step
+    key, keep = device_key(rays.device)
+    if key is not None:
+        z_vals = stratified(rays, N_samples, rng=key)
+    else:
+        z_vals = stratified(rays, N_samples, current_random_source().rand((B, N_samples), rays.device))  # rendering.py:143
     model = models["coarse"]
     rays_t = None
     if args.beta:

@@ -9,7 +9,11 @@ per inference call (spnerf.py:122), ``rand (B,S)`` for the predicted-depth windo
 skips the σ-noise draw when ``noise_std == 0`` (the product with 0 is exactly 0) and draws
 the GT-window ``u`` for every ray, indexed by ray, so no host synchronisation is needed to
 count the valid rays.  ``ReplayRandom`` hands back pre-recorded draws (the reference's, in
-the parity tests) in the reference's order and shapes.
+the parity tests) in the reference's order and shapes.  ``PhiloxRandom`` draws nothing on the
+host: the kernels that consume a draw generate it themselves (counter-based Philox4x32-10,
+spnerf_rng in include/spnerf_amd.h) from (seed, step, global ray id, draw slot), so the draws
+of a ray do not depend on which rank renders it or with which other rays, and a render launches
+no RNG kernels.
 """
 from __future__ import annotations
 
@@ -58,6 +62,77 @@ class ReplayRandom:
         full = torch.zeros(valid_mask.shape[0], n)
         full[sel] = arr
         return full.to(device)
+
+
+class PhiloxRandom:
+    """On-device draws keyed by (seed, step, global ray id, slot) — SURVEY §8(b).
+
+    Each ``render_rays`` is one step: ``begin_render`` advances the step in a device counter
+    (an in-place add, so a captured HIP graph advances it on every replay) and snapshots
+    {seed, step} into a tensor of its own that the render's kernels — and its backward's — read.
+    Within a render every draw stream takes the next slot, in the render's fixed call order (the
+    guided sampler takes two).  ``ray_offset`` is the global id of the call's first ray: a
+    data-parallel rank passes rank · rays_per_rank and draws what a single process rendering
+    the whole batch draws for those rays."""
+
+    on_device = True
+
+    def __init__(self, seed: int = 0, ray_offset: int = 0):
+        self.seed, self.ray_offset = int(seed), int(ray_offset)
+        self._state = None
+        self._snap = None
+        self._slot = 0
+
+    def begin_render(self, device):
+        if self._state is None or self._state.device != torch.device(device):
+            self._state = torch.tensor([self.seed, -1], dtype=torch.int64, device=device)
+        self._state[1:].add_(1)
+        self._snap = self._state.clone()
+        self._slot = 0
+
+    def key(self, device, nslots: int = 1):
+        """(spnerf_rng, the tensor it points at — keep it alive while a kernel may read it)"""
+        from ._lib import Rng
+        if self._snap is None:
+            self.begin_render(device)
+        r = Rng(self._snap.data_ptr(), self.ray_offset, self._slot, 0)
+        self._slot += nslots
+        return r, self._snap
+
+    # draws a host-side caller asks for as tensors (the standalone drop-ins, e.g. sample_3sigma):
+    # a generator seeded from the key, not rank-keyed per ray
+    def _gen(self, device):
+        step = int(self._state[1]) if self._state is not None else 0
+        g = torch.Generator(device=device)
+        g.manual_seed((self.seed * 1000003 + step * 8191 + self._slot) & ((1 << 63) - 1))
+        self._slot += 1
+        return g
+
+    def rand(self, shape, device):
+        return torch.rand(shape, device=device, generator=self._gen(device))
+
+    def noise(self, shape, device, noise_std):
+        if noise_std == 0:
+            return None
+        return torch.randn(shape, device=device, generator=self._gen(device))
+
+    def gt_uniform(self, valid_mask, n, device):
+        return self.rand((valid_mask.shape[0], n), device)
+
+
+def begin_render(device) -> None:
+    """Start of a render_rays call: a keyed on-device source advances its step."""
+    src = current_random_source()
+    if getattr(src, "on_device", False):
+        src.begin_render(device)
+
+
+def device_key(device, nslots: int = 1):
+    """(spnerf_rng, keep-alive) of the current source when it draws on the device, else (None, None)."""
+    src = current_random_source()
+    if getattr(src, "on_device", False):
+        return src.key(device, nslots)
+    return None, None
 
 
 _state = threading.local()

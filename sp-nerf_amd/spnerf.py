@@ -21,7 +21,7 @@ import torch
 from . import _lib
 from ._lib import (SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_ACCUMULATE, SPNERF_MLP_SAVE, SPNERF_MLP_SIGMA_ONLY,
                    SPNERF_MLP_SUN_ONLY)
-from .rng import current_random_source
+from .rng import current_random_source, device_key
 
 
 class Mapping(torch.nn.Module):
@@ -422,7 +422,7 @@ def max_points_per_call(model: SPNeRF) -> int:
 
 class _Composite(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, out, z, noise, noise_std, sem_col, n_sem, weights_only):
+    def forward(ctx, out, z, noise, noise_std, sem_col, n_sem, weights_only, rng=None, rng_keep=None):
         B, S = z.shape
         NO = out.shape[1]
         dev = out.device
@@ -434,10 +434,11 @@ class _Composite(torch.autograd.Function):
         T = torch.empty(B, S, device=dev)
         _lib.check(_lib.lib().spnerf_composite_forward(B, S, _lib.ptr(z), _lib.ptr(out), NO, _lib.ptr(noise),
                                                        float(noise_std), sem_col, n_sem, f, _lib.ptr(rgb), _lib.ptr(depth),
-                                                       _lib.ptr(w), _lib.ptr(T), _lib.ptr(sem), _lib.stream_of(out)),
-                   "composite_forward")
+                                                       _lib.ptr(w), _lib.ptr(T), _lib.ptr(sem), _lib.rng_ref(rng),
+                                                       _lib.stream_of(out)), "composite_forward")
         ctx.save_for_backward(out, z, noise)
         ctx.cfg = (float(noise_std), sem_col, n_sem, f)
+        ctx.rng, ctx.rng_keep = rng, rng_keep   # the backward redraws the same on-device noise
         ctx.set_materialize_grads(False)
         return rgb, depth, w, T, sem
 
@@ -452,19 +453,21 @@ class _Composite(torch.autograd.Function):
         _lib.check(_lib.lib().spnerf_composite_backward(B, S, _lib.ptr(z), _lib.ptr(out), out.shape[1], _lib.ptr(noise),
                                                         noise_std, sem_col, n_sem, f, _lib.ptr(g_rgb),
                                                         _lib.ptr(g_depth), _lib.ptr(g_w), _lib.ptr(g_T),
-                                                        _lib.ptr(g_sem), _lib.ptr(d_out), _lib.stream_of(out)),
-                   "composite_backward")
-        return d_out, None, None, None, None, None, None
+                                                        _lib.ptr(g_sem), _lib.ptr(d_out), _lib.rng_ref(ctx.rng),
+                                                        _lib.stream_of(out)), "composite_backward")
+        return d_out, None, None, None, None, None, None, None, None
 
 
 def composite(model: SPNeRF, out: torch.Tensor, z: torch.Tensor, noise_std: float, weights_only=False):
     B, S = z.shape
-    noise = current_random_source().noise((B, S), z.device, noise_std)       # spnerf.py:122
+    key, keep = device_key(z.device)   # on-device σ noise: a slot per inference call, drawn or not
+    noise = None if key is not None else current_random_source().noise((B, S), z.device, noise_std)   # spnerf.py:122
     if noise is not None:
         noise = noise.contiguous().float()
     sem_col = 8 + (1 if model.beta else 0)
     n_sem = model.num_sem_classes if model.sem else 0
-    return _Composite.apply(out, z.contiguous(), noise, noise_std, sem_col, n_sem, weights_only)
+    return _Composite.apply(out, z.contiguous(), noise, noise_std, sem_col, n_sem, weights_only,
+                            key if noise_std != 0 else None, keep)
 
 
 def _result(model, out, z, rgb, depth, w, T, sem, z_unsort=None):

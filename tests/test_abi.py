@@ -74,7 +74,7 @@ def test_errors_are_reported_not_fallen_back():
     assert L.spnerf_param_count(ctypes.byref(c)) < 0
     assert b"width" in L.spnerf_last_error()
     assert L.spnerf_mlp_workspace_bytes(ctypes.byref(c), 10, 64, 0) == -1
-    assert L.spnerf_sample_stratified(4, 64, None, 11, None, None, None) == -1
+    assert L.spnerf_sample_stratified(4, 64, None, 11, None, None, None, None) == -1
     assert b"NULL" in L.spnerf_last_error()
 
 

@@ -127,3 +127,64 @@ def test_two_ranks_on_hip_equal_single_process(tmp_path, precision, tol):
     print(precision, f"flat {total:.2e}", sorted(worst.items(), key=lambda kv: -kv[1])[:4])
     assert total < tol, total
     assert max(worst.values()) < 10 * tol, worst
+
+
+def render_slice(rank, world, precision="bf16", noise_std=0.0):
+    """C3-flags render of this rank's slice of the shared-seed global batch with the production
+    random source, spnerf_amd.PhiloxRandom (draws generated inside the kernels, keyed by seed,
+    step and GLOBAL ray id: ray_offset = rank · rays per rank); per-ray outputs on the host."""
+    import types
+    import spnerf_amd
+    from spnerf_amd import dp
+    from spnerf_amd.scene import synthetic_scene
+    dev = torch.device("cuda", 0)
+    scene = synthetic_scene(4.0, seed=0, device=dev)
+    sampler = dp.SharedSeedSampler(scene.rays.shape[0], GLOBAL_B, rank, world, seed=5, device=dev)
+    gidx, idx = sampler.next()
+    b = GLOBAL_B // world
+    torch.manual_seed(0)
+    model = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True, precision=precision).to(dev)
+    args = types.SimpleNamespace(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+                                 sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=noise_std)
+    R = scene
+    outs = []
+    with spnerf_amd.random_source(spnerf_amd.PhiloxRandom(seed=11, ray_offset=rank * b)), torch.no_grad():
+        for _ in range(2):   # two renders = two steps: the draws must move on
+            res = spnerf_amd.render_rays({"coarse": model}, args, R.rays[idx], None, semantics=R.sems[idx], mode="train",
+                                         valid_depth=R.valid_depth[idx], target_depths=R.depths[idx],
+                                         target_std=R.depth_std[idx], clamp_near_far=R.rays[gidx[0], 6:8])
+            outs.append({k: v.detach().cpu().numpy() for k, v in res.items()})
+    return outs
+
+
+def _render_worker(rank, world, port, outdir, noise_std):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    from spnerf_amd import dp
+    torch.cuda.set_device(0)
+    dp.init_from_env("gloo")
+    outs = render_slice(rank, world, noise_std=noise_std)
+    np.savez(os.path.join(outdir, f"render{rank}.npz"), **{f"{i}|{k}": v for i, o in enumerate(outs) for k, v in o.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("noise_std", [0.0, 0.5])
+def test_two_ranks_philox_renders_equal_single_process_bitwise(tmp_path, noise_std):
+    """On-device Philox draws keyed by (seed, step, global ray id, slot): two gloo ranks that each
+    render half of the global batch produce, ray for ray, exactly the single-process render of the
+    whole batch — stratified jitter, guided windows (predicted and GT), σ noise — over two steps,
+    with no replayed draw tables; and the second step's draws differ from the first's."""
+    world = 2
+    mp.spawn(_render_worker, args=(world, _free_port(), str(tmp_path), noise_std), nprocs=world, join=True)
+    parts = [dict(np.load(tmp_path / f"render{r}.npz")) for r in range(world)]
+    single = render_slice(0, 1, noise_std=noise_std)
+    for step, ref in enumerate(single):
+        for k, v in ref.items():
+            got = np.concatenate([p[f"{step}|{k}"] for p in parts])
+            assert got.shape == v.shape, k
+            assert np.array_equal(got, v), (step, k, float(np.abs(got - v).max()))
+    assert not np.array_equal(single[0]["z_vals_coarse"], single[1]["z_vals_coarse"])

@@ -20,3 +20,17 @@ def test_training_psnr_matches_cpu_reference(precision):
     assert r["targets"] == "real JAX_269 RGB"
     assert r["loss_first_last"][-1][0] < r["loss_first_last"][0][0]  # it trains
     assert abs(r["delta_db"]) <= 0.05, r
+
+
+def test_long_horizon_bf16_psnr_matches_fp32_hip():
+    """bench.psnr_long at a test-sized horizon (the default bench line runs 2000 steps of 1024
+    rays): the bf16 MLP and the reference-pinned fp32 HIP path trained side by side with the C3
+    flags on the real JAX_269 targets, same init / batches / on-device draws."""
+    import bench
+    r = bench.psnr_long(steps=300, batch=256, n_eval=2048)
+    print({k: v for k, v in r.items() if k != "loss_curve"})
+    assert r["targets"] == "real JAX_269 RGB"
+    for prec in ("fp32", "bf16"):
+        curve = r["loss_curve"][prec]
+        assert curve[-1][1] < curve[0][1]   # both train
+    assert abs(r["delta_db"]) <= 0.05, r
