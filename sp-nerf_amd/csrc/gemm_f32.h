@@ -23,7 +23,11 @@ struct NTArgs {
     const float* Dmul = nullptr; int ld_dmul = 0;
     // bf16 outputs instead of C / Dout (sine epilogue only: layer 0 of the bf16 MLP), same ld
     bf16* C16 = nullptr; bf16* D16 = nullptr;
+    // precision study (option "emu_bf16", fp32 MLP only): 1 = outputs of forward layers (C, Dout)
+    // rounded to bf16, 2 = the backward dX outputs (Dmul instances) rounded to bf16
+    int emu = 0;
 };
+extern int g_emu_bf16;  // option "emu_bf16": bits 1 / 2 as NTArgs::emu, 4 = GEMM weights packed bf16-rounded
 
 // slab[s][n][k] = Σ_{p in split s} A[p][n] · B[p][k]  (B split along K at K1 like NTArgs.A);
 // slab_b[s][n] = Σ_{p in split s} A[p][n]  (bias gradient), if slab_b != nullptr.

@@ -542,6 +542,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
                         for (int e = 0; e < 8; ++e) v[e] *= dm[q4][e >> 2][e & 3];
                     }
+                    if (g.emu && (g.Dmul ? (g.emu & 2) : (g.emu & 1))) {  // precision study: bf16 rounding
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            v[e] = (float)(bf16)v[e];
+                            d[e] = (float)(bf16)d[e];
+                        }
+                    }
                     if (row < g.M && colok) {
                         if (out16) {
                             *reinterpret_cast<u32x4*>(g.C16 + (int64_t)row * g.ldc + col) = pack8(v);
@@ -908,7 +915,11 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __res
 // around the MFMA groups measured 0.5% slower.
 int g_nt_variant = 8;
 
-int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant) {
+int g_emu_bf16 = 0;
+
+int32_t gemm_nt(const NTArgs& a0, hipStream_t s, int variant) {
+    NTArgs a = a0;
+    a.emu = (a.C16 || g_nt_variant != 8) ? 0 : (g_emu_bf16 & 3);   // the study covers the default kernel
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
     SPN_ARG(a.K % BK == 0 && a.K1 % BK == 0 && a.K1 <= a.K, "gemm_nt: K=%d/K1=%d must be multiples of %d", a.K, a.K1, BK);
     SPN_ARG(a.K1 == a.K || a.A2 != nullptr, "gemm_nt: second A segment missing");

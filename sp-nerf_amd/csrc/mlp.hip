@@ -38,6 +38,7 @@ struct PackPiece {
     int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;
     int64_t dst;
     int nsrc = 0;  // bf = 6: source rows
+    int rnd = 0;   // fp32 destination rounded to bf16 (precision study, option emu_bf16 & 4)
 };
 constexpr int kMaxPieces = 64;
 constexpr int kPackTR = 32, kPackTC = 64;  // a block re-lays one 32 x 64 tile of a piece
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             if (r < pc.rows && c < pc.cols) {
                 const int64_t o = pc.dst + (pc.bf == 2 ? trunk_frag_off(c, r, pc.dst_ld) : (int64_t)c * pc.dst_ld + r);
                 if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)tileT[cc][rr];
-                else a.packed[o] = tileT[cc][rr];
+                else a.packed[o] = pc.rnd ? (float)(bf16)tileT[cc][rr] : tileT[cc][rr];
             }
         }
         return;
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
                                     : pc.transpose ? (int64_t)c * pc.dst_ld + r
                                                    : (int64_t)r * pc.dst_ld + c);
         if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)v;
-        else a.packed[o] = v;
+        else a.packed[o] = pc.rnd ? (float)(bf16)v : v;
     }
 }
 
@@ -525,6 +526,7 @@ struct HeadsBwdArgs {
     float* hpre;
     T *dZQ, *dZG, *dS3;
     int64_t P; int mode;
+    int emu = 0;  // precision study (fp32 only): the dX outputs rounded to bf16
 };
 
 // Backward of the narrow heads, one wavefront per point: per-point pre-activation gradients
@@ -675,20 +677,25 @@ __global__ __launch_bounds__(256) void k_heads_bwd_v(HeadsBwdArgs<T> a, PackedOf
             a.hpre[p * d.HP + lane] = v;
         }
         if (!sun_on) return;
+        auto st = [&](T* q, f32x4 v) {
+            if (a.emu)
+                for (int e = 0; e < 4; ++e) v[e] = (float)(bf16)v[e];
+            st4(q, v);
+        };
 #pragma unroll
         for (int i = 0; i < NH; ++i)
-            if (vh[i]) st4(a.dS3 + p * H + ch[i], (dys * w4[i]) * raw_f32(cur.s3[i]));
+            if (vh[i]) st(a.dS3 + p * H + ch[i], (dys * w4[i]) * raw_f32(cur.s3[i]));
         if (!full) return;
 #pragma unroll
         for (int i = 0; i < NH; ++i) {
             if (!vh[i]) continue;
-            st4(a.dZQ + p * d.NQ + H + ch[i], (dy[0] * wr[0][i] + dy[1] * wr[1][i] + dy[2] * wr[2][i]) * raw_f32(cur.qr[i]));
-            if (d.beta) st4(a.dZQ + p * d.NQ + 2 * H + ch[i], (db * wb[i]) * raw_f32(cur.qb[i]));
+            st(a.dZQ + p * d.NQ + H + ch[i], (dy[0] * wr[0][i] + dy[1] * wr[1][i] + dy[2] * wr[2][i]) * raw_f32(cur.qr[i]));
+            if (d.beta) st(a.dZQ + p * d.NQ + 2 * H + ch[i], (db * wb[i]) * raw_f32(cur.qb[i]));
             if (d.sem) {
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
                 for (int j = 0; j < d.C; ++j)
                     acc += col(cur.g, d.sem_col + j) * *reinterpret_cast<const f32x4*>(wsem + j * H + ch[i]);
-                st4(a.dZG + p * d.NG + d.W + ch[i], acc * raw_f32(cur.gm[i]));
+                st(a.dZG + p * d.NG + d.W + ch[i], acc * raw_f32(cur.gm[i]));
             }
         }
     };
@@ -871,31 +878,46 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
         return SPNERF_OK;
     };
     const int W = d.W, H = d.H;
+    // precision study: the fp32 MLP's GEMM weights rounded to bf16 (as the bf16 MLP packs them)
+    const bool rnd16 = !d.bf && (g_emu_bf16 & 4);
+    auto mark = [&]() { v.back().rnd = rnd16 ? 1 : 0; };
     for (int i = 0; i < d.L; ++i) {
         const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
         SPN_TRY(piece(x.fcW[i], 0, W, kreal, k.Wt[i], k.Kp[i], 0));
+        if (i > 0) mark();
         SPN_TRY(piece(x.fcb[i], 0, 1, W, k.bt[i], W, 0));
-        if (i > 0) SPN_TRY(piece(x.fcW[i], 0, W, W, k.WTt[i], W, 1));
+        if (i > 0) {
+            SPN_TRY(piece(x.fcW[i], 0, W, W, k.WTt[i], W, 1));
+            mark();
+        }
     }
     if (d.sem) {
         SPN_TRY(piece(x.fcW[0], d.K0, W, d.sd, k.Wsem0, d.sd, 0));
         SPN_TRY(piece(x.fcW[d.skip], W + d.K0, W, d.sd, k.Wsem4, d.sd, 0));
         SPN_TRY(piece(x.emb, 0, d.C + 1, d.sd, k.emb, d.sd, 0));
         SPN_TRY(piece(x.m1W, 0, H, W, k.WG + (int64_t)W * W, W, 0));
+        mark();
         SPN_TRY(piece(x.m1b, 0, 1, H, k.bG + W, H, 0));
         SPN_TRY(piece(x.m1W, 0, H, W, k.WGT + W, d.NG, 1));
+        mark();
         SPN_TRY(piece(x.m2W, 0, d.C, H, k.Wm2, H, 0));
         SPN_TRY(piece(x.m2b, 0, 1, d.C, k.bm2, d.C, 0));
     }
     SPN_TRY(piece(x.featW, 0, W, W, k.WG, W, 0));
+    mark();
     SPN_TRY(piece(x.featb, 0, 1, W, k.bG, W, 0));
     SPN_TRY(piece(x.featW, 0, W, W, k.WGT, d.NG, 1));
+    mark();
     SPN_TRY(piece(x.s1W, 0, H, W, k.WQ, W, 0));
+    mark();
     SPN_TRY(piece(x.r1W, 0, H, W, k.WQ + (int64_t)H * W, W, 0));
+    mark();
     SPN_TRY(piece(x.s1b, 0, 1, H, k.bQ, H, 0));
     SPN_TRY(piece(x.r1b, 0, 1, H, k.bQ + H, H, 0));
     SPN_TRY(piece(x.s1W, 0, H, W, k.WQT, d.NQ, 1));
+    mark();
     SPN_TRY(piece(x.r1W, 0, H, W, k.WQT + H, d.NQ, 1));
+    mark();
     SPN_TRY(piece(x.s1W, W, H, 3, k.Wsun, 3, 0));
     if (d.beta) {
         SPN_TRY(piece(x.b1W, 0, H, W, k.WQ + (int64_t)2 * H * W, W, 0));
@@ -906,11 +928,15 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
         SPN_TRY(piece(x.b2b, 0, 1, 1, k.bb2, 1, 0));
     }
     SPN_TRY(piece(x.s2W, 0, H, H, k.Ws2, H, 0));
+    mark();
     SPN_TRY(piece(x.s2b, 0, 1, H, k.bs2, H, 0));
     SPN_TRY(piece(x.s2W, 0, H, H, k.Ws2T, H, 1));
+    mark();
     SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3, H, 0));
+    mark();
     SPN_TRY(piece(x.s3b, 0, 1, H, k.bs3, H, 0));
     SPN_TRY(piece(x.s3W, 0, H, H, k.Ws3T, H, 1));
+    mark();
     SPN_TRY(piece(x.sigW, 0, 1, W, k.wsig, W, 0));
     SPN_TRY(piece(x.sigb, 0, 1, 1, k.bsig, 1, 0));
     SPN_TRY(piece(x.r2W, 0, 3, H, k.Wr2, H, 0));
@@ -1411,7 +1437,7 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     // 1. narrow heads
     {
         HeadsBwdArgs<T> a{packed, d, d_out, c.at(c.w.hsave), buf(c.w.DQ), buf(c.w.DG), buf(c.w.DS3), hpre, dZQ, dZG, dS3,
-                          P, mode};
+                          P, mode, (!BF && (g_emu_bf16 & 2)) ? 1 : 0};
         const double eb = BF ? 2.0 : 4.0;
         ProfScope prof("heads_bwd", s, 2.0 * P * 4 * H, 4.0 * P * (d.NO + d.HP) + eb * P * 6 * H);
         const unsigned grid = (unsigned)std::min<int64_t>(cdiv(P, 4), 8192);
@@ -1656,6 +1682,7 @@ static int* option_slot(const char* name) {
     if (n == "fused_bwd") return &g_fused_bwd;
     if (n == "trunk2") return &g_trunk2;
     if (n == "trunk2_tile") return &g_trunk2_tile;
+    if (n == "emu_bf16") return &g_emu_bf16;
     return nullptr;
 }
 
