@@ -252,65 +252,124 @@ def psnr_parity(steps: int = 30, batch: int = 128, n_eval: int = 1024, seed: int
                      "JAX_269 cameras at img_downscale 4 (JAX_214 absent); CPU side = oracle/ref_cpu.py (fp32)"}
 
 
-def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: int = 3, dev="cuda:0"):
-    """Long-horizon training parity (BASELINE.json "PSNR vs ref", north star |Δ| <= 0.05 dB):
-    the bf16 MLP (configs 3-5) against the fp32 HIP path — itself pinned to the reference at
-    1e-4 per step (tests/test_gpu_parity.py) — trained side by side for ``steps`` steps with the
-    C3 flags (64 + 64 guided samples, solar pass, depth + semantic heads, W=512; the trainer's
-    loss sum and Adam lr 5e-4, main.py:97,125-186) on the JAX_269 cameras at img_downscale 4
-    against the REAL JAX_269 images, from the same init, on the same batches, with the same
-    on-device draws (PhiloxRandom, same seed); then both render the same held-out rays."""
+def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: int = 3, dev="cuda:0",
+              checkpoints: int = 10):
+    """Long-horizon training parity (BASELINE.json "PSNR vs ref", north star |Δ| <= 0.05 dB) of
+    the bf16 MLP (configs 3-5) against the fp32 HIP path — itself pinned to the reference at 1e-4
+    per step (tests/test_gpu_parity.py) — with the C3 flags (64 + 64 guided samples, solar pass,
+    depth + semantic heads, W=512; the trainer's loss sum and Adam lr 5e-4, main.py:97,125-186) on
+    the JAX_269 cameras at img_downscale 4 against the REAL JAX_269 images.
+
+    Three arms train side by side from the same init on the same batches and on-device draws:
+    ``fp32``, ``bf16`` and ``fp32_control`` — fp32 again from the init scaled by (1 + 1e-6·N(0,1)):
+    the distance between two trajectories of the SAME arithmetic, i.e. the floor below which a
+    trained-PSNR difference says nothing about precision (Adam turns rounding-level gradient
+    differences into lr-sized steps and SIREN training at lr 5e-4 has loss spikes: measured
+    replicas differ by up to ~1 dB after 1 000 steps).  Reported beside the final
+    PSNRs (and their means over the second half of the held-out checkpoints):
+      * ``bf16_inference_at_fp32_trained``: the fp32 arm's final weights rendered by the bf16 MLP —
+        the precision effect on PSNR at a trained state, free of trajectory noise;
+      * ``grad_rel_err``: at each checkpoint the bf16 MLP's gradient at the fp32 arm's current
+        weights on its batch and draws, norm-relative to the fp32 gradient — the bf16 gradients
+        stay as close along the whole run as at init."""
     import numpy as np
     from spnerf_amd import PhiloxRandom, random_source
 
     c = CONFIGS["c3"]
     args = make_args(c)
-    scene = synthetic_scene(4.0, seed=0, device=dev)
-    R = scene
+    R = synthetic_scene(4.0, seed=0, device=dev)
     rng = np.random.default_rng(seed)
     perm = rng.permutation(R.rays.shape[0])
     held, pool = torch.as_tensor(perm[:n_eval], device=dev), perm[n_eval:]
-    models, opts, srcs, curves = {}, {}, {}, {}
-    for prec in ("fp32", "bf16"):
+    arms = ("fp32", "bf16", "fp32_control")
+
+    def new_model(prec):
         torch.manual_seed(seed)
-        models[prec] = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True,
-                                         sem=True, precision=prec).to(dev).use_flat_grads()
-        opts[prec] = spnerf_amd.optim.Adam(list(models[prec].parameters()), lr=5e-4)
-        srcs[prec] = PhiloxRandom(seed=seed)
-        curves[prec] = []
+        return spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=True,
+                                 precision=prec).to(dev).use_flat_grads()
+
+    models = {a: new_model("bf16" if a == "bf16" else "fp32") for a in arms}
+    g = torch.Generator(device="cpu").manual_seed(99)
+    with torch.no_grad():
+        for p in models["fp32_control"].parameters():
+            p.mul_(1 + 1e-6 * torch.randn(p.shape, generator=g).to(dev))
+    probe = new_model("bf16")
+    opts = {a: spnerf_amd.optim.Adam(list(models[a].parameters()), lr=5e-4) for a in arms}
+    srcs = {a: PhiloxRandom(seed=seed) for a in arms}
     floss = FusedRenderLoss(c["sc_lambda"], 1.0, 1.0)
-    t0 = time.perf_counter()
-    for step in range(steps):
-        idx = torch.as_tensor(rng.choice(pool, batch, replace=False), device=dev)
-        for prec in ("fp32", "bf16"):
-            m = models[prec]
-            opts[prec].zero_grad(set_to_none=True)
-            with random_source(srcs[prec]):
-                res = spnerf_amd.render_rays({"coarse": m}, args, R.rays[idx], None, semantics=R.sems[idx], mode="train",
-                                             valid_depth=R.valid_depth[idx], target_depths=R.depths[idx],
-                                             target_std=R.depth_std[idx])
-            loss, _ = floss(res, R.rgbs[idx], R.depths[idx], R.valid_depth[idx], R.depth_std[idx], R.sems[idx])
-            loss.backward()
-            opts[prec].step()
-            if step % max(1, steps // 20) == 0 or step == steps - 1:
-                curves[prec].append((step, float(loss.detach())))
-    train_s = time.perf_counter() - t0
-    psnr = {}
-    for prec in ("fp32", "bf16"):
+
+    def train_loss(m, idx):
+        res = spnerf_amd.render_rays({"coarse": m}, args, R.rays[idx], None, semantics=R.sems[idx], mode="train",
+                                     valid_depth=R.valid_depth[idx], target_depths=R.depths[idx],
+                                     target_std=R.depth_std[idx])
+        return floss(res, R.rgbs[idx], R.depths[idx], R.valid_depth[idx], R.depth_std[idx], R.sems[idx])[0]
+
+    def held_psnr(m):
         rgb = []
         with torch.no_grad(), random_source(PhiloxRandom(seed=seed + 1)):
             for i0 in range(0, n_eval, 2048):
                 ii = held[i0:i0 + 2048]
-                rgb.append(spnerf_amd.render_rays({"coarse": models[prec]}, args, R.rays[ii], None, semantics=R.sems[ii],
+                rgb.append(spnerf_amd.render_rays({"coarse": m}, args, R.rays[ii], None, semantics=R.sems[ii],
                                                   mode="test")["rgb_coarse"])
-        mse = float(torch.mean((torch.cat(rgb) - R.rgbs[held]) ** 2))
-        psnr[prec] = float(-10.0 * np.log10(mse))
-    return {"psnr_bf16_db": psnr["bf16"], "psnr_fp32_hip_db": psnr["fp32"], "delta_db": psnr["bf16"] - psnr["fp32"],
+        return float(-10.0 * np.log10(float(torch.mean((torch.cat(rgb) - R.rgbs[held]) ** 2))))
+
+    every = max(1, steps // checkpoints)
+    curves = {a: [] for a in arms}
+    loss_curve = {a: [] for a in arms}
+    grad_err = []
+    t0 = time.perf_counter()
+    for step in range(steps):
+        idx = torch.as_tensor(rng.choice(pool, batch, replace=False), device=dev)
+        check = step % every == 0 or step == steps - 1
+        if check:   # the bf16 gradient at the fp32 arm's weights, same batch, same draws
+            with torch.no_grad():
+                for q, p in zip(probe.parameters(), models["fp32"].parameters()):
+                    q.copy_(p)
+            psrc = PhiloxRandom(seed=seed)
+            if srcs["fp32"]._state is not None:
+                psrc._state = srcs["fp32"]._state.clone()
+            for q in probe.parameters():
+                q.grad = None
+            with random_source(psrc):
+                train_loss(probe, idx).backward()
+            g16 = probe._flat_grad.clone()
+        for a in arms:
+            m = models[a]
+            opts[a].zero_grad(set_to_none=True)
+            with random_source(srcs[a]):
+                loss = train_loss(m, idx)
+            loss.backward()
+            if check and a == "fp32":
+                g32 = m._flat_grad
+                grad_err.append((step, float(torch.linalg.norm(g16 - g32) / torch.linalg.norm(g32))))
+            opts[a].step()
+            if check:
+                loss_curve[a].append((step, float(loss.detach())))
+        if check and step > 0:
+            for a in arms:
+                curves[a].append((step + 1, held_psnr(models[a])))
+    train_s = time.perf_counter() - t0
+    final = {a: curves[a][-1][1] for a in arms}
+    half = [k for k in range(len(curves["fp32"])) if curves["fp32"][k][0] > steps // 2]
+    tail = {a: float(np.mean([curves[a][k][1] for k in half])) for a in arms}
+    with torch.no_grad():
+        for q, p in zip(probe.parameters(), models["fp32"].parameters()):
+            q.copy_(p)
+    p16 = held_psnr(probe)
+    return {"psnr_bf16_db": final["bf16"], "psnr_fp32_hip_db": final["fp32"],
+            "delta_db": final["bf16"] - final["fp32"],
+            "control_delta_db": final["fp32_control"] - final["fp32"],
+            "tail_mean_delta_db": tail["bf16"] - tail["fp32"],
+            "tail_mean_control_delta_db": tail["fp32_control"] - tail["fp32"],
+            "bf16_inference_at_fp32_trained": {"psnr_db": p16, "delta_db": p16 - final["fp32"]},
+            "grad_rel_err": grad_err, "max_grad_rel_err": max(e for _, e in grad_err),
+            "psnr_curve": curves, "loss_curve": loss_curve,
             "steps": steps, "batch_rays": batch, "held_out_rays": n_eval, "train_seconds": train_s,
-            "loss_curve": curves, "targets": scene.rgb_source,
+            "targets": R.rgb_source,
             "setup": "C3 flags (64+64 guided, solar pass, depth + semantic heads, W=512) at img_downscale 4 on the "
                      "JAX_269 cameras (JAX_214 absent), trainer's loss sum, Adam lr 5e-4, same init / batches / "
-                     "on-device Philox draws for both; the fp32 HIP path is the reference-pinned one (1e-4 per step)"}
+                     "on-device Philox draws for every arm; fp32_control = fp32 from the init x (1 + 1e-6 N(0,1)); the "
+                     "fp32 HIP path is the reference-pinned one (1e-4 per step)"}
 
 
 def ref_cpu_replay(draws):
@@ -576,6 +635,8 @@ def parse_args(argv=None):
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="library kernel switch (spnerf_set_option), e.g. fused_trunk=0, nt_f32_variant=4")
     ap.add_argument("--global-batch", type=int, default=0, help="override the config's global batch (rays per step)")
+    ap.add_argument("--flat-allreduce", action="store_true",
+                    help="one all-reduce of the flat gradient after the backward instead of overlapped buckets")
     ap.add_argument("--share-device", action="store_true",
                     help="(rehearsal on a 1-GPU box) every rank on cuda:0 over gloo instead of RCCL")
     return ap.parse_args(argv)
@@ -684,20 +745,34 @@ def run_train(a, config, rank, world, dev, secondary=False):
         loss.backward()
         return loss.detach()   # no autograd graph outlives the step (captured nodes would pin their stream)
 
-    # all-reduce time per timed step, from HIP events on the current stream around the call (the
-    # collective's completion is ordered before the end event); summed after the timed region
+    # The gradient all-reduce (N > 1): by default in buckets (dp.GradBuckets), each issued on a
+    # communication stream behind the backward mark after which its gradients are final, so the
+    # collectives overlap the rest of the backward; --flat-allreduce = one all-reduce after it.
+    # allreduce_ms_per_step = the EXPOSED part: HIP events on the compute stream from the end of
+    # the backward to the moment every bucket has landed
+    buckets = dp.GradBuckets(model, world) if (world > 1 and not a.flat_allreduce) else None
+    if buckets is not None:
+        buckets.arm(True)
     ar_events = []
     ar_timing = [False]
+
+    def reduce_grads():
+        if buckets is not None:
+            flat = model._flat_grad
+            buckets.launch(flat)
+            buckets.finish(flat)
+        else:
+            dp.allreduce_grads(params, world)   # one RCCL all-reduce of the flat gradient
 
     def finish():
         if world > 1 and ar_timing[0]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            dp.allreduce_grads(params, world)   # one RCCL all-reduce of the flat gradient (N > 1)
+            reduce_grads()
             e1.record()
             ar_events.append((e0, e1))
         else:
-            dp.allreduce_grads(params, world)
+            reduce_grads()
         opt.step()
         args.noise_std *= 0.9               # main.py:155
 
@@ -802,6 +877,9 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "roofline": roofline_of(dom, nt, traffic, traffic_src),
         "mlp_mfma_utilisation": gemm_totals(prof_steps),
         "allreduce_ms_per_step": allreduce_ms,
+        "allreduce": (None if world == 1 else
+                      f"{len(buckets.buckets)} buckets issued behind the backward's gradient marks (exposed ms above)"
+                      if buckets is not None else "one flat all-reduce after the backward"),
         "kernels": kernels,
         "final_loss": final_loss,
         "execution": ("hip graph of render+loss+backward per step, eager all-reduce + fused Adam; kernel timings "
@@ -811,6 +889,8 @@ def run_train(a, config, rank, world, dev, secondary=False):
     }
     del graph
     set_random_source(None)
+    if buckets is not None:
+        buckets.arm(False)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not secondary:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or min(B, 512))
         if config in ("c2", "c4"):

@@ -220,6 +220,21 @@ int32_t spnerf_adam_step(int32_t n, void* const* params, const void* const* grad
                          void* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2,
                          double eps, int32_t step, void* stream);
 
+/* ---- gradient readiness marks for data parallelism (no reference counterpart: the reference
+ *      trains on one GPU, main.py:322-337).  A backward passes n_marks = layers + 2 points after
+ *      which groups of parameter gradients are final: mark 0 after the output heads', mark
+ *      1 + (layers-1-i) after trunk layer i's, mark layers+1 at its end (per-ray parameters).
+ *      spnerf_grad_marks fills mark_of_param[idx] (canonical order) with the mark after which
+ *      parameter idx receives no more writes from a main or a solar-pass backward and returns
+ *      n_marks.  While armed, every spnerf_mlp_backward records the library's mark events (one
+ *      set per device) on its stream — as external event nodes when the stream is being captured
+ *      into a HIP graph, so each replay records them — and spnerf_grad_mark_wait makes `stream`
+ *      wait for the latest record of `mark`: an all-reduce issued behind it overlaps the rest of
+ *      the backward. */
+int32_t spnerf_grad_marks(const spnerf_model_cfg* cfg, int32_t* mark_of_param, int32_t n_params);
+int32_t spnerf_grad_marks_arm(int32_t on);
+int32_t spnerf_grad_mark_wait(int32_t mark, void* stream);
+
 /* ---- in-library kernel timing (HIP events on the launch stream) ------------------------- */
 int32_t spnerf_prof_enable(int32_t on);
 int32_t spnerf_prof_reset(void);

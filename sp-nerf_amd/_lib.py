@@ -92,6 +92,9 @@ SIGNATURES = {
     "spnerf_prof_reset": (c_int32, []),
     "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
     "spnerf_prof_classes": (c_int32, [c_char_p, c_int32]),
+    "spnerf_grad_marks": (c_int32, [POINTER(ModelCfg), POINTER(c_int32), c_int32]),
+    "spnerf_grad_marks_arm": (c_int32, [c_int32]),
+    "spnerf_grad_mark_wait": (c_int32, [c_int32, c_void_p]),
 }
 
 _lib = None
@@ -163,6 +166,24 @@ def prof_classes() -> list:
     buf = ctypes.create_string_buffer(8192)
     check(lib().spnerf_prof_classes(buf, len(buf)), "prof_classes")
     return [c for c in buf.value.decode().split(",") if c]
+
+
+def grad_marks(cfg: ModelCfg, n_params: int):
+    """(mark of each parameter, number of marks): spnerf_grad_marks"""
+    arr = (c_int32 * n_params)()
+    n = lib().spnerf_grad_marks(ctypes.byref(cfg), arr, n_params)
+    if n < 0:
+        check(n, "grad_marks")
+    return list(arr), n
+
+
+def grad_marks_arm(on: bool) -> None:
+    check(lib().spnerf_grad_marks_arm(1 if on else 0), "grad_marks_arm")
+
+
+def grad_mark_wait(mark: int, stream) -> None:
+    """``stream`` (a torch.cuda.Stream) waits for the latest record of gradient mark ``mark``."""
+    check(lib().spnerf_grad_mark_wait(int(mark), c_void_p(stream.cuda_stream)), "grad_mark_wait")
 
 
 def prof_read(kernel_class: str) -> dict:

@@ -73,5 +73,12 @@ int32_t tn_skinny(const SkinnyArgs& a, hipStream_t s);
 extern int g_tn_variant;  // 0 = one LDS stage, 1 = double-buffered
 int32_t gemm_tn(const TNArgs& a, int splits, hipStream_t s, int variant = -1);
 int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s);
+constexpr int kReduceMulti = 4;
+struct ReduceMulti {
+    ReduceArgs seg[kReduceMulti];
+    int n = 0;
+};
+// up to kReduceMulti reductions (empty ones skipped) in one launch; bit-identical to one each
+int32_t reduce_slabs_multi(const ReduceArgs* a, int n, hipStream_t s);
 
 }  // namespace spn

@@ -744,11 +744,9 @@ __global__ __launch_bounds__(256) void k_gemm_tn(TNArgs g) {
 // dst[r][c] (+)= Σ_s slab[s][row0+r][c] for c < ncols; dst_b[r] = Σ_s slab_b[s][row0+r];
 // with `transpose`, dst[c][r] instead.  256 threads = 64 columns x 4 split phases, the four
 // phase partials combined in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void k_reduce_slabs(ReduceArgs g) {
+__device__ __forceinline__ void reduce_slab_row(const ReduceArgs& g, const int r, f32x4 (*part)[64]) {
     // a block: one row, 256 columns (float4 quads), the splits in 4 phases (waves); per column
     // the phases add their splits in order and combine as (p0 + p1) + (p2 + p3)
-    __shared__ f32x4 part[4][64];
-    const int r = blockIdx.y;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int c = (blockIdx.x * 64 + tx) * 4;  // first column of this thread's quad
     const int n = g.row0 + r;
@@ -797,6 +795,21 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(ReduceArgs g) {
             }
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_reduce_slabs(ReduceArgs g) {
+    __shared__ f32x4 part[4][64];
+    reduce_slab_row(g, blockIdx.y, part);
+}
+
+// several reductions in one launch (the outputs of one weight-gradient GEMM: rows of the
+// concatenated heads, the skinny reductions' product and column-sum rows): grid.y runs over the
+// segments' rows in order
+__global__ __launch_bounds__(256) void k_reduce_slabs_multi(ReduceMulti m) {
+    __shared__ f32x4 part[4][64];
+    int r = blockIdx.y, i = 0;
+    while (i + 1 < m.n && r >= m.seg[i].nrows) r -= m.seg[i++].nrows;
+    reduce_slab_row(m.seg[i], r, part);
 }
 
 // Skinny weight gradient: slab[chunk][m][k] = Σ_{p in chunk} a_m(p) · B[p][k] for m < Ma
@@ -1008,6 +1021,27 @@ int32_t gemm_tn(const TNArgs& a0, int splits, hipStream_t s, int variant) {
     if (v == 2) hipLaunchKernelGGL(k_gemm_tn<3>, dim3(nb * splits), dim3(256), 0, s, a);
     else if (v == 1) hipLaunchKernelGGL(k_gemm_tn<2>, dim3(nb * splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_gemm_tn<1>, dim3(nb * splits), dim3(256), 0, s, a);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+int32_t reduce_slabs_multi(const ReduceArgs* a, int n, hipStream_t s) {
+    ReduceMulti m;
+    m.n = 0;
+    int rows = 0, cols = 0;
+    double bytes = 0.0;
+    for (int i = 0; i < n; ++i) {
+        if (a[i].nrows <= 0) continue;
+        SPN_ARG(m.n < kReduceMulti, "reduce_slabs_multi: too many segments");
+        m.seg[m.n++] = a[i];
+        rows += a[i].nrows;
+        cols = std::max(cols, a[i].ncols + 1);
+        bytes += 4.0 * (double)a[i].nrows * (a[i].ncols + 1) * (a[i].splits + (a[i].accumulate ? 2.0 : 1.0));
+    }
+    if (m.n == 0) return SPNERF_OK;
+    if (m.n == 1) return reduce_slabs(m.seg[0], s);
+    ProfScope prof("reduce_slabs", s, 0.0, bytes);
+    hipLaunchKernelGGL(k_reduce_slabs_multi, dim3(cdiv(cols, 256), rows), dim3(256), 0, s, m);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -326,6 +326,41 @@ Side* side_stream() {
 }
 
 // `to` waits for everything issued so far on `from`
+// Gradient readiness marks (spnerf_grad_marks): when armed, a backward records mark k's event
+// on the stream that finishes that group of weight gradients — mark 0 after the output heads',
+// 1 + (L-1-i) after trunk layer i's, L+1 at the end (per-ray parameters) — so that a data-parallel
+// caller can all-reduce each group while the rest of the backward runs.  One event set per device;
+// a stream being captured into a HIP graph gets external event-record nodes (a replay records them).
+struct Marks {
+    hipEvent_t ev[64] = {};
+    bool ok = false;
+};
+Marks g_marks[64];
+int g_marks_armed = 0;
+
+static Marks* marks_of_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    Marks& m = g_marks[dev];
+    if (!m.ok) {
+        for (auto& e : m.ev)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        m.ok = true;
+    }
+    return &m;
+}
+
+static int32_t grad_mark(int k, hipStream_t s) {
+    if (!g_marks_armed) return SPNERF_OK;
+    Marks* m = marks_of_device();
+    SPN_ARG(m && k >= 0 && k < 64, "grad_mark: no mark events");
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    SPN_HIP(hipStreamIsCapturing(s, &st));
+    if (st == hipStreamCaptureStatusActive) SPN_HIP(hipEventRecordWithFlags(m->ev[k], s, hipEventRecordExternal));
+    else SPN_HIP(hipEventRecord(m->ev[k], s));
+    return SPNERF_OK;
+}
+
 int32_t stream_dep(Side* sd, hipStream_t from, hipStream_t to) {
     if (!sd || from == to) return SPNERF_OK;
     hipEvent_t e = sd->ev[sd->next];
@@ -1081,12 +1116,15 @@ static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int
     t.slab_b = c.at(c.w.slab_b);
     t.P = P; t.N = N; t.K = K;
     SPN_TRY(G::tn(t, splits, s));
+    std::vector<ReduceArgs> rs;
     for (ReduceArgs r : outs) {
         r.slab = t.slab; r.ld_slab = K; r.slab_stride = t.slab_stride; r.splits = splits; r.N = N;
         r.slab_b = t.slab_b;
         r.accumulate = c.acc;
-        SPN_TRY(reduce_slabs(r, s));
+        rs.push_back(r);
     }
+    for (size_t i = 0; i < rs.size(); i += kReduceMulti)
+        SPN_TRY(reduce_slabs_multi(rs.data() + i, (int)std::min<size_t>(kReduceMulti, rs.size() - i), s));
     return SPNERF_OK;
 }
 
@@ -1113,13 +1151,15 @@ static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int M
     r.slab = k.slab; r.ld_slab = K; r.slab_stride = (int64_t)Mt * K; r.splits = chunks; r.N = Mt; r.slab_b = k.slab_b;
     r.transpose = transpose;
     r.accumulate = c.acc;
-    if (dst) SPN_TRY(reduce_slabs(r, s));
+    ReduceArgs rr[2];
+    int n = 0;
+    if (dst) rr[n++] = r;
     if (dst_ones) {
         ReduceArgs o = r;
         o.row0 = Ma; o.nrows = 1; o.dst = dst_ones; o.ld_dst = K; o.dst_b = nullptr; o.transpose = 0;
-        SPN_TRY(reduce_slabs(o, s));
+        rr[n++] = o;
     }
-    return SPNERF_OK;
+    return reduce_slabs_multi(rr, n, s);
 }
 
 // Trunk + G/Q/sun_v GEMMs of the forward (spnerf.py:323-355).  In the bf16 MLP, layer 0 stays
@@ -1508,6 +1548,7 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
                                {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
         else
             SPN_TRY(tn_grad<T>(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s2, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
+        SPN_TRY(grad_mark(0, s2));   // every output head's gradient is final (spnerf_grad_marks)
         NT g;
         g.A = dZG; g.lda = d.NG; g.K1 = NG; g.B = G::w(c, c.k.WGT, c.k.WGT16); g.ldb = d.NG; g.C = dZ; g.ldc = W;
         g.M = (int)P; g.N = W; g.K = NG;
@@ -1535,7 +1576,7 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
         if (d.sem && (i == 0 || i == d.skip))
             SPN_TRY(ray_rowsum<T>(dZi, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
-        return SPNERF_OK;
+        return grad_mark(1 + (d.L - 1 - i), s2);
     };
     if (BF && !zs && g_fused_bwd && !c.k.Wb16.empty() && c.k.Wb16[1] >= 0) {
         // the whole dX chain in one launch (k_trunk_bwd_bf16): dZ_{i-1} overwrites D_{i-1} in
@@ -1645,7 +1686,7 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
         }
     }
     SPN_TRY(stream_dep(sd, s2, s_main));  // join: the caller's stream sees every gradient
-    return SPNERF_OK;
+    return grad_mark(d.L + 1, s_main);
 }
 
 }  // namespace spn
@@ -1699,6 +1740,40 @@ extern "C" int32_t spnerf_get_option(const char* name, int32_t* value) {
     int* slot = option_slot(name);
     SPN_ARG(slot != nullptr, "get_option: unknown option '%s'", name);
     *value = *slot;
+    return SPNERF_OK;
+}
+
+extern "C" int32_t spnerf_grad_marks(const spnerf_model_cfg* cfg, int32_t* mark_of_param, int32_t n_params) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    PIdx x;
+    auto specs = param_specs(d, &x);
+    SPN_ARG(mark_of_param && n_params == (int32_t)specs.size(), "spnerf_grad_marks: need one slot per parameter");
+    SPN_ARG(d.L + 2 <= 64, "spnerf_grad_marks: too many layers");
+    const int end = d.L + 1;
+    for (size_t i = 0; i < specs.size(); ++i) mark_of_param[i] = 0;  // output heads (mark 0)
+    for (int i = 0; i < d.L; ++i) {
+        const int m = 1 + (d.L - 1 - i);
+        mark_of_param[x.fcb[i]] = m;
+        // the semantic columns of layer 0 / the skip layer come from per-ray sums at the end
+        mark_of_param[x.fcW[i]] = (d.sem && (i == 0 || i == d.skip)) ? end : m;
+    }
+    // per-ray parameters and columns (step 7 of the backward)
+    for (int pi : {x.emb, x.s1W, x.k1W, x.k1b, x.k2W, x.k2b, x.b1W})
+        if (pi >= 0) mark_of_param[pi] = end;
+    return d.L + 2;
+}
+
+extern "C" int32_t spnerf_grad_marks_arm(int32_t on) {
+    if (on) SPN_ARG(marks_of_device() != nullptr, "spnerf_grad_marks_arm: cannot create the mark events");
+    g_marks_armed = on ? 1 : 0;
+    return SPNERF_OK;
+}
+
+extern "C" int32_t spnerf_grad_mark_wait(int32_t mark, void* stream) {
+    Marks* m = marks_of_device();
+    SPN_ARG(m && mark >= 0 && mark < 64, "spnerf_grad_mark_wait: bad mark");
+    SPN_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), m->ev[mark], 0));
     return SPNERF_OK;
 }
 

@@ -86,6 +86,76 @@ def allreduce_grads(params, world: int, group=None):
         p.grad.copy_(g)
 
 
+def bucket_ranges(numels, marks):
+    """Buckets of a flat gradient laid out in canonical parameter order: maximal runs of
+    consecutive parameters that become final at the same backward mark, as (mark, lo, hi)
+    element ranges sorted by mark (stable), covering [0, sum(numels)) exactly once."""
+    out, off = [], 0
+    for n, m in zip(numels, marks):
+        if out and out[-1][0] == m and out[-1][2] == off:
+            out[-1] = (m, out[-1][1], off + n)
+        else:
+            out.append((m, off, off + n))
+        off += n
+    return sorted(out, key=lambda r: r[0])
+
+
+class GradBuckets:
+    """The gradient all-reduce of a flat-gradient SPNeRF split into buckets, each issued as soon
+    as the backward has finished writing it, so the collectives overlap the rest of the backward.
+
+    The library's backward records mark events at fixed points (spnerf_grad_marks: after the
+    output heads' gradients, after each trunk layer's weight gradient, at the end); parameter p
+    is final at mark(p).  ``launch`` makes a communication stream wait for each bucket's mark and
+    issues its all_reduce(SUM) there (RCCL runs it on its own stream behind that wait); ``finish``
+    makes the current stream wait for every bucket, then divides by the world size.  ``arm``
+    must precede the backward (and a HIP graph capture of it: the marks are then captured as
+    external event nodes that every replay records)."""
+
+    def __init__(self, model, world: int, group=None, layout=None):
+        """``layout`` = (numels, marks) instead of the model's (host tests of the bucketing on
+        CPU tensors: no mark events, no streams)."""
+        from . import _lib
+        self._lib = _lib
+        self.world, self.group = world, group
+        if layout is None:
+            params = list(model.parameters())
+            numels = [p.numel() for p in params]
+            marks, self.n_marks = _lib.grad_marks(model.cfg(), len(params))
+        else:
+            numels, marks = layout
+            self.n_marks = max(marks) + 1
+        self.buckets = bucket_ranges(numels, marks)
+        self.stream = None
+        self.works = []
+
+    def arm(self, on: bool = True) -> None:
+        self._lib.grad_marks_arm(on)
+
+    def launch(self, flat: torch.Tensor) -> None:
+        if self.world <= 1:
+            return
+        on_gpu = flat.is_cuda
+        if on_gpu and self.stream is None:
+            self.stream = torch.cuda.Stream(device=flat.device)
+        for mark, lo, hi in self.buckets:
+            if not on_gpu:
+                self.works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+                continue
+            self._lib.grad_mark_wait(mark, self.stream)
+            with torch.cuda.stream(self.stream):
+                self.works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                                  async_op=True))
+
+    def finish(self, flat: torch.Tensor) -> None:
+        if self.world <= 1:
+            return
+        for w in self.works:
+            w.wait()
+        self.works = []
+        flat.div_(self.world)
+
+
 def _shared_flat(grads):
     """The buffer the gradients are consecutive views of, covering it exactly; else None."""
     base = grads[0]._base

@@ -49,6 +49,76 @@ def _step_grads(idx, world):
     return p
 
 
+def _cfg(d):
+    from spnerf_amd import _lib
+    c = _lib.ModelCfg()
+    c.width, c.layers, c.skip = d.width, d.layers, d.skips[0]
+    c.n_freq = d.n_freq if d.mapping else 0
+    c.sem_classes = d.num_sem_classes if d.sem else 0
+    c.sem_dim = d.sem_dim
+    c.beta, c.t_dim = int(d.beta), (d.t_dim if d.beta else 0)
+    return c
+
+
+def _bucket_worker(rank, world, port, out):
+    """the bucketed all-reduce (dp.GradBuckets, marks from the library) vs the flat one"""
+    from spnerf_amd import _lib
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    r, _, w = dp.init_from_env("gloo")
+    sampler = dp.SharedSeedSampler(N_RAYS, GB, r, w, seed=3)
+    _, idx = sampler.next()
+    params = list(_step_grads(idx, w).values())
+    flat = torch.cat([t.grad.reshape(-1) for t in params])
+    marks, n = _lib.grad_marks(_cfg(DIMS), len(params))
+    b = dp.GradBuckets(None, w, layout=([t.numel() for t in params], marks))
+    bucketed = flat.clone()
+    b.launch(bucketed)
+    b.finish(bucketed)
+    dp.allreduce_grads(params, w)
+    out[rank] = (bucketed.numpy(), torch.cat([t.grad.reshape(-1) for t in params]).numpy(), len(b.buckets), n)
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_equals_flat_allreduce():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for rank in range(world):
+        bucketed, flat, nb, n_marks = out[rank]
+        assert np.array_equal(bucketed, flat)    # same sums (a + b per element), same /world
+        assert nb > 8 and n_marks == DIMS.layers + 2
+    assert np.array_equal(out[0][0], out[1][0])
+
+
+@pytest.mark.parametrize("sem", [False, True])
+def test_grad_marks_cover_every_parameter_in_backward_order(sem):
+    """every parameter gets a mark; trunk layers become final top-down after the heads; the
+    per-ray parameters (and the semantic columns of layer 0 / the skip layer) at the end"""
+    from spnerf_amd import _lib
+    from oracle.weights import param_specs
+    d = ModelDims(width=64, sem=sem)
+    specs = param_specs(d)
+    marks, n = _lib.grad_marks(_cfg(d), len(specs))
+    m = {name: k for (name, _, _), k in zip(specs, marks)}
+    L, end = d.layers, d.layers + 1
+    assert n == L + 2 and min(marks) == 0 and max(marks) == end
+    for i in range(L):
+        assert m[f"fc_net.{2 * i}.bias"] == 1 + (L - 1 - i)
+        sem_cols = sem and i in (0, d.skips[0])
+        assert m[f"fc_net.{2 * i}.weight"] == (end if sem_cols else 1 + (L - 1 - i))
+    assert m["sigma_from_xyz.0.weight"] == m["feats_from_xyz.weight"] == m["sun_v_net.2.weight"] == 0
+    assert m["sun_v_net.0.weight"] == m["sky_color.0.weight"] == end
+    numels = [int(np.prod(s)) for _, s, _ in specs]
+    b = dp.bucket_ranges(numels, marks)
+    covered = sorted((lo, hi) for _, lo, hi in b)
+    assert covered[0][0] == 0 and covered[-1][1] == sum(numels)
+    assert all(a[1] == c[0] for a, c in zip(covered, covered[1:]))
+    assert [k for k, _, _ in b] == sorted(k for k, _, _ in b)
+
+
 def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))

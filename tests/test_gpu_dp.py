@@ -188,3 +188,102 @@ def test_two_ranks_philox_renders_equal_single_process_bitwise(tmp_path, noise_s
             assert got.shape == v.shape, k
             assert np.array_equal(got, v), (step, k, float(np.abs(got - v).max()))
     assert not np.array_equal(single[0]["z_vals_coarse"], single[1]["z_vals_coarse"])
+
+
+def bucket_runs(rank, world):
+    """One C3-flags training step of this rank's slice, three ways, same draws (the Philox
+    step is reset before each): eager + the flat all-reduce; eager + dp.GradBuckets (each
+    bucket's all-reduce issued behind its backward mark, overlapping the rest of the backward);
+    a HIP-graph replay of the step + GradBuckets (marks captured as external event nodes).
+    Returns the three reduced flat gradients."""
+    import types
+    import spnerf_amd
+    from spnerf_amd import dp
+    from spnerf_amd.losses import FusedRenderLoss
+    from spnerf_amd.scene import synthetic_scene
+    dev = torch.device("cuda", 0)
+    R = synthetic_scene(4.0, seed=0, device=dev)
+    sampler = dp.SharedSeedSampler(R.rays.shape[0], GLOBAL_B, rank, world, seed=5, device=dev)
+    gidx, idx = sampler.next()
+    b = GLOBAL_B // world
+    torch.manual_seed(0)
+    model = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True,
+                              precision="bf16").to(dev).use_flat_grads()
+    params = list(model.parameters())
+    args = types.SimpleNamespace(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+                                 sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)
+    floss = FusedRenderLoss(0.1, 1.0, 1.0)
+    src = spnerf_amd.PhiloxRandom(seed=11, ray_offset=rank * b)
+    buckets = dp.GradBuckets(model, world)
+
+    def fwd_bwd():
+        res = spnerf_amd.render_rays({"coarse": model}, args, R.rays[idx], None, semantics=R.sems[idx], mode="train",
+                                     valid_depth=R.valid_depth[idx], target_depths=R.depths[idx],
+                                     target_std=R.depth_std[idx], clamp_near_far=R.rays[gidx[0], 6:8])
+        loss, _ = floss(res, R.rgbs[idx], R.depths[idx], R.valid_depth[idx], R.depth_std[idx], R.sems[idx],
+                        labels_global=R.sems[gidx], world=world)
+        loss.backward()
+
+    def reset():
+        for p in params:
+            p.grad = None
+        if src._state is not None:
+            src._state[1].fill_(-1)
+
+    out = []
+    with spnerf_amd.random_source(src):
+        reset()
+        fwd_bwd()
+        dp.allreduce_grads(params, world)
+        out.append(model._flat_grad.cpu().numpy().copy())
+        reset()
+        buckets.arm(True)
+        fwd_bwd()
+        flat = model._flat_grad
+        buckets.launch(flat)
+        buckets.finish(flat)
+        out.append(flat.cpu().numpy().copy())
+        # graph: capture on a side stream after the eager warm-up above
+        reset()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fwd_bwd()
+        flat = model._flat_grad
+        src._state[1].fill_(-1)
+        graph.replay()
+        buckets.launch(flat)
+        buckets.finish(flat)
+        out.append(flat.cpu().numpy().copy())
+        buckets.arm(False)
+    return out
+
+
+def _bucket_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    from spnerf_amd import dp
+    torch.cuda.set_device(0)
+    dp.init_from_env("gloo")
+    flat, bucketed, graphed = bucket_runs(rank, world)
+    np.savez(os.path.join(outdir, f"bucket{rank}.npz"), flat=flat, bucketed=bucketed, graphed=graphed)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_overlapping_the_backward_equals_flat(tmp_path):
+    """dp.GradBuckets on the HIP path: the bucket all-reduces wait only for their backward marks
+    (spnerf_grad_marks) and run while the rest of the backward does — eager and inside a HIP graph
+    replay — and give exactly the flat all-reduce's gradient (any bucket read before its last
+    write would differ: the backward is deterministic)."""
+    world = 2
+    mp.spawn(_bucket_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    parts = [dict(np.load(tmp_path / f"bucket{r}.npz")) for r in range(world)]
+    for p in parts:
+        assert np.abs(p["flat"]).max() > 0
+        assert np.array_equal(p["bucketed"], p["flat"])
+        assert np.array_equal(p["graphed"], p["flat"])
+    assert np.array_equal(parts[0]["flat"], parts[1]["flat"])

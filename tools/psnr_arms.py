@@ -37,8 +37,17 @@ def main():
     ap.add_argument("--n-eval", type=int, default=4096)
     ap.add_argument("--lr", type=float, default=5e-4)
     ap.add_argument("--arms", default=",".join(a[0] for a in ARMS))
+    ap.add_argument("--seeds", default="", help="replica study: e.g. 3,4,5 -> each of --kinds per seed "
+                    "(init perturbed 1e-6 with that seed unless it is the first, Philox seed = it)")
+    ap.add_argument("--kinds", default="fp32,bf16", help="with --seeds: fp32, bf16, emu (fp32 + emu_bf16 7)")
     a = ap.parse_args()
-    arms = [x for x in ARMS if x[0] in a.arms.split(",")]
+    if a.seeds:
+        seeds = [int(x) for x in a.seeds.split(",")]
+        kinds = {"fp32": ("fp32", 0), "bf16": ("bf16", 0), "emu": ("fp32", 7)}
+        arms = [(f"{k}_s{sd}", kinds[k][0], 0.0 if sd == seeds[0] else 1e-6, sd, kinds[k][1])
+                for sd in seeds for k in a.kinds.split(",")]
+    else:
+        arms = [x for x in ARMS if x[0] in a.arms.split(",")]
     dev = "cuda:0"
     c = bench.CONFIGS["c3"]
     args = bench.make_args(c)
@@ -53,7 +62,7 @@ def main():
         m = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=True,
                               precision=prec).to(dev).use_flat_grads()
         if eps:
-            g = torch.Generator(device="cpu").manual_seed(99)
+            g = torch.Generator(device="cpu").manual_seed(99 + seed)
             with torch.no_grad():
                 for p in m.parameters():
                     p.mul_(1 + eps * torch.randn(p.shape, generator=g).to(dev))
