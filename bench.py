@@ -635,6 +635,8 @@ def parse_args(argv=None):
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="library kernel switch (spnerf_set_option), e.g. fused_trunk=0, nt_f32_variant=4")
     ap.add_argument("--global-batch", type=int, default=0, help="override the config's global batch (rays per step)")
+    ap.add_argument("--no-defer-wgrad", action="store_true",
+                    help="one trunk weight-gradient GEMM per pass instead of one over the main + solar passes")
     ap.add_argument("--flat-allreduce", action="store_true",
                     help="one all-reduce of the flat gradient after the backward instead of overlapped buckets")
     ap.add_argument("--share-device", action="store_true",
@@ -688,6 +690,7 @@ def run_train(a, config, rank, world, dev, secondary=False):
     model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"],
                               precision=c["precision"]).to(dev)
     model.use_flat_grads()   # backward adds into one flat buffer: the .grads are its views (one all-reduce)
+    model.defer_trunk_wgrad = not a.no_defer_wgrad
     params = list(model.parameters())
     if a.torch_adam:
         opt = torch.optim.Adam(params, lr=5e-4, fused=True)

@@ -64,6 +64,8 @@ typedef struct spnerf_rng {
 #define SPNERF_MLP_SIGMA_ONLY 2  /* trunk + sigma head only (pass 1 of guided sampling)      */
 #define SPNERF_MLP_SUN_ONLY 4    /* sigma + sun-visibility heads (solar-correction pass)     */
 #define SPNERF_MLP_ACCUMULATE 8  /* backward: add into grad_flat instead of overwriting it   */
+#define SPNERF_MLP_DEFER_TRUNK_WGRAD 16  /* backward: leave the trunk layers' weight gradients to
+                                          * spnerf_mlp_trunk_wgrad (the workspace must stay intact) */
 
 /* composite flags */
 #define SPNERF_COMP_WEIGHTS_ONLY 1  /* weights, transparency, depth only (no rgb / sem)      */
@@ -102,6 +104,17 @@ int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed,
                             const int64_t* labels, const float* t_emb, int32_t flags,
                             void* workspace, const float* d_out, float* grad_flat, float* grad_t_emb,
                             void* stream);
+
+/* The trunk layers' weight gradients (fc_net.2i.weight / .bias, without the per-ray semantic
+ * columns) of up to n_seg deferred backwards (SPNERF_MLP_DEFER_TRUNK_WGRAD), added into grad_flat:
+ * the points of two workspaces (e.g. a render's main and solar-correction passes, rendering.py:
+ * 165-177, whose backwards both reach the same trunk) run as ONE weight-gradient GEMM per layer —
+ * half the launches and split reductions of one GEMM per pass.  n_rays / n_samples / flags are
+ * those of each workspace's forward.  n_seg = 0: returns 1 if a backward may defer under the
+ * current options (the bf16 MLP with its fused dX chain), else 0. */
+int32_t spnerf_mlp_trunk_wgrad(const spnerf_model_cfg* cfg, int32_t n_seg, void* const* workspaces,
+                               const int64_t* n_rays, const int32_t* n_samples, const int32_t* flags,
+                               float* grad_flat, void* stream);
 
 /* ---- compositing: inference() (spnerf.py:109-157) --------------------------------------- */
 /* noise (n_rays, n_samples) N(0,1) draws scaled by noise_std, or NULL with rng set: drawn on the

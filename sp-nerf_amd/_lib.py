@@ -18,6 +18,7 @@ SPNERF_MLP_SAVE = 1
 SPNERF_MLP_SIGMA_ONLY = 2
 SPNERF_MLP_SUN_ONLY = 4
 SPNERF_MLP_ACCUMULATE = 8
+SPNERF_MLP_DEFER_TRUNK_WGRAD = 16
 SPNERF_COMP_WEIGHTS_ONLY = 1
 
 
@@ -92,6 +93,8 @@ SIGNATURES = {
     "spnerf_prof_reset": (c_int32, []),
     "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
     "spnerf_prof_classes": (c_int32, [c_char_p, c_int32]),
+    "spnerf_mlp_trunk_wgrad": (c_int32, [POINTER(ModelCfg), c_int32, POINTER(c_void_p), POINTER(c_int64),
+                                         POINTER(c_int32), POINTER(c_int32), c_void_p, c_void_p]),
     "spnerf_grad_marks": (c_int32, [POINTER(ModelCfg), POINTER(c_int32), c_int32]),
     "spnerf_grad_marks_arm": (c_int32, [c_int32]),
     "spnerf_grad_mark_wait": (c_int32, [c_int32, c_void_p]),

@@ -1,5 +1,6 @@
 // Launch descriptors of the bf16 MFMA GEMMs (gemm_bf16.hip), the cfg.dtype = 1 path.
 #pragma once
+#include <climits>
 #include "common.h"
 
 namespace spn {
@@ -43,6 +44,11 @@ struct TN16Args {
     int p_per_split = 0;  // set by gemm_tn_bf16
     int b_sin = 0;        // B's columns [0, K1) hold a saved Z (fp16): staged as bf16(sin(Z)) (= the layer's H)
     int dbg = 0;          // ablations (tools only; wide tiles): 1 = no MFMAs
+    // Second point segment (one weight gradient over two passes' points, spnerf_mlp_trunk_wgrad):
+    // rows p >= P1 read A_s2 / B_s2 / B2_s2 + p * ld — pointers the host shifted back by P1 rows,
+    // same leading dimensions.  P1 >= P (the default) = one segment.
+    int64_t P1 = INT64_MAX;
+    const bf16 *A_s2 = nullptr, *B_s2 = nullptr, *B2_s2 = nullptr;
 };
 
 // variant: prefetch depth in K-steps (1 or 2); <= 0 = library default (g_nt16_variant)

@@ -754,6 +754,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
     const int nc = min(n0 + 8 * ch, g.N - 8);
     const int kc = min(k0 + 8 * ch, g.K - 8);
     const bf16* pb = kc < g.K1 ? g.B + kc : g.B2 + (kc - g.K1);
+    const bf16* pb2 = kc < g.K1 ? g.B_s2 + kc : g.B2_s2 + (kc - g.K1);  // second segment
     const bool bsin = g.b_sin && kc < g.K1;  // this thread's B chunk is a saved Z: stage sin(Z)
     const int ldb = kc < g.K1 ? g.ldb : g.ldb2;
     const int lda = g.lda;
@@ -763,8 +764,9 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int pc = min(p0 + lrow + 16 * i, p_end - 1);
-            ra[i] = ldg16(g.A + (int64_t)pc * lda + nc);
-            rb[i] = ldg16(pb + (int64_t)pc * ldb);
+            const bool s2 = pc >= g.P1;
+            ra[i] = ldg16((s2 ? g.A_s2 : g.A) + (int64_t)pc * lda + nc);
+            rb[i] = ldg16((s2 ? pb2 : pb) + (int64_t)pc * ldb);
         }
     };
     auto sstore = [&](int stg) {
@@ -898,6 +900,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
     const int nc = min(n0 + 8 * ch, g.N - 8);
     const int kc = min(k0 + 8 * ch, g.K - 8);
     const bf16* pb = kc < g.K1 ? g.B + kc : g.B2 + (kc - g.K1);
+    const bf16* pb2 = kc < g.K1 ? g.B_s2 + kc : g.B2_s2 + (kc - g.K1);  // second segment
     const bool bsin = g.b_sin && kc < g.K1;  // this thread's B chunk is a saved Z: stage sin(Z)
     const int ldb = kc < g.K1 ? g.ldb : g.ldb2;
     const int lda = g.lda;
@@ -908,8 +911,9 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int pc = min(p0 + lrow + 16 * i, p_end - 1);
-            ra[i] = ldg16(g.A + (int64_t)pc * lda + nc);
-            rb[i] = ldg16(pb + (int64_t)pc * ldb);
+            const bool s2 = pc >= g.P1;
+            ra[i] = ldg16((s2 ? g.A_s2 : g.A) + (int64_t)pc * lda + nc);
+            rb[i] = ldg16((s2 ? pb2 : pb) + (int64_t)pc * ldb);
         }
     };
     auto sstore = [&](int stg) {
@@ -1045,7 +1049,9 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 
     // this lane's 4 DMA sources (instructions q = wid + 8 i: i < 2 → A, else B), advanced by
     // TD_STEP rows per step
+    // second point segment (g.P1 a multiple of TD_STEP, host-checked): a step lies in one segment
     const bf16* src[4];
+    const bf16* src2[4];
     int ld[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1055,20 +1061,23 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
         const int f = (X ? k0 : n0) + hf * 128 + 8 * chl;
         if (X == 0) {
             src[i] = g.A + (int64_t)row * g.lda + min(f, g.N - 8);
+            src2[i] = g.A_s2 + (int64_t)row * g.lda + min(f, g.N - 8);
             ld[i] = g.lda;
         } else {
             const int kc = min(f, g.K - 8);
             const bool s2 = kc >= g.K1;
             ld[i] = s2 ? g.ldb2 : g.ldb;
             src[i] = (s2 ? g.B2 + (kc - g.K1) : g.B + kc) + (int64_t)row * ld[i];
+            src2[i] = (s2 ? g.B2_s2 + (kc - g.K1) : g.B_s2 + kc) + (int64_t)row * ld[i];
         }
     }
     auto issue = [&](int st, int stg) {
         const int64_t p0 = p_beg + (int64_t)TD_STEP * st;
+        const bool sg2 = p0 >= g.P1;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int q = wid + 8 * i;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src[i] + p0 * ld[i]),
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)((sg2 ? src2[i] : src[i]) + p0 * ld[i]),
                                              (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
         }
     };
@@ -1302,7 +1311,10 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     pps = (pps + 63) / 64 * 64;
     a.p_per_split = pps < 64 ? 64 : pps;
     const bool wide = tn_wide(a.N, a.K, -1);
-    const bool dma = wide && g_tn16_variant == 3 && a.P % TD_STEP == 0 && !a.b_sin;  // DMA: whole 32-point steps
+    const bool two = a.P1 < a.P;
+    SPN_ARG(!two || (a.A_s2 && a.B_s2 && (a.K1 >= a.K || a.B2_s2)), "gemm_tn_bf16: second segment incomplete");
+    // DMA: whole 32-point steps (and a segment boundary on a step)
+    const bool dma = wide && g_tn16_variant == 3 && a.P % TD_STEP == 0 && !a.b_sin && (!two || a.P1 % TD_STEP == 0);
     ProfScope prof(dma ? "gemm_tn_bf16d" : wide ? "gemm_tn_bf16w" : "gemm_tn_bf16", s, 2.0 * a.P * a.N * a.K,
                    2.0 * (double)a.P * (a.N + a.K) + 4.0 * splits * (double)a.N * a.K);
     if (wide) {

@@ -1039,6 +1039,7 @@ struct Ctx {
     float* ws;       // workspace base
     int S;
     int acc = 0;     // backward: gradient reductions add into the flat gradient
+    int defer = 0;   // backward: the trunk layers' weight gradients are left to spnerf_mlp_trunk_wgrad
     // the forward's ray inputs (the fused inference trunk encodes layer 0's input itself)
     const float* rays = nullptr;
     const float* z = nullptr;
@@ -1077,11 +1078,20 @@ struct Gemms<bf16> {
 
 int g_tn_split_tail = 1;  // option "tn_split_tail": see tn_grad
 
+// A second point segment of a weight gradient: the same operands in another pass's workspace
+// (spnerf_mlp_trunk_wgrad: the main and the solar pass of a render in one GEMM per layer)
+struct TnSeg {
+    const bf16 *A = nullptr, *B = nullptr, *B2 = nullptr;
+    int64_t P = 0;
+};
+
 template <typename T>
 static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int ldb, const T* B2, int ldb2, int K1,
-                       int K, hipStream_t s, const std::vector<ReduceArgs>& outs, bool b_sin = false) {
+                       int K, hipStream_t s, const std::vector<ReduceArgs>& outs, bool b_sin = false,
+                       const TnSeg* sg = nullptr) {
     using G = Gemms<T>;
-    const int P = (int)c.w.P;
+    const int P1 = (int)c.w.P;
+    const int P = P1 + (sg ? (int)sg->P : 0);
     // bf16 skip layer ([H | x0], K = 512 + K0p): the K = 576 GEMM has no 256-wide tiling and ran
     // on the 128x128 kernel at 710 us per 524 288 points; split into the wide K = 512 part and
     // the K0p tail (two passes over dZ, the tail's slab reduced into columns K1..) it is ≈470.
@@ -1103,11 +1113,19 @@ static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int
                 tail.push_back(t);
             }
         }
-        SPN_TRY(tn_grad<T>(c, A, lda, N, B, ldb, nullptr, 0, K1, K1, s, head, b_sin));
-        if (!tail.empty()) SPN_TRY(tn_grad<T>(c, A, lda, N, B2, ldb2, nullptr, 0, K - K1, K - K1, s, tail));
+        TnSeg sh, st;
+        if (sg) {
+            sh = {sg->A, sg->B, nullptr, sg->P};
+            st = {sg->A, sg->B2, nullptr, sg->P};
+        }
+        SPN_TRY(tn_grad<T>(c, A, lda, N, B, ldb, nullptr, 0, K1, K1, s, head, b_sin, sg ? &sh : nullptr));
+        if (!tail.empty())
+            SPN_TRY(tn_grad<T>(c, A, lda, N, B2, ldb2, nullptr, 0, K - K1, K - K1, s, tail, false, sg ? &st : nullptr));
         return SPNERF_OK;
     }
-    const int splits = G::splits(P, N, K);
+    // the slab buffer is sized for this workspace's points: a longer (two-segment) GEMM takes
+    // no more splits than that
+    const int splits = std::min(G::splits(P, N, K), G::splits(P1, N, K));
     typename G::TN t;
     t.A = A; t.lda = lda;
     t.B = B; t.ldb = ldb; t.B2 = B2; t.ldb2 = ldb2; t.K1 = K1;
@@ -1115,6 +1133,17 @@ static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int
     t.slab = c.at(c.w.slab); t.ld_slab = K; t.slab_stride = (int64_t)N * K;
     t.slab_b = c.at(c.w.slab_b);
     t.P = P; t.N = N; t.K = K;
+    if (sg) {
+        if constexpr (std::is_same<T, bf16>::value) {
+            // rows p >= P1 come from the second segment: its pointers shifted back by P1 rows
+            t.P1 = P1;
+            t.A_s2 = sg->A - (int64_t)P1 * lda;
+            t.B_s2 = sg->B - (int64_t)P1 * ldb;
+            t.B2_s2 = sg->B2 ? sg->B2 - (int64_t)P1 * ldb2 : nullptr;
+        } else {
+            SPN_ARG(false, "tn_grad: two point segments need the bf16 MLP");
+        }
+    }
     SPN_TRY(G::tn(t, splits, s));
     std::vector<ReduceArgs> rs;
     for (ReduceArgs r : outs) {
@@ -1568,7 +1597,8 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         const T* In = i == 0 ? X0 : buf(zin ? c.w.Db[i - 1] : c.w.Hb[i - 1]);
         const int ldin = i == 0 ? d.K0p : W;
         const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
-        if (i == d.skip)
+        if (c.defer) {   // spnerf_mlp_trunk_wgrad computes it later, over this and other passes' points
+        } else if (i == d.skip)
             SPN_TRY(tn_grad<T>(c, dZi, W, W, In, W, X0, d.K0p, W, W + d.K0p, s2,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
         else
@@ -1621,13 +1651,66 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     return SPNERF_OK;
 }
 
+// Deferred trunk weight gradients need every layer's dZ to outlive the backward: the fused dX
+// chain of the bf16 MLP leaves dZ_i in Db[i] (and dZ_{L-1} in dZa) — the layer-by-layer chain
+// rotates three buffers.
+static bool trunk_wgrad_ok(const Ctx& c) {
+    return c.d.bf && !g_zsave && g_fused_bwd && !c.k.Wb16.empty() && c.k.Wb16[1] >= 0;
+}
+
+// The trunk layers' weight gradients (fc_net.2i weight / bias, without the per-ray semantic
+// columns, which each backward adds itself) over the points of up to two deferred backwards'
+// workspaces per GEMM, added into grad (spnerf_mlp_trunk_wgrad).
+static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int64_t* n_rays, const int32_t* S,
+                           const int32_t* flags, float* grad, hipStream_t s) {
+    PIdx x;
+    auto specs = param_specs(d, &x);
+    auto gp = [&](int pi) { return grad + specs[pi].off; };
+    auto ld = [&](int pi) { return (int)specs[pi].ld(); };
+    const int W = d.W;
+    for (int j = 0; j < n_seg; j += 2) {
+        auto ctx = [&](int k) {
+            const int fl = flags[k] & ~(SPNERF_MLP_ACCUMULATE | SPNERF_MLP_DEFER_TRUNK_WGRAD);
+            Ctx c{d, packed_layout(d), ws_layout(d, n_rays[k], S[k], fl), nullptr, static_cast<float*>(wss[k]), S[k]};
+            c.acc = 1;
+            return c;
+        };
+        const Ctx c = ctx(j);
+        SPN_ARG(wss[j] && (flags[j] & SPNERF_MLP_SAVE) && trunk_wgrad_ok(c), "spnerf_mlp_trunk_wgrad: bad segment");
+        const bool two = j + 1 < n_seg;
+        Ctx c2 = two ? ctx(j + 1) : c;
+        if (two) SPN_ARG(wss[j + 1] && (flags[j + 1] & SPNERF_MLP_SAVE), "spnerf_mlp_trunk_wgrad: bad segment");
+        if (c.w.P + (two ? c2.w.P : 0) == 0) continue;
+        for (int i = d.L - 1; i >= 0; --i) {
+            auto dz = [&](const Ctx& q) { return q.hb(i == d.L - 1 ? q.w.dZa : q.w.Db[i]); };
+            auto in = [&](const Ctx& q) { return q.hb(i == 0 ? q.w.X0b : q.w.Hb[i - 1]); };
+            const int ldin = i == 0 ? d.K0p : W;
+            const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
+            const TnSeg sg{dz(c2), in(c2), c2.hb(c2.w.X0b), c2.w.P};
+            const TnSeg* psg = two ? &sg : nullptr;
+            if (i == d.skip)
+                SPN_TRY(tn_grad<bf16>(c, dz(c), W, W, in(c), W, c.hb(c.w.X0b), d.K0p, W, W + d.K0p, s,
+                                      {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, false, psg));
+            else
+                SPN_TRY(tn_grad<bf16>(c, dz(c), W, W, in(c), ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s,
+                                      {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, false, psg));
+            SPN_TRY(grad_mark(1 + (d.L - 1 - i), s));
+        }
+    }
+    return grad_mark(d.L + 1, s);
+}
+
 static int32_t mlp_backward(const Dims& d, const float* packed, const float* rays, int rs, int64_t n_rays, int S,
                             const int64_t* labels, const float* temb, int flags, float* ws, const float* d_out,
                             float* grad, float* grad_t, hipStream_t s) {
     SPN_ARG(flags & SPNERF_MLP_SAVE, "backward needs a workspace written with SPNERF_MLP_SAVE");
     SPN_ARG(!(flags & SPNERF_MLP_SIGMA_ONLY), "backward of a sigma-only pass is not supported");
-    Ctx c{d, packed_layout(d), ws_layout(d, n_rays, S, flags & ~SPNERF_MLP_ACCUMULATE), packed, ws, S};
+    Ctx c{d, packed_layout(d), ws_layout(d, n_rays, S, flags & ~(SPNERF_MLP_ACCUMULATE | SPNERF_MLP_DEFER_TRUNK_WGRAD)),
+          packed, ws, S};
     c.acc = (flags & SPNERF_MLP_ACCUMULATE) ? 1 : 0;
+    c.defer = (flags & SPNERF_MLP_DEFER_TRUNK_WGRAD) ? 1 : 0;
+    SPN_ARG(!c.defer || trunk_wgrad_ok(c), "backward: SPNERF_MLP_DEFER_TRUNK_WGRAD needs the bf16 MLP's fused dX chain "
+                                           "(spnerf_mlp_trunk_wgrad with n_seg = 0 tells)");
     const int mode = (flags & SPNERF_MLP_SUN_ONLY) ? 2 : 0;
     const int64_t P = n_rays * S;
     const int W = d.W, H = d.H;
@@ -1741,6 +1824,19 @@ extern "C" int32_t spnerf_get_option(const char* name, int32_t* value) {
     SPN_ARG(slot != nullptr, "get_option: unknown option '%s'", name);
     *value = *slot;
     return SPNERF_OK;
+}
+
+extern "C" int32_t spnerf_mlp_trunk_wgrad(const spnerf_model_cfg* cfg, int32_t n_seg, void* const* workspaces,
+                                          const int64_t* n_rays, const int32_t* n_samples, const int32_t* flags,
+                                          float* grad_flat, void* stream) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    if (n_seg == 0) {   // capability query: may a backward defer under the current options?
+        Ctx c{d, packed_layout(d), WS{}, nullptr, nullptr, 0};
+        return trunk_wgrad_ok(c) ? 1 : 0;
+    }
+    SPN_ARG(n_seg > 0 && workspaces && n_rays && n_samples && flags && grad_flat, "spnerf_mlp_trunk_wgrad: NULL argument");
+    return trunk_wgrad(d, n_seg, workspaces, n_rays, n_samples, flags, grad_flat, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int32_t spnerf_grad_marks(const spnerf_model_cfg* cfg, int32_t* mark_of_param, int32_t n_params) {

@@ -40,7 +40,7 @@ namespace spn {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // 0 = the one-workgroup kernels (default); 1 = this kernel for the saving (training) launches;
-// 2 = also for inference launches.  Measured on MI355X (tools/gpu_t2ab.sh, tools/pmc_trunk2.sh,
+// 2 = for every launch; 3 = for the inference (non-saving) launches only.  Measured on MI355X (tools/gpu_t2ab.sh, tools/pmc_trunk2.sh,
 // training forward at 524 288 points): one-workgroup k_trunk_bf16<64> 3.05 ms, this kernel
 // 3.08 ms (64-point tiles, two workgroups per CU) and 3.38 ms (128-point tiles); without any HBM
 // copy-out it is the faster one (1.84–1.96 against 2.45 ms), but PMC shows the waves waiting on
@@ -403,7 +403,8 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(T
 int g_trunk2_tile = 128;  // option "trunk2_tile": 64 (two workgroups per CU) or 128
 
 bool trunk2_supported(const TrunkArgs& a, bool save) {
-    if (g_trunk2 == 0 || (g_trunk2 == 1 && !save) || a.zround) return false;
+    const bool on = g_trunk2 == 2 || (g_trunk2 == 1 && save) || (g_trunk2 == 3 && !save);
+    if (!on || a.zround) return false;
     const int TM = g_trunk2_tile == 64 ? 64 : 128;
     const bool l0 = a.X0 || a.rays;
     if (l0 && !(a.K0p % 4 == 0 && (a.K0p / 4) % TPD == 0)) return false;

@@ -19,8 +19,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_ACCUMULATE, SPNERF_MLP_SAVE, SPNERF_MLP_SIGMA_ONLY,
-                   SPNERF_MLP_SUN_ONLY)
+from ._lib import (SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_ACCUMULATE, SPNERF_MLP_DEFER_TRUNK_WGRAD, SPNERF_MLP_SAVE,
+                   SPNERF_MLP_SIGMA_ONLY, SPNERF_MLP_SUN_ONLY)
 from .rng import current_random_source, device_key
 
 
@@ -133,6 +133,8 @@ class SPNeRF(torch.nn.Module):
         self._pack_pool = []
         self._flat_grad = None
         self.flat_grads = False  # opt-in direct gradient path (use_flat_grads)
+        # with flat gradients: one trunk weight-gradient GEMM per layer over all passes of a render
+        self.defer_trunk_wgrad = True
 
     # ---------------------------------------------------------------- library plumbing
     def cfg(self) -> _lib.ModelCfg:
@@ -300,7 +302,27 @@ class WeightPack:
 
     def __init__(self, model, owned: bool):
         self.model, self.owned, self.pending = model, owned, 0
+        self.nsave = 0          # saving forwards of this render (main pass, solar pass, ...)
+        self.deferred = []      # backwards that left their trunk weight gradients (see _MLP.backward)
         self.buf = model.packed_weights(own=owned)
+
+    def flush_trunk_wgrad(self):
+        """The trunk layers' weight gradients of the deferred backwards: ONE weight-gradient GEMM
+        per layer over their points (spnerf_mlp_trunk_wgrad), added into the model's flat
+        gradient.  Queued as an autograd-engine callback, so it runs once the whole backward pass
+        is done, whichever of the render's passes were differentiated."""
+        if not self.deferred:
+            return
+        segs, self.deferred = self.deferred, []
+        grad, stream = segs[0][4], segs[0][5]
+        n = len(segs)
+        wss = (ctypes.c_void_p * n)(*[t[0].data_ptr() for t in segs])
+        nr = (ctypes.c_int64 * n)(*[t[1] for t in segs])
+        ns = (ctypes.c_int32 * n)(*[t[2] for t in segs])
+        fl = (ctypes.c_int32 * n)(*[t[3] for t in segs])
+        # on the stream the backwards ran on (an engine callback may run on another thread / stream)
+        _lib.check(_lib.lib().spnerf_mlp_trunk_wgrad(ctypes.byref(self.model.cfg()), n, wss, nr, ns, fl, _lib.ptr(grad),
+                                                      ctypes.c_void_p(stream.cuda_stream)), "mlp_trunk_wgrad")
 
     def done(self):
         self.pending -= 1
@@ -339,6 +361,7 @@ class _MLP(torch.autograd.Function):
                                         _lib.ptr(out), _lib.stream_of(rays)), "mlp_forward")
         if need_grad:
             pack.pending += 1
+            pack.nsave += 1
             ctx.model, ctx.flags, ctx.ws, ctx.pack, ctx.packed = model, flags, ws, pack, packed
             ctx.shape = (B, S)
             ctx.save_for_backward(rays, labels, temb)
@@ -357,14 +380,27 @@ class _MLP(torch.autograd.Function):
         flags = ctx.flags
         grad = model.flat_grad_target(params)
         direct = grad is not None
+        pack = ctx.pack
+        # A render with several saving passes (main + solar correction) over one bf16 trunk: each
+        # backward leaves the trunk's weight gradients, and one GEMM per layer over all the passes'
+        # points runs when the backward pass ends (half the launches and split reductions)
+        defer = (direct and pack.nsave > 1 and model.precision == "bf16" and model.defer_trunk_wgrad
+                 and _lib.lib().spnerf_mlp_trunk_wgrad(ctypes.byref(model.cfg()), 0, None, None, None, None, None,
+                                                       None) == 1)
         if direct:   # add straight into the .grad views (the library's fixed-order reductions)
             flags |= SPNERF_MLP_ACCUMULATE
         else:
             grad = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=rays.device)
+        if defer:
+            flags |= SPNERF_MLP_DEFER_TRUNK_WGRAD
         _lib.check(_lib.lib().spnerf_mlp_backward(ctypes.byref(model.cfg()), _lib.ptr(ctx.packed), _lib.ptr(rays),
                                                   rays.stride(0), B, S, _lib.ptr(labels), _lib.ptr(temb), flags,
                                                   _lib.ptr(ctx.ws), _lib.ptr(d_out), _lib.ptr(grad),
                                                   _lib.ptr(gt), _lib.stream_of(rays)), "mlp_backward")
+        if defer:
+            if not pack.deferred:
+                torch.autograd.Variable._execution_engine.queue_callback(pack.flush_trunk_wgrad)
+            pack.deferred.append((ctx.ws, B, S, ctx.flags, grad, torch.cuda.current_stream(rays.device)))
         ctx.pack.done()
         ctx.pack = ctx.packed = None
         ctx.ws = None

@@ -44,3 +44,39 @@ def test_flat_grads_never_touch_frozen_parameters():
     _loss(m).backward()
     assert frozen.grad is None
     assert all(p.grad is not None for n, p in m.named_parameters() if p.requires_grad and "semantic" not in n)
+
+
+@pytest.mark.parametrize("sem", [False, True])
+def test_deferred_trunk_weight_gradients_match_per_pass(sem):
+    """bf16 MLP, main + solar pass: with flat gradients the two backwards leave the trunk's weight
+    gradients to one two-segment GEMM per layer (spnerf_mlp_trunk_wgrad, run by an autograd
+    callback).  Same gradient as one GEMM per pass up to fp32 summation order."""
+    import types
+    args = types.SimpleNamespace(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+                                 sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)
+    rays = torch.tensor(gu_rays(96, 4), device=DEV)
+    g = torch.Generator().manual_seed(3)
+    depths = torch.rand(96, 2, generator=g).to(DEV) * 0.5 + 0.2
+    valid = (torch.rand(96, generator=g) > 0.3).long().to(DEV)
+    sems = torch.randint(0, 3, (96,), generator=g).to(DEV)
+    grads = {}
+    for defer in (False, True):
+        torch.manual_seed(0)
+        m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=sem,
+                              precision="bf16").to(DEV).use_flat_grads()
+        m.defer_trunk_wgrad = defer
+        with spnerf_amd.random_source(spnerf_amd.PhiloxRandom(seed=5)):
+            res = spnerf_amd.render_rays({"coarse": m}, args, rays, None, semantics=sems if sem else None, mode="train",
+                                         valid_depth=valid, target_depths=depths, target_std=depths[:, 1] * 0 + 0.01)
+        loss = (res["rgb_coarse"] ** 2).mean() + res["sun_sc_coarse"].mean() + res["depth_coarse"].mean()
+        loss.backward()
+        grads[defer] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    num = den = 0.0
+    for n, a in grads[False].items():
+        b = grads[True][n]
+        num += float(((a - b).double() ** 2).sum())
+        den += float((a.double() ** 2).sum())
+        if a.numel() >= 64 and float(a.norm()) > 0:
+            assert float((a - b).norm() / a.norm()) <= 1e-3, n
+    assert (num / den) ** 0.5 <= 1e-5
+    assert float(grads[True]["fc_net.2.weight"].norm()) > 0
