@@ -348,6 +348,8 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
         if check and step > 0:
             for a in arms:
                 curves[a].append((step + 1, held_psnr(models[a])))
+            print(f"psnr_long: step {step + 1}/{steps} " + " ".join(f"{a} {curves[a][-1][1]:.3f}" for a in arms)
+                  + f" grad_rel_err {grad_err[-1][1]:.2e} ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
     train_s = time.perf_counter() - t0
     final = {a: curves[a][-1][1] for a in arms}
     half = [k for k in range(len(curves["fp32"])) if curves["fp32"][k][0] > steps // 2]

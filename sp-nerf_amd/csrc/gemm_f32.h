@@ -70,10 +70,17 @@ int32_t gemm_nt(const NTArgs& a, hipStream_t s, int variant = -1);
 int tn_splits(int P, int N, int K);
 int skinny_chunk(int64_t P);
 int32_t tn_skinny(const SkinnyArgs& a, hipStream_t s);
+constexpr int kSkinnyMulti = 8;
+struct SkinnyMulti {
+    SkinnyArgs t[kSkinnyMulti];
+    int n = 0;
+};
+// up to kSkinnyMulti fp32-B skinny reductions (own slabs each) in one launch
+int32_t tn_skinny_multi(const SkinnyArgs* a, int n, hipStream_t s);
 extern int g_tn_variant;  // 0 = one LDS stage, 1 = double-buffered
 int32_t gemm_tn(const TNArgs& a, int splits, hipStream_t s, int variant = -1);
 int32_t reduce_slabs(const ReduceArgs& a, hipStream_t s);
-constexpr int kReduceMulti = 4;
+constexpr int kReduceMulti = 8;
 struct ReduceMulti {
     ReduceArgs seg[kReduceMulti];
     int n = 0;

@@ -819,15 +819,14 @@ __global__ __launch_bounds__(256) void k_reduce_slabs_multi(ReduceMulti m) {
 // loads issued before their arithmetic (the rows still add in increasing order); the row phases'
 // partials are combined through LDS in phase order.
 template <int MA, typename TB>
-__global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __restrict__ Bm) {
+__device__ __forceinline__ void skinny_block(const SkinnyArgs& g, const TB* __restrict__ Bm, const int blk, float* red) {
     constexpr int V = sizeof(TB) == 2 ? 8 : 4;     // B values per 16-B load
-    __shared__ float red[256 * V];
     const int tid = threadIdx.x;
     const int kq = g.K / V;                        // column groups (kq <= 256, checked on host)
     const int rph = 256 / kq;                      // row phases
     const int c4 = tid % kq, ph = tid / kq;
     const bool live = ph < rph;
-    const int64_t p0 = (int64_t)blockIdx.x * g.chunk;
+    const int64_t p0 = (int64_t)blk * g.chunk;
     const int64_t p1 = min(g.P, p0 + g.chunk);
     const int Mt = g.Ma + (g.ones ? 1 : 0);
     float acc[MA + 1][V];
@@ -900,7 +899,7 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __res
             for (int e = 0; e < V; ++e) {
                 float sum = v[e];
                 for (int r = 1; r < rph; ++r) sum += red[V * (r * kq + c4) + e];
-                g.slab[((int64_t)blockIdx.x * Mt + m) * g.K + V * c4 + e] = sum;
+                g.slab[((int64_t)blk * Mt + m) * g.K + V * c4 + e] = sum;
             }
         }
     }
@@ -916,10 +915,28 @@ __global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __res
             if (tid == 0) {
                 float sum = 0.f;
                 for (int q = 0; q < rph; ++q) sum += red[q * kq];
-                g.slab_b[(int64_t)blockIdx.x * g.Ma + m] = sum;
+                g.slab_b[(int64_t)blk * g.Ma + m] = sum;
             }
         }
     }
+}
+
+template <int MA, typename TB>
+__global__ __launch_bounds__(256) void k_tn_skinny(SkinnyArgs g, const TB* __restrict__ Bm) {
+    __shared__ float red[256 * (sizeof(TB) == 2 ? 8 : 4)];
+    skinny_block<MA, TB>(g, Bm, blockIdx.x, red);
+}
+
+// several skinny reductions in one launch (the per-ray parameter gradients of a backward, the
+// narrow heads' weight gradients): blockIdx.y = task, blockIdx.x = chunk (tasks with fewer
+// chunks leave the rest idle); every task's B rows of type TB
+template <int MA, typename TB>
+__global__ __launch_bounds__(256) void k_tn_skinny_multi(SkinnyMulti m) {
+    __shared__ float red[256 * (sizeof(TB) == 2 ? 8 : 4)];
+    const SkinnyArgs& g = m.t[blockIdx.y];
+    if ((int64_t)blockIdx.x * g.chunk >= g.P) return;   // whole block: before any barrier
+    if constexpr (sizeof(TB) == 2) skinny_block<MA, bf16>(g, g.B16, blockIdx.x, red);
+    else skinny_block<MA, float>(g, g.B, blockIdx.x, red);
 }
 
 // 8: 256x128 tiles on 4-wave blocks, two per CU, LDS-DMA K-steps of 16 (k_gemm_nt_w<.., 2, 2, 3>);
@@ -989,6 +1006,41 @@ int32_t tn_skinny(const SkinnyArgs& a0, hipStream_t s) {
         if (a.Ma <= 1) hipLaunchKernelGGL((k_tn_skinny<1, float>), dim3(nb), dim3(256), 0, s, a, a.B);
         else if (a.Ma <= 3) hipLaunchKernelGGL((k_tn_skinny<3, float>), dim3(nb), dim3(256), 0, s, a, a.B);
         else hipLaunchKernelGGL((k_tn_skinny<8, float>), dim3(nb), dim3(256), 0, s, a, a.B);
+    }
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+int32_t tn_skinny_multi(const SkinnyArgs* a, int n, hipStream_t s) {
+    SPN_ARG(n >= 0 && n <= kSkinnyMulti, "tn_skinny_multi: %d tasks", n);
+    SkinnyMulti m;
+    m.n = 0;
+    int nb = 0, ma = 1;
+    double fl = 0.0, by = 0.0;
+    const bool b16 = n > 0 && a[0].B16;
+    for (int i = 0; i < n; ++i) {
+        SkinnyArgs t = a[i];
+        SPN_ARG(t.Ma >= 1 && t.Ma <= 8 && (b16 ? (t.B16 && t.K % 8 == 0 && t.K <= 2048 && t.ldb % 8 == 0)
+                                                : (!t.B16 && t.B && t.K % 4 == 0 && t.K <= 1024 && t.ldb % 4 == 0)),
+                "tn_skinny_multi: bad task Ma=%d K=%d", t.Ma, t.K);
+        if (t.P <= 0) continue;
+        t.chunk = skinny_chunk(t.P);
+        nb = std::max(nb, cdiv(t.P, t.chunk));
+        ma = std::max(ma, t.Ma);
+        fl += 2.0 * t.P * t.K * (t.Ma + t.ones);
+        by += 4.0 * t.P * (t.K + t.Ma);
+        m.t[m.n++] = t;
+    }
+    if (m.n == 0) return SPNERF_OK;
+    ProfScope prof("tn_skinny", s, fl, by);
+    if (b16) {
+        if (ma <= 1) hipLaunchKernelGGL((k_tn_skinny_multi<1, bf16>), dim3(nb, m.n), dim3(256), 0, s, m);
+        else if (ma <= 3) hipLaunchKernelGGL((k_tn_skinny_multi<3, bf16>), dim3(nb, m.n), dim3(256), 0, s, m);
+        else hipLaunchKernelGGL((k_tn_skinny_multi<8, bf16>), dim3(nb, m.n), dim3(256), 0, s, m);
+    } else if (ma <= 3) {
+        hipLaunchKernelGGL((k_tn_skinny_multi<3, float>), dim3(nb, m.n), dim3(256), 0, s, m);
+    } else {
+        hipLaunchKernelGGL((k_tn_skinny_multi<8, float>), dim3(nb, m.n), dim3(256), 0, s, m);
     }
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;

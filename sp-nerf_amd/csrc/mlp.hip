@@ -1191,6 +1191,52 @@ static int32_t skinny(const Ctx& c, int64_t rows, const float* A, int lda, int M
     return reduce_slabs_multi(rr, n, s);
 }
 
+// Skinny reductions with fp32 rows batched into ONE launch (tn_skinny_multi) plus one reduction
+// launch per kReduceMulti outputs — the per-ray parameter gradients of a backward (step 7) were
+// a dozen launches of a few microseconds of work each.  Same arithmetic as skinny().
+struct SkinnyBatch {
+    const Ctx& c;
+    std::vector<SkinnyArgs> tasks;
+    std::vector<ReduceArgs> reds;
+    int64_t off = 0, off_b = 0;
+    explicit SkinnyBatch(const Ctx& cc) : c(cc) {}
+    template <typename TB>
+    int32_t add(int64_t rows, const float* A, int lda, int Ma, const TB* B, int ldb, int K, float* dst, int ld_dst,
+                int transpose, float* dst_b, float* dst_ones) {
+        SkinnyArgs k;
+        k.A = A; k.lda = lda; k.Ma = Ma; k.ldb = ldb; k.K = K; k.P = rows; k.ones = dst_ones ? 1 : 0;
+        if constexpr (std::is_same<TB, bf16>::value) k.B16 = B;
+        else k.B = B;
+        const int64_t chunks = rows > 0 ? cdiv(rows, skinny_chunk(rows)) : 0;
+        const int Mt = Ma + k.ones;
+        SPN_ARG(off + chunks * Mt * K <= c.w.sk_slab_n && off_b + chunks * Ma <= c.w.sk_slab_b_n &&
+                (int)tasks.size() < kSkinnyMulti, "skinny batch: slab capacity");
+        k.slab = c.at(c.w.sk_slab) + off;
+        k.slab_b = c.at(c.w.sk_slab_b) + off_b;
+        off += chunks * Mt * K;
+        off_b += chunks * Ma;
+        tasks.push_back(k);
+        ReduceArgs r = red(0, Ma, K, dst, ld_dst, dst_b);
+        r.slab = k.slab; r.ld_slab = K; r.slab_stride = (int64_t)Mt * K; r.splits = (int)chunks; r.N = Mt;
+        r.slab_b = k.slab_b;
+        r.transpose = transpose;
+        r.accumulate = c.acc;
+        if (dst) reds.push_back(r);
+        if (dst_ones) {
+            ReduceArgs o = r;
+            o.row0 = Ma; o.nrows = 1; o.dst = dst_ones; o.ld_dst = K; o.dst_b = nullptr; o.transpose = 0;
+            reds.push_back(o);
+        }
+        return SPNERF_OK;
+    }
+    int32_t run(hipStream_t s) {
+        SPN_TRY(tn_skinny_multi(tasks.data(), (int)tasks.size(), s));
+        for (size_t i = 0; i < reds.size(); i += kReduceMulti)
+            SPN_TRY(reduce_slabs_multi(reds.data() + i, (int)std::min<size_t>(kReduceMulti, reds.size() - i), s));
+        return SPNERF_OK;
+    }
+};
+
 // Trunk + G/Q/sun_v GEMMs of the forward (spnerf.py:323-355).  In the bf16 MLP, layer 0 stays
 // an fp32 GEMM (sin(30·x) amplifies operand rounding 30x) that writes bf16 H_1 / D_1.
 // bf16 MLP: layer 0 runs inside the fused trunk launch (reading the fp32 PE rows itself)
@@ -1519,13 +1565,17 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     }
     // from here on: dX chain on s, weight gradients on s2 (each after a fork from s)
     SPN_TRY(stream_dep(sd, s, s2));
-    // 2. narrow-head weights: reductions over points
-    SPN_TRY(skinny(c, P, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), W, 0, gp(x.sigb), nullptr, s2));
-    SPN_TRY(skinny(c, P, hpre + 4, d.HP, 1, buf(c.w.S3), H, H, gp(x.s4W), H, 0, gp(x.s4b), nullptr, s2));
-    if (mode == 0) {
-        SPN_TRY(skinny(c, P, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), H, 0, gp(x.r2b), nullptr, s2));
-        if (d.beta) SPN_TRY(skinny(c, P, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), H, 0, gp(x.b2b), nullptr, s2));
-        if (d.sem) SPN_TRY(skinny(c, P, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), H, 0, gp(x.m2b), nullptr, s2));
+    // 2. narrow-head weights: reductions over points (one launch + one reduction launch)
+    {
+        SkinnyBatch sb(c);
+        SPN_TRY(sb.add(P, hpre + 0, d.HP, 1, HL, W, W, gp(x.sigW), W, 0, gp(x.sigb), nullptr));
+        SPN_TRY(sb.add(P, hpre + 4, d.HP, 1, buf(c.w.S3), H, H, gp(x.s4W), H, 0, gp(x.s4b), nullptr));
+        if (mode == 0) {
+            SPN_TRY(sb.add(P, hpre + 1, d.HP, 3, Qb + H, d.NQ, H, gp(x.r2W), H, 0, gp(x.r2b), nullptr));
+            if (d.beta) SPN_TRY(sb.add(P, hpre + 5, d.HP, 1, Qb + 2 * H, d.NQ, H, gp(x.b2W), H, 0, gp(x.b2b), nullptr));
+            if (d.sem) SPN_TRY(sb.add(P, hpre + 6, d.HP, d.C, Gb + W, d.NG, H, gp(x.m2W), H, 0, gp(x.m2b), nullptr));
+        }
+        SPN_TRY(sb.run(s2));
     }
     // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
     {
@@ -1748,20 +1798,29 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
         }
         const float* sun = rays + 8;
         const int64_t B = n_rays;
+        SkinnyBatch sb(c);
         // sun_v_net.0 sun-direction columns: dW[n][W+j] = Σ_ray RQ[ray][n] sun[ray][j]
-        SPN_TRY(skinny(c, B, sun, rs, 3, c.at(c.w.RQ), d.NQ, H, gp(x.s1W) + W, ld(x.s1W), 1, nullptr, nullptr, s));
+        SPN_TRY(sb.add(B, sun, rs, 3, c.at(c.w.RQ), d.NQ, H, gp(x.s1W) + W, ld(x.s1W), 1, nullptr, nullptr));
         if (sky_on) {
-            SPN_TRY(skinny(c, B, sun, rs, 3, c.at(c.w.skydh), H, H, gp(x.k1W), 3, 1, nullptr, gp(x.k1b), s));
-            SPN_TRY(skinny(c, B, c.at(c.w.skyd), 4, 3, c.at(c.w.skyh), H, H, gp(x.k2W), H, 0, gp(x.k2b), nullptr, s));
+            SPN_TRY(sb.add(B, sun, rs, 3, c.at(c.w.skydh), H, H, gp(x.k1W), 3, 1, nullptr, gp(x.k1b)));
+            SPN_TRY(sb.add(B, c.at(c.w.skyd), 4, 3, c.at(c.w.skyh), H, H, gp(x.k2W), H, 0, gp(x.k2b), nullptr));
         }
-        if (d.beta && mode == 0)
-            SPN_TRY(skinny(c, B, temb, d.td, d.td, c.at(c.w.RQ) + 2 * H, d.NQ, H, gp(x.b1W) + W, ld(x.b1W), 1, nullptr,
-                           nullptr, s));
+        if (d.beta && mode == 0) {
+            if (d.td <= 8)
+                SPN_TRY(sb.add(B, temb, d.td, d.td, c.at(c.w.RQ) + 2 * H, d.NQ, H, gp(x.b1W) + W, ld(x.b1W), 1, nullptr,
+                               nullptr));
+            else
+                SPN_TRY(skinny(c, B, temb, d.td, d.td, c.at(c.w.RQ) + 2 * H, d.NQ, H, gp(x.b1W) + W, ld(x.b1W), 1,
+                               nullptr, nullptr, s));
+        }
         if (d.sem) {
-            SPN_TRY(skinny(c, B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R0), W, W, gp(x.fcW[0]) + d.K0, ld(x.fcW[0]), 1,
-                           nullptr, nullptr, s));
-            SPN_TRY(skinny(c, B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R4), W, W, gp(x.fcW[d.skip]) + W + d.K0,
-                           ld(x.fcW[d.skip]), 1, nullptr, nullptr, s));
+            SPN_TRY(sb.add(B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R0), W, W, gp(x.fcW[0]) + d.K0, ld(x.fcW[0]), 1,
+                           nullptr, nullptr));
+            SPN_TRY(sb.add(B, c.at(c.w.embr), d.sd, d.sd, c.at(c.w.R4), W, W, gp(x.fcW[d.skip]) + W + d.K0,
+                           ld(x.fcW[d.skip]), 1, nullptr, nullptr));
+        }
+        SPN_TRY(sb.run(s));
+        if (d.sem) {
             ProfScope prof("ray_terms", s, 0.0, 0.0);
             hipLaunchKernelGGL(k_class_sum, dim3((d.C + 1) * d.sd), dim3(256), 0, s, n_rays, c.at(c.w.gemb), d.sd, labels,
                                d.C, gp(x.emb), c.acc);

@@ -251,9 +251,13 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         w.skydh = take(B * H);
         w.gemb = take(B * (d.sd ? d.sd : 1));
         w.embr = take(B * (d.sd ? d.sd : 1));
-        const int64_t chunks = std::max((P + skinny_chunk(P) - 1) / skinny_chunk(P), (B + skinny_chunk(B) - 1) / skinny_chunk(B));
-        w.sk_slab = take(chunks * 9 * W);
-        w.sk_slab_b = take(chunks * 9);
+        // skinny slabs: one point reduction at a time, or the per-ray batch (≤ kSkinnyMulti tasks of
+        // ≤ 9 rows x max(W, H) columns each, mlp.hip SkinnyBatch)
+        const int64_t cP = (P + skinny_chunk(P) - 1) / skinny_chunk(P), cB = (B + skinny_chunk(B) - 1) / skinny_chunk(B);
+        w.sk_slab_n = std::max(cP * 9 * W, cB * kSkinnyMulti * 9 * W);
+        w.sk_slab_b_n = std::max(cP * 9, cB * kSkinnyMulti * 9);
+        w.sk_slab = take(w.sk_slab_n);
+        w.sk_slab_b = take(w.sk_slab_b_n);
     }
     w.total = off;
     return w;
