@@ -479,12 +479,29 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
     do {               \
     } while (0)
 #endif
-// DM: the backward dX epilogue only (C = acc · Dmul, no bias / rank-1 / sine): every epilogue
-// load is unconditional, so no branch drains the in-flight DMAs (vmcnt(0)).
+// DM: the backward dX epilogue only (C = acc · Dmul, no bias / rank-1 / sine).
 // IP: issue placement of the next K-step's DMAs, as k_gemm_tn_bf16d (option nt_bf16_ip; the
 // backward xDmul epilogue only, 2 by default: 536 -> 429 us on 524 288 x 512 x 512 in isolation,
 // within noise in the C4 step)
-template <bool DM, int IP = 0>
+// EV: the epilogue's inputs as COMPILE-TIME choices.  An epilogue load behind a runtime branch
+// (`g.Dmul ? load : 0`, `if (g.rowbias)`, the zsave option's `g.dmul_z ? cos(Z) : D`) makes hipcc
+// wait vmcnt(0) at the join — for the next tile's in-flight DMAs and every earlier store — once per
+// 32 x 64 piece (16 per tile; counted in the --save-temps assembly).  Every load of a non-generic
+// variant is unconditional:
+//   DM:  0 = Dmul holds D (bf16), 1 = Dmul holds the saved Z (fp16; option zsave): D = cos(Z);
+//   !DM: 0 = generic (runtime flags: zsave rounding, rank-1, Dmul, rowbias), 1 = bias + sine/linear
+//        columns, 2 = the same + per-ray rows (rows_per_ray % 32 == 0: a 32-row piece lies in one
+//        ray, each lane loads one column of the wave's ray row at the tile start and the piece
+//        takes its 8 values by ds_bpermute), 3 = bias + rank-1 + Dmul (no sine).
+// The bias of variants 1-3 is read from a zero row when absent: + 0.f, which the generic
+// epilogue also adds (bit-identical).
+__device__ const float kZeroRow[2048 + 8] = {};
+// a float through an explicitly GLOBAL pointer: a generic (flat) load may alias LDS, so hipcc
+// makes it wait for the in-flight LDS-DMA writes (vmcnt(0)) — which a select between a kernel
+// argument and kZeroRow otherwise compiles to
+typedef const __attribute__((address_space(1))) float* gfloat_ptr;
+__device__ __forceinline__ float ldgf(const float* p) { return *(gfloat_ptr)p; }
+template <bool DM, int IP = 0, int EV = 0>
 __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
     __shared__ __attribute__((aligned(16))) char smem[ND_STAGES * ND_STG + 8 * 4096];
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -553,6 +570,9 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
     const int st_base = (wid >> 2) * 4096;
     int st_n = 0;
 #endif
+    constexpr bool GEN = !DM && EV == 0;           // runtime epilogue flags
+    constexpr bool RBL = !DM && EV == 2;           // per-ray rows by lane loads
+    constexpr bool R1D = !DM && EV == 3;           // rank-1 + Dmul
     int gs = 0;  // flat step counter: step gs sits in stage gs % ND_STAGES
     issue(0);
     issue(1);
@@ -561,6 +581,30 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
         const int bm = (t / nN) * 256, bn = (t % nN) * 256;
         const int tn = t + G;
         const bool more = tn < ntiles;
+        // variants 1-3: the tile's bias (and rank-1 / per-ray row) values load before its K-loop,
+        // so no epilogue wait covers the next tile's DMAs
+        float bias8[8], r1v8[8], rbl[4];
+        {
+            const int cq0 = (opaque(lane) & 7) * 8;
+            const int colc0 = min(bn + wc * 64 + cq0, g.N - 8);
+            if constexpr (!DM && !GEN) {
+                const float* bp = g.bias ? g.bias : kZeroRow;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bias8[e] = ldgf(bp + colc0 + e);
+            }
+            if constexpr (R1D) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) r1v8[e] = ldgf(g.r1_v + colc0 + e);
+            }
+            if constexpr (RBL) {
+                const int cl = min(bn + wc * 64 + opaque(lane), g.N - 1);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int ray = min(bm + wr * 128 + i * 32, g.M - 1) / g.rows_per_ray;
+                    rbl[i] = ldgf(g.rowbias + (int64_t)ray * g.ld_rb + cl);
+                }
+            }
+        }
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -608,9 +652,15 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                 if constexpr (DM) {
                     dm[q4] = ldg16(g.Dmul + (int64_t)row * g.ld_dmul + colc);
                     r1a[q4] = 0.f;
-                } else {
+                } else if constexpr (R1D) {
+                    dm[q4] = ldg16(g.Dmul + (int64_t)row * g.ld_dmul + colc);
+                    r1a[q4] = ldgf(g.r1_a + (int64_t)row * g.r1_lda);
+                } else if constexpr (GEN) {
                     dm[q4] = g.Dmul ? ldg16(g.Dmul + (int64_t)row * g.ld_dmul + colc) : u32x4{0u, 0u, 0u, 0u};
                     r1a[q4] = g.r1_a ? g.r1_a[(int64_t)row * g.r1_lda] : 0.f;
+                } else {
+                    dm[q4] = u32x4{0u, 0u, 0u, 0u};
+                    r1a[q4] = 0.f;
                 }
             }
         };
@@ -620,11 +670,12 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
         float r1a[NB][4];
 #pragma unroll
         for (int p = 0; p + 1 < NB; ++p) dload(dm[p], r1a[p], p);
-        float bias8[8], r1v8[8];
+        if constexpr (DM || GEN) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            bias8[e] = !DM && g.bias ? g.bias[colc + e] : 0.f;
-            r1v8[e] = !DM && g.r1_a ? g.r1_v[colc + e] : 0.f;
+            for (int e = 0; e < 8; ++e) {
+                bias8[e] = !DM && g.bias ? g.bias[colc + e] : 0.f;
+                r1v8[e] = !DM && g.r1_a ? g.r1_v[colc + e] : 0.f;
+            }
         }
         // every wave is done reading stage (gs - 1) % 4 before waves 4..7 stage into it
         ND_STAMP(5);
@@ -632,7 +683,14 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
         ND_STAMP(6);
         float* stage = wid < 4 ? reinterpret_cast<float*>(smem + ND_STAGES * ND_STG + wid * 8192)
                                : reinterpret_cast<float*>(smem + ((gs + 3) % ND_STAGES) * ND_STG + (wid - 4) * 8192);
-        const bool sine_cols = !DM && g.act == 1 && col >= g.n_lin;  // n_lin is a multiple of 8
+        const bool sine_cols = !DM && !R1D && g.act == 1 && col >= g.n_lin;  // n_lin is a multiple of 8
+        // store descriptors over the tile's rows of C and (sine layers) Dout
+        const int trows = min(256, g.M - bm);
+        const __amdgpu_buffer_rsrc_t rsC =
+            __builtin_amdgcn_make_buffer_rsrc(g.C + (int64_t)bm * g.ldc, 0, trows * g.ldc * 2, 0x00020000);
+        const bool dout_on = !DM && g.Dout && g.act == 1;
+        const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
+            dout_on ? g.Dout + (int64_t)bm * g.ld_dout : g.C, 0, dout_on ? trows * g.ld_dout * 2 : 0, 0x00020000);
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             if (i + NB - 1 < MI) dload(dm[(i + NB - 1) % NB], r1a[(i + NB - 1) % NB], i + NB - 1);
@@ -645,6 +703,12 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                     stage[rr * 64 + ((((cc >> 2) ^ (rr & 1)) << 2) | (cc & 3))] = acc[i][j][r];
                 }
             lds_order();
+            // variant 2: the piece's per-ray row (one ray per 32-row piece) from the lanes holding it
+            float rbv[8];
+            if constexpr (RBL) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) rbv[e] = __shfl(rbl[i], cq + e);
+            }
             u32x4 oc[4], od[4];
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4) {
@@ -658,12 +722,17 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                     v[e] = lo[e] + bias8[e];
                     v[e + 4] = hi[e] + bias8[e + 4];
                 }
-                if (!DM && g.rowbias) {
-                    const float* rb = g.rowbias + (int64_t)(min(row, g.M - 1) / g.rows_per_ray) * g.ld_rb + colc;
+                if constexpr (RBL) {
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += rb[e];
+                    for (int e = 0; e < 8; ++e) v[e] += rbv[e];
+                } else if constexpr (GEN) {
+                    if (g.rowbias) {
+                        const float* rb = g.rowbias + (int64_t)(min(row, g.M - 1) / g.rows_per_ray) * g.ld_rb + colc;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] += rb[e];
+                    }
                 }
-                if (!DM && g.r1_a) {
+                if (R1D || (GEN && g.r1_a)) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[e] += r1a[i % NB][q4] * r1v8[e];
                 }
@@ -671,18 +740,18 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         float sn, cs;
-                        const float z = g.zround ? zr16(v[e]) : v[e];
+                        const float z = (GEN && g.zround) ? zr16(v[e]) : v[e];
                         fast_sincos(g.w0 * z, &sn, &cs);
                         v[e] = sn;
-                        d[e] = g.dout_z ? z : g.w0 * cs;
+                        d[e] = (GEN && g.dout_z) ? z : g.w0 * cs;
                     }
                 } else {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) d[e] = 1.f;
                 }
-                if (DM || g.Dmul) {
+                if (DM || R1D || (GEN && g.Dmul)) {
                     float m[8];
-                    if (g.dmul_z) {  // Dmul holds the saved Z (fp16): D = cos(Z)
+                    if ((DM && EV == 1) || (GEN && g.dmul_z)) {  // Dmul holds the saved Z (fp16): D = cos(Z)
                         unpack8_f16(dm[i % NB][q4], m);
 #pragma unroll
                         for (int e = 0; e < 8; ++e) m[e] = fast_cos(m[e]);
@@ -693,18 +762,23 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                     for (int e = 0; e < 8; ++e) v[e] *= m[e];
                 }
                 oc[q4] = pack8(v);
-                od[q4] = g.dout_z ? pack8_f16(d) : pack8(d);
+                od[q4] = (GEN && g.dout_z) ? pack8_f16(d) : pack8(d);
                 // materialise the piece's results here: hipcc otherwise sinks the arithmetic
                 // (and the Dmul waits, as vmcnt(0)) into the guarded stores below
                 asm volatile("" : "+v"(oc[q4]));
                 if constexpr (!DM) asm volatile("" : "+v"(od[q4]));
             }
+            // unconditional stores through the tile's buffer descriptors: rows past M fall outside
+            // the descriptor's range and invalid lanes get an out-of-range offset, so the hardware
+            // drops them — a branch around the stores would make every later load wait vmcnt(0)
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4) {
-                const int row = rbase + i * 32 + 8 * q4;
-                if (row < g.M && colok) {
-                    *reinterpret_cast<u32x4*>(g.C + (int64_t)row * g.ldc + col) = oc[q4];
-                    if (!DM && g.Dout && sine_cols) *reinterpret_cast<u32x4*>(g.Dout + (int64_t)row * g.ld_dout + col) = od[q4];
+                const int lr = wr * 128 + erow + i * 32 + 8 * q4;   // row within the tile
+                const uint32_t oc_off = colok ? (uint32_t)(((int64_t)lr * g.ldc + col) * 2) : 0x7FFFFFF0u;
+                __builtin_amdgcn_raw_buffer_store_b128(oc[q4], rsC, oc_off, 0, 0);
+                if constexpr (!DM && !R1D) {
+                    const uint32_t od_off = (colok && sine_cols) ? (uint32_t)(((int64_t)lr * g.ld_dout + col) * 2) : 0x7FFFFFF0u;
+                    __builtin_amdgcn_raw_buffer_store_b128(od[q4], rsD, od_off, 0, 0);
                 }
             }
             ND_STAMP(8);
@@ -1219,6 +1293,7 @@ int g_nt16_variant = 8;
 int g_nt16_ip = 2;  // DMA NT / TN: where a K-step issues the next step's DMAs (0 before its MFMAs, 1 after, 2 between the k-halves)
 int g_tn16_ip = 2;
 int g_nt16_ip_gen = 2;  // the same for the general (bias / sine / rank-1) epilogue instances
+int g_nt16_epi = 1;     // option "nt_bf16_epi": 1 = compile-time epilogue variants of the DMA NT, 0 = the generic one
 int g_tn16_variant = 3;
 
 static bool tn_wide(int N, int K, int variant) {
@@ -1257,11 +1332,45 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     if (v == 8) {
         const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
         const int ip = (a.dbg & 64) ? 2 : (a.dbg & 32) ? 1 : g_nt16_ip;
-        if (dm && ip == 2) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
-        else if (dm && ip == 1) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
-        else if (dm) hipLaunchKernelGGL(k_gemm_nt_bf16d<true>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
-        else if (g_nt16_ip_gen == 2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
-        else hipLaunchKernelGGL(k_gemm_nt_bf16d<false>, dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        const dim3 grid(std::min(nt, 256)), block(512);
+        if (dm) {
+            const bool z = a.dmul_z != 0;   // zsave: Dmul holds Z
+            if (ip == 2) {
+                if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 1>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 0>), grid, block, 0, s, a, nt);
+            } else if (ip == 1) {
+                if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1, 1>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1, 0>), grid, block, 0, s, a, nt);
+            } else {
+                if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 0, 1>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 0, 0>), grid, block, 0, s, a, nt);
+            }
+        } else {
+            // the epilogue's inputs as a compile-time variant (see k_gemm_nt_bf16d); option
+            // nt_bf16_epi 0 forces the generic one
+            const bool zs = a.zround || a.dout_z || a.dmul_z;
+            const bool bias_ok = a.bias || a.N <= 2048;   // the zero row covers the columns
+            int ev = 0;
+            if (!zs && bias_ok && g_nt16_epi) {
+                if (!a.Dmul && !a.r1_a && !a.rowbias) ev = 1;
+                else if (!a.Dmul && !a.r1_a && a.rowbias && a.rows_per_ray % 32 == 0) ev = 2;
+                else if (a.Dmul && a.r1_a && !a.rowbias && a.act == 0 && !a.Dout) ev = 3;
+            }
+            const bool ip2 = g_nt16_ip_gen == 2;
+            if (ev == 1) {
+                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 1>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 1>), grid, block, 0, s, a, nt);
+            } else if (ev == 2) {
+                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 2>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 2>), grid, block, 0, s, a, nt);
+            } else if (ev == 3) {
+                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 3>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 3>), grid, block, 0, s, a, nt);
+            } else {
+                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 0>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 0>), grid, block, 0, s, a, nt);
+            }
+        }
         SPN_HIP(hipGetLastError());
         return SPNERF_OK;
     }

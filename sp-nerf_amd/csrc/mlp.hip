@@ -1852,6 +1852,7 @@ static int* option_slot(const char* name) {
     if (n == "nt_bf16_ip") return &g_nt16_ip;
     if (n == "tn_bf16_ip") return &g_tn16_ip;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
+    if (n == "nt_bf16_epi") return &g_nt16_epi;
     if (n == "tn_bf16_variant") return &g_tn16_variant;
     if (n == "heads_variant") return &g_heads_variant;
     if (n == "l0_split") return &g_l0_split;

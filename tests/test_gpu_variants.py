@@ -130,3 +130,21 @@ def test_bf16_fused_backward_bitwise_equal(n, ns):
     for k in g0:
         assert torch.isfinite(g1[k]).all(), k
         assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("opts,n,ns", [({"nt_bf16_epi": 0}, 300, 64), ({"nt_bf16_epi": 0}, 301, 40),
+                                       ({"nt_bf16_variant": 5}, 300, 64)])
+def test_bf16_nt_epilogue_variants_bitwise_equal(opts, n, ns):
+    """The DMA NT GEMM's compile-time epilogue variants (bias + sine; + per-ray rows read once per
+    tile and spread by ds_bpermute; rank-1 + Dmul; stores through buffer descriptors) against the
+    generic runtime-flag epilogue (nt_bf16_epi 0) and the register-staged kernel (nt_bf16_variant
+    5): same arithmetic, same k order — renders and gradients bit for bit.  40 samples per ray (80
+    after the guided pass) is not a multiple of 32 rows: the per-ray-row variant falls back."""
+    r0, g0 = _render_bf16({}, n=n, ns=ns)
+    r1, g1 = _render_bf16(opts, n=n, ns=ns)
+    for k in r0:
+        assert torch.isfinite(r0[k]).all(), k
+        assert torch.equal(r0[k], r1[k]), (opts, k)
+    assert sorted(g0) == sorted(g1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), (opts, k)
