@@ -753,31 +753,37 @@ def run_train(a, config, rank, world, dev, secondary=False):
     # The gradient all-reduce (N > 1): by default in buckets (dp.GradBuckets), each issued on a
     # communication stream behind the backward mark after which its gradients are final, so the
     # collectives overlap the rest of the backward; --flat-allreduce = one all-reduce after it.
-    # allreduce_ms_per_step = the EXPOSED part: HIP events on the compute stream from the end of
-    # the backward to the moment every bucket has landed
+    # With RCCL the buckets are captured INTO the step's HIP graph (the marks are the graph's own
+    # edges); if that capture is refused, or with gloo, the graph holds the backward only and the
+    # buckets follow each replay.  allreduce_ms_per_step = the EXPOSED part: HIP events on the
+    # compute stream from the end of the backward to the moment every bucket has landed (not
+    # separable when the all-reduce is inside the graph: null then)
     buckets = dp.GradBuckets(model, world) if (world > 1 and not a.flat_allreduce) else None
     if buckets is not None:
         buckets.arm(True)
     ar_events = []
     ar_timing = [False]
+    in_graph = [False]   # the all-reduce is part of the captured graph
 
-    def reduce_grads():
+    def reduce_grads(overlap=True):
         if buckets is not None:
             flat = model._flat_grad
-            buckets.launch(flat)
+            buckets.launch(flat, overlap=overlap)
             buckets.finish(flat)
         else:
             dp.allreduce_grads(params, world)   # one RCCL all-reduce of the flat gradient
 
-    def finish():
-        if world > 1 and ar_timing[0]:
+    def finish(replayed=False):
+        if in_graph[0] and replayed:
+            pass                                # the graph reduced the gradients
+        elif world > 1 and ar_timing[0]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            reduce_grads()
+            reduce_grads(overlap=not replayed)
             e1.record()
             ar_events.append((e0, e1))
         else:
-            reduce_grads()
+            reduce_grads(overlap=not replayed)
         opt.step()
         args.noise_std *= 0.9               # main.py:155
 
@@ -803,21 +809,37 @@ def run_train(a, config, rank, world, dev, secondary=False):
         opt.zero_grad(set_to_none=True)
         model.invalidate_packed()           # the capture must contain the weight re-pack
         load_batch()
-        try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                static_loss = fwd_bwd()
-        except Exception as e:  # capture refused: run the same work eagerly, and say so
-            print(f"bench: HIP graph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
-            graph = None
-            a.graph = False
-            torch.cuda.synchronize()
+        if buckets is not None and dist.get_backend() == "nccl":
+            try:   # render + loss + backward + the overlapped bucket all-reduces in one graph
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    static_loss = fwd_bwd()
+                    buckets.launch(model._flat_grad, overlap=True)
+                    buckets.finish(model._flat_grad)
+                in_graph[0] = True
+            except Exception as e:
+                print(f"bench: capturing the all-reduce refused ({type(e).__name__}: {e}); it follows each replay",
+                      file=sys.stderr)
+                graph = None
+                buckets.works = []
+                torch.cuda.synchronize()
+                opt.zero_grad(set_to_none=True)
+        if graph is None:
+            try:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    static_loss = fwd_bwd()
+            except Exception as e:  # capture refused: run the same work eagerly, and say so
+                print(f"bench: HIP graph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
+                graph = None
+                a.graph = False
+                torch.cuda.synchronize()
 
     if graph is not None:
         def step():
             load_batch()
             graph.replay()
-            finish()
+            finish(replayed=True)
             return static_loss
     else:
         step = eager_step
@@ -883,7 +905,11 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "mlp_mfma_utilisation": gemm_totals(prof_steps),
         "allreduce_ms_per_step": allreduce_ms,
         "allreduce": (None if world == 1 else
-                      f"{len(buckets.buckets)} buckets issued behind the backward's gradient marks (exposed ms above)"
+                      f"{len(buckets.buckets)} buckets behind the backward's gradient marks, inside the HIP graph"
+                      if in_graph[0] else
+                      f"{len(buckets.buckets)} buckets after each graph replay (exposed ms above)"
+                      if (buckets is not None and a.graph) else
+                      f"{len(buckets.buckets)} buckets behind the backward's gradient marks (exposed ms above)"
                       if buckets is not None else "one flat all-reduce after the backward"),
         "kernels": kernels,
         "final_loss": final_loss,

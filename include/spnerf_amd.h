@@ -239,11 +239,11 @@ int32_t spnerf_adam_step(int32_t n, void* const* params, const void* const* grad
  *      1 + (layers-1-i) after trunk layer i's, mark layers+1 at its end (per-ray parameters).
  *      spnerf_grad_marks fills mark_of_param[idx] (canonical order) with the mark after which
  *      parameter idx receives no more writes from a main or a solar-pass backward and returns
- *      n_marks.  While armed, every spnerf_mlp_backward records the library's mark events (one
- *      set per device) on its stream — as external event nodes when the stream is being captured
- *      into a HIP graph, so each replay records them — and spnerf_grad_mark_wait makes `stream`
- *      wait for the latest record of `mark`: an all-reduce issued behind it overlaps the rest of
- *      the backward. */
+ *      n_marks.  While armed, every spnerf_mlp_backward (and spnerf_mlp_trunk_wgrad) records the
+ *      library's mark events (one set per device) on its stream, and spnerf_grad_mark_wait makes
+ *      `stream` wait for the latest record of `mark`: an all-reduce issued behind it overlaps the
+ *      rest of the backward.  Under HIP-graph capture a mark is a dependency edge of the graph
+ *      being captured, so the waiting stream's work must be captured into the same graph. */
 int32_t spnerf_grad_marks(const spnerf_model_cfg* cfg, int32_t* mark_of_param, int32_t n_params);
 int32_t spnerf_grad_marks_arm(int32_t on);
 int32_t spnerf_grad_mark_wait(int32_t mark, void* stream);

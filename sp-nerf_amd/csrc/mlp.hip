@@ -329,14 +329,16 @@ Side* side_stream() {
 // Gradient readiness marks (spnerf_grad_marks): when armed, a backward records mark k's event
 // on the stream that finishes that group of weight gradients — mark 0 after the output heads',
 // 1 + (L-1-i) after trunk layer i's, L+1 at the end (per-ray parameters) — so that a data-parallel
-// caller can all-reduce each group while the rest of the backward runs.  One event set per device;
-// a stream being captured into a HIP graph gets external event-record nodes (a replay records them).
+// caller can all-reduce each group while the rest of the backward runs.  One event set per device.
+// Inside a HIP-graph capture the marks are the graph's own dependency edges: the all-reduces must
+// then be captured into the same graph (dp.GradBuckets).
 struct Marks {
     hipEvent_t ev[64] = {};
     bool ok = false;
 };
 Marks g_marks[64];
 int g_marks_armed = 0;
+int g_marks_flags = hipEventDisableTiming;  // option "grad_marks_flags": hipEventCreateWithFlags flags (before the first arm)
 
 static Marks* marks_of_device() {
     int dev = 0;
@@ -344,7 +346,7 @@ static Marks* marks_of_device() {
     Marks& m = g_marks[dev];
     if (!m.ok) {
         for (auto& e : m.ev)
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+            if (hipEventCreateWithFlags(&e, (unsigned)g_marks_flags) != hipSuccess) return nullptr;
         m.ok = true;
     }
     return &m;
@@ -354,10 +356,10 @@ static int32_t grad_mark(int k, hipStream_t s) {
     if (!g_marks_armed) return SPNERF_OK;
     Marks* m = marks_of_device();
     SPN_ARG(m && k >= 0 && k < 64, "grad_mark: no mark events");
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    SPN_HIP(hipStreamIsCapturing(s, &st));
-    if (st == hipStreamCaptureStatusActive) SPN_HIP(hipEventRecordWithFlags(m->ev[k], s, hipEventRecordExternal));
-    else SPN_HIP(hipEventRecord(m->ev[k], s));
+    // a plain record: under stream capture it becomes a dependency edge of the graph being
+    // captured (a wait on it from another stream of the same capture joins that stream to the
+    // graph); this HIP runtime refuses external event-record nodes (hipEventRecordExternal)
+    SPN_HIP(hipEventRecord(m->ev[k], s));
     return SPNERF_OK;
 }
 
@@ -1853,6 +1855,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_ip") return &g_tn16_ip;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;
+    if (n == "grad_marks_flags") return &g_marks_flags;
     if (n == "tn_bf16_variant") return &g_tn16_variant;
     if (n == "heads_variant") return &g_heads_variant;
     if (n == "l0_split") return &g_l0_split;

@@ -109,8 +109,9 @@ class GradBuckets:
     is final at mark(p).  ``launch`` makes a communication stream wait for each bucket's mark and
     issues its all_reduce(SUM) there (RCCL runs it on its own stream behind that wait); ``finish``
     makes the current stream wait for every bucket, then divides by the world size.  ``arm``
-    must precede the backward (and a HIP graph capture of it: the marks are then captured as
-    external event nodes that every replay records)."""
+    must precede the backward.  Under HIP-graph capture the marks are edges of the graph being
+    captured, so the overlapped all-reduces must be captured with the backward (RCCL); a graph
+    that holds only the backward is followed by ``launch(flat, overlap=False)``."""
 
     def __init__(self, model, world: int, group=None, layout=None):
         """``layout`` = (numels, marks) instead of the model's (host tests of the bucketing on
@@ -132,28 +133,36 @@ class GradBuckets:
     def arm(self, on: bool = True) -> None:
         self._lib.grad_marks_arm(on)
 
-    def launch(self, flat: torch.Tensor) -> None:
-        if self.world <= 1:
+    def launch(self, flat: torch.Tensor, overlap: bool = True, force: bool = False) -> None:
+        """Issue every bucket's all-reduce.  ``overlap``: behind its backward mark — in the same
+        eager step or the same HIP-graph capture as the backward; otherwise (a graph replay's
+        backward, whose marks are that graph's internal edges) behind the whole compute stream.
+        ``force``: also with one rank (a capture rehearsal of the collective on one GPU)."""
+        if self.world <= 1 and not force:
             return
         on_gpu = flat.is_cuda
         if on_gpu and self.stream is None:
             self.stream = torch.cuda.Stream(device=flat.device)
+        if on_gpu and not overlap:
+            self.stream.wait_stream(torch.cuda.current_stream(flat.device))
         for mark, lo, hi in self.buckets:
             if not on_gpu:
                 self.works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
                 continue
-            self._lib.grad_mark_wait(mark, self.stream)
+            if overlap:
+                self._lib.grad_mark_wait(mark, self.stream)
             with torch.cuda.stream(self.stream):
                 self.works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                                   async_op=True))
 
-    def finish(self, flat: torch.Tensor) -> None:
-        if self.world <= 1:
+    def finish(self, flat: torch.Tensor, force: bool = False) -> None:
+        if self.world <= 1 and not force:
             return
         for w in self.works:
             w.wait()
         self.works = []
-        flat.div_(self.world)
+        if self.world > 1:
+            flat.div_(self.world)
 
 
 def _shared_flat(grads):

@@ -194,7 +194,8 @@ def bucket_runs(rank, world):
     """One C3-flags training step of this rank's slice, three ways, same draws (the Philox
     step is reset before each): eager + the flat all-reduce; eager + dp.GradBuckets (each
     bucket's all-reduce issued behind its backward mark, overlapping the rest of the backward);
-    a HIP-graph replay of the step + GradBuckets (marks captured as external event nodes).
+    a HIP-graph replay of the step + GradBuckets behind the replay (gloo cannot be captured; with
+    RCCL bench.py captures the overlapped buckets into the graph, tools/rccl_capture_probe.py).
     Returns the three reduced flat gradients."""
     import types
     import spnerf_amd
@@ -216,10 +217,11 @@ def bucket_runs(rank, world):
     src = spnerf_amd.PhiloxRandom(seed=11, ray_offset=rank * b)
     buckets = dp.GradBuckets(model, world)
 
-    def fwd_bwd():
+    def fwd_bwd():   # graph-capturable: no host sync (the clamp ray by index_select)
         res = spnerf_amd.render_rays({"coarse": model}, args, R.rays[idx], None, semantics=R.sems[idx], mode="train",
                                      valid_depth=R.valid_depth[idx], target_depths=R.depths[idx],
-                                     target_std=R.depth_std[idx], clamp_near_far=R.rays[gidx[0], 6:8])
+                                     target_std=R.depth_std[idx],
+                                     clamp_near_far=R.rays.index_select(0, gidx[:1])[0, 6:8])
         loss, _ = floss(res, R.rgbs[idx], R.depths[idx], R.valid_depth[idx], R.depth_std[idx], R.sems[idx],
                         labels_global=R.sems[gidx], world=world)
         loss.backward()
@@ -252,7 +254,7 @@ def bucket_runs(rank, world):
         flat = model._flat_grad
         src._state[1].fill_(-1)
         graph.replay()
-        buckets.launch(flat)
+        buckets.launch(flat, overlap=False)   # the replay's marks are the graph's own edges
         buckets.finish(flat)
         out.append(flat.cpu().numpy().copy())
         buckets.arm(False)
@@ -276,9 +278,9 @@ def _bucket_worker(rank, world, port, outdir):
 
 def test_bucketed_allreduce_overlapping_the_backward_equals_flat(tmp_path):
     """dp.GradBuckets on the HIP path: the bucket all-reduces wait only for their backward marks
-    (spnerf_grad_marks) and run while the rest of the backward does — eager and inside a HIP graph
-    replay — and give exactly the flat all-reduce's gradient (any bucket read before its last
-    write would differ: the backward is deterministic)."""
+    (spnerf_grad_marks) and run while the rest of the backward does, and give exactly the flat
+    all-reduce's gradient (any bucket read before its last write would differ: the backward is
+    deterministic); after a graph replay they give it too."""
     world = 2
     mp.spawn(_bucket_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     parts = [dict(np.load(tmp_path / f"bucket{r}.npz")) for r in range(world)]
