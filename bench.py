@@ -316,7 +316,7 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
     every = max(1, steps // checkpoints)
     curves = {a: [] for a in arms}
     loss_curve = {a: [] for a in arms}
-    grad_err = []
+    grad_err, grad_err_top = [], []
     t0 = time.perf_counter()
     for step in range(steps):
         idx = torch.as_tensor(rng.choice(pool, batch, replace=False), device=dev)
@@ -342,6 +342,15 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
             if check and a == "fp32":
                 g32 = m._flat_grad
                 grad_err.append((step, float(torch.linalg.norm(g16 - g32) / torch.linalg.norm(g32))))
+                # where it is: the parameters with the largest share of the error
+                off, parts = 0, []
+                for name, p in m.named_parameters():
+                    n = p.numel()
+                    d = float(torch.linalg.norm(g16[off:off + n] - g32[off:off + n]))
+                    parts.append((d, name, float(torch.linalg.norm(g32[off:off + n]))))
+                    off += n
+                parts.sort(reverse=True)
+                grad_err_top.append((step, [(nm, round(d, 6), round(r, 6)) for d, nm, r in parts[:3]]))
             opts[a].step()
             if check:
                 loss_curve[a].append((step, float(loss.detach())))
@@ -365,6 +374,7 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
             "tail_mean_control_delta_db": tail["fp32_control"] - tail["fp32"],
             "bf16_inference_at_fp32_trained": {"psnr_db": p16, "delta_db": p16 - final["fp32"]},
             "grad_rel_err": grad_err, "max_grad_rel_err": max(e for _, e in grad_err),
+            "grad_err_top_params": grad_err_top,
             "psnr_curve": curves, "loss_curve": loss_curve,
             "steps": steps, "batch_rays": batch, "held_out_rays": n_eval, "train_seconds": train_s,
             "targets": R.rgb_source,

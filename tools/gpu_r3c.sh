@@ -10,3 +10,4 @@ for o in "" "--no-defer-wgrad" "--option nt_bf16_epi=0" "" "--no-defer-wgrad" "-
 r=$(timeout -k 10 200 python bench.py --config c4 --global-batch $gb --steps 20 --warmup 5 --no-cpu-baseline --no-secondary $o 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernels', {}); print(round(d['ms_per_step'],3), {c: round(v['ms_per_step'],3) for c, v in k.items() if v['ms_per_step'] > 0.1})")
 echo "c4@$gb [$o] $r" >> gpurun_out/r3c_defer.log
 done; done
+timeout -k 10 300 python bench.py --gpus 2 --share-device --steps 10 --warmup 3 --no-secondary > gpurun_out/r3d_share2.json 2> gpurun_out/r3d_share2.err
