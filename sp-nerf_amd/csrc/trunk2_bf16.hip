@@ -39,15 +39,16 @@ namespace spn {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// 0 = the one-workgroup kernels (default); 1 = this kernel for the saving (training) launches;
-// 2 = for every launch; 3 = for the inference (non-saving) launches only.  Measured on MI355X (tools/gpu_t2ab.sh, tools/pmc_trunk2.sh,
+// 0 = the one-workgroup kernels; 1 = this kernel for the saving (training) launches; 2 = for
+// every launch; 3 = for the inference (non-saving) launches only — the default: C5 23.41 / 23.42
+// against 23.33 / 23.25 ms per step, trunk 16.13 -> 15.92 ms (pairs in one call, 128-point tiles).  Measured on MI355X (tools/gpu_t2ab.sh, tools/pmc_trunk2.sh,
 // training forward at 524 288 points): one-workgroup k_trunk_bf16<64> 3.05 ms, this kernel
 // 3.08 ms (64-point tiles, two workgroups per CU) and 3.38 ms (128-point tiles); without any HBM
 // copy-out it is the faster one (1.84–1.96 against 2.45 ms), but PMC shows the waves waiting on
 // s_waitcnt 51–65 % of their cycles (one-workgroup kernel 37 %): vmcnt retires loads and stores
 // in order, so the weight refills issued after an epilogue's D stores wait for those stores'
-// acknowledgements.  Bit-identical (tests/test_gpu_trunk.py); kept as an option.
-int g_trunk2 = 0;
+// acknowledgements.  Bit-identical (tests/test_gpu_trunk.py).
+int g_trunk2 = 3;
 
 namespace {
 constexpr int TW = 512;
