@@ -50,7 +50,7 @@ HBM_PEAK_GBS = 8000.0
 GEMM_CLASSES = {
     "gemm_nt_f32": ("k_gemm_nt_w<256,128,2,2,3> (fp32 MFMA NT GEMM, persistent 256x128 tiles, LDS-DMA)", FP32_MFMA_PEAK_TFLOPS),
     "gemm_tn_f32": ("k_gemm_tn<3> (fp32 MFMA weight-gradient GEMM)", FP32_MFMA_PEAK_TFLOPS),
-    "gemm_nt_bf16d": ("k_gemm_nt_bf16d<false,2> (bf16 MFMA NT GEMM, 256x256 persistent tiles, LDS-DMA ring; "
+    "gemm_nt_bf16d": ("k_gemm_nt_bf16d<false,2,EV> (bf16 MFMA NT GEMM, LDS-DMA, bias / sine / per-ray-row / rank-1 epilogues)"
                       "bias / sin / D epilogue: head layers and layer 0)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_nt_bf16d_dmul": ("k_gemm_nt_bf16d<true,2> (bf16 MFMA dX GEMM with the x D epilogue)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_nt_bf16w": ("k_gemm_nt_bf16w (bf16 MFMA NT GEMM, register-staged)", BF16_MFMA_PEAK_TFLOPS),
@@ -58,12 +58,13 @@ GEMM_CLASSES = {
     "gemm_tn_bf16d": ("k_gemm_tn_bf16d<2> (bf16 MFMA weight-gradient GEMM, 256x256 tiles, LDS-DMA)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16w": ("k_gemm_tn_bf16w (bf16 MFMA weight-gradient GEMM, 256x256 register-staged)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA weight-gradient GEMM, 128x128 tiles)", BF16_MFMA_PEAK_TFLOPS),
-    "trunk_bf16": ("k_trunk_bf16<128> (fused bf16 trunk, inference tiles, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
+    "trunk_bf16": ("k_trunk2_bf16<128> (fused bf16 trunk, inference: 128-point LDS-resident tiles, option trunk2 3; "
+                   "k_trunk_bf16<128> with trunk2 0)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bf16_train": ("k_trunk_bf16<64> (fused bf16 trunk, training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bwd_bf16": ("k_trunk_bwd_bf16 (fused bf16 backward dX chain, LDS-resident dZ)", BF16_MFMA_PEAK_TFLOPS),
     "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS)}
-HBM_CLASSES = {"tn_skinny": "k_tn_skinny (narrow-head / per-ray weight gradients)",
-               "reduce_slabs": "k_reduce_slabs (fixed-order weight-gradient split reduction)",
+HBM_CLASSES = {"tn_skinny": "k_tn_skinny_multi (narrow-head / per-ray weight gradients, one launch per backward step)",
+               "reduce_slabs": "k_reduce_slabs(_multi) (fixed-order weight-gradient split reductions)",
                "encode": "k_encode (positional encoding)", "heads_fwd": "k_heads_fwd_v (narrow heads)",
                "heads_bwd": "k_heads_bwd_v (narrow-head backward)", "composite_fwd": "k_composite_fwd",
                "composite_bwd": "k_composite_bwd", "sample_guided": "k_guided", "render_loss": "k_loss_*",
