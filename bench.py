@@ -50,8 +50,9 @@ HBM_PEAK_GBS = 8000.0
 GEMM_CLASSES = {
     "gemm_nt_f32": ("k_gemm_nt_w<256,128,2,2,3> (fp32 MFMA NT GEMM, persistent 256x128 tiles, LDS-DMA)", FP32_MFMA_PEAK_TFLOPS),
     "gemm_tn_f32": ("k_gemm_tn<3> (fp32 MFMA weight-gradient GEMM)", FP32_MFMA_PEAK_TFLOPS),
-    "gemm_nt_bf16d": ("k_gemm_nt_bf16d<false,2,EV> (bf16 MFMA NT GEMM, LDS-DMA, bias / sine / per-ray-row / rank-1 epilogues)"
-                      "bias / sin / D epilogue: head layers and layer 0)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_nt_bf16d": ("k_gemm_nt_bf16d<false,2,EV> (bf16 MFMA NT GEMM, 256x256 persistent tiles, LDS-DMA ring; "
+                      "bias / sine / per-ray-row / rank-1 epilogue variants: head layers, layer 0, heads' dX)",
+                      BF16_MFMA_PEAK_TFLOPS),
     "gemm_nt_bf16d_dmul": ("k_gemm_nt_bf16d<true,2> (bf16 MFMA dX GEMM with the x D epilogue)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_nt_bf16w": ("k_gemm_nt_bf16w (bf16 MFMA NT GEMM, register-staged)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_nt_bf16": ("k_gemm_nt_bf16 (bf16 MFMA NT GEMM, 128x128 tiles)", BF16_MFMA_PEAK_TFLOPS),
