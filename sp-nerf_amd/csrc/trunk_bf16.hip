@@ -33,6 +33,10 @@
 
 #include "trunk.h"
 
+#ifndef SPN_TRUNK_BUFSTORE
+#define SPN_TRUNK_BUFSTORE 1  // copy-outs through buffer descriptors (0: guarded stores, A/B builds)
+#endif
+
 namespace spn {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -103,10 +107,15 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             ring[d][1] = ldg16(src + d * kTrunkKStride + 512);
         }
     };
-    // copy chunks [q0, q0 + n) (per thread) of an image to HBM rows p0 + row
+    // copy chunks [q0, q0 + n) (per thread) of an image to HBM rows p0 + row.  The stores go
+    // through a buffer descriptor over the tile's valid rows (rows past P are dropped by the
+    // hardware): a branch around them made every later wait on an older load (the weight ring's
+    // refills) hipcc's conservative count, i.e. a wait for these stores as well
     auto copy_out = [&](const char* img, bf16* dst, int64_t p0, int q0, auto kn) {
         constexpr int n = decltype(kn)::value;
         const int ct = opaque(tid);
+        const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + p0 * TW, 0, rows * TW * 2, 0x00020000);
         u32x4 v[n];
 #pragma unroll
         for (int q = 0; q < n; ++q) {
@@ -116,11 +125,17 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 #pragma unroll
         for (int q = 0; q < n; ++q) {
             const int c = ct + 512 * (q0 + q);
+#if SPN_TRUNK_BUFSTORE
+            const int off = ((c >> 6) * TW + (c & 63) * 8) * 2;
+            if (g.nt) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // block-uniform: glc slc
+            else __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 0);
+#else  // A/B build: the guarded stores
             if (p0 + (c >> 6) < g.P) {
                 u32x4* o = reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8);
-                if (g.nt) __builtin_nontemporal_store(v[q], o);  // block-uniform
+                if (g.nt) __builtin_nontemporal_store(v[q], o);
                 else *o = v[q];
             }
+#endif
         }
     };
 
@@ -307,7 +322,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             // kpass 0: cos (or Z) into the image (TMt = 128 when saving: it leaves between two
             // barriers); 1: sin into the image; 2: sin into the image and cos (or Z) into the D image
             // kl0: layer 0 (SIREN w0 = 30 of fc_net.0; ×1 elsewhere, exact, so not multiplied)
-            auto epilogue = [&](auto kpass, auto kl0) {
+            auto epilogue = [&](auto kpass, auto kl0, auto krb) {
                 if constexpr (NOEPI) {  // keep the accumulators (and so the MFMAs) live
                     float t = 0.f;
 #pragma unroll
@@ -319,6 +334,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 }
                 constexpr int pass = decltype(kpass)::value;
                 constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
+                constexpr bool RB = decltype(krb)::value;  // per-ray rows (layer 0, the skip layer)
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
@@ -332,7 +348,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                             float v[4];
 #pragma unroll
                             for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] + bv[e];
-                            if (rb) {
+                            if constexpr (RB) {
                                 const f32x4 rv = ld4(rb + (std::min<int64_t>(p0 + row, g.P - 1) / g.S) * TW + f0);
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) v[e] += rv[e];
@@ -365,9 +381,17 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                         __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
                     }
             };
+            // block-uniform choices of compile-time instances: a load behind a runtime branch would
+            // be waited for with vmcnt(0) — every refill and copy-out store in flight
             auto epi = [&](auto kpass) {
-                if (i == 0) epilogue(kpass, std::true_type{});  // block-uniform
-                else epilogue(kpass, std::false_type{});
+                if (i == 0) {
+                    if (rb) epilogue(kpass, std::true_type{}, std::true_type{});
+                    else epilogue(kpass, std::true_type{}, std::false_type{});
+                } else if (rb) {
+                    epilogue(kpass, std::false_type{}, std::true_type{});
+                } else {
+                    epilogue(kpass, std::false_type{}, std::false_type{});
+                }
             };
             if constexpr (Geo::DIMG) {
                 if (Ds) epi(std::integral_constant<int, 2>{});  // block-uniform
