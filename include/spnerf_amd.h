@@ -64,7 +64,7 @@ typedef struct spnerf_rng {
 #define SPNERF_MLP_SIGMA_ONLY 2  /* trunk + sigma head only (pass 1 of guided sampling)      */
 #define SPNERF_MLP_SUN_ONLY 4    /* sigma + sun-visibility heads (solar-correction pass)     */
 #define SPNERF_MLP_ACCUMULATE 8  /* backward: add into grad_flat instead of overwriting it   */
-#define SPNERF_MLP_DEFER_TRUNK_WGRAD 16  /* backward: leave the trunk layers' weight gradients to
+#define SPNERF_MLP_DEFER_TRUNK_WGRAD 16  /* backward: leave the trunk (and sun_v 2/4) weight gradients to
                                           * spnerf_mlp_trunk_wgrad (the workspace must stay intact) */
 
 /* composite flags */
@@ -106,7 +106,8 @@ int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed,
                             void* stream);
 
 /* The trunk layers' weight gradients (fc_net.2i.weight / .bias, without the per-ray semantic
- * columns) of up to n_seg deferred backwards (SPNERF_MLP_DEFER_TRUNK_WGRAD), added into grad_flat:
+ * columns) and those of sun_v_net.2 / .4 (present in every pass) of up to n_seg deferred
+ * backwards (SPNERF_MLP_DEFER_TRUNK_WGRAD), added into grad_flat:
  * the points of two workspaces (e.g. a render's main and solar-correction passes, rendering.py:
  * 165-177, whose backwards both reach the same trunk) run as ONE weight-gradient GEMM per layer —
  * half the launches and split reductions of one GEMM per pass.  n_rays / n_samples / flags are

@@ -1080,6 +1080,10 @@ struct Gemms<bf16> {
 
 int g_tn_split_tail = 1;  // option "tn_split_tail": see tn_grad
 
+#ifndef SPN_DEFER_SUNV
+#define SPN_DEFER_SUNV 1  // sun_v_net.2 / .4's weight gradients deferred with the trunk's (0: A/B builds)
+#endif
+
 // A second point segment of a weight gradient: the same operands in another pass's workspace
 // (spnerf_mlp_trunk_wgrad: the main and the solar pass of a render in one GEMM per layer)
 struct TnSeg {
@@ -1581,13 +1585,17 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     }
     // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
     {
-        SPN_TRY(tn_grad<T>(c, dS3, H, H, buf(c.w.S2), H, nullptr, 0, H, H, s2, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}));
+        // deferred (SPNERF_MLP_DEFER_TRUNK_WGRAD): sun_v_net.4 / .2's weight gradients run in
+        // spnerf_mlp_trunk_wgrad too — every pass of a render has them
+        if (!c.defer || !SPN_DEFER_SUNV)
+            SPN_TRY(tn_grad<T>(c, dS3, H, H, buf(c.w.S2), H, nullptr, 0, H, H, s2, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}));
         NT g;
         g.A = dS3; g.lda = H; g.K1 = H; g.B = G::w(c, c.k.Ws3T, c.k.Ws3T16); g.ldb = H; g.C = dS2; g.ldc = H;
         g.M = (int)P; g.N = H; g.K = H; g.Dmul = buf(c.w.DS2); g.ld_dmul = H;
         SPN_TRY(G::nt(g, s));
         SPN_TRY(stream_dep(sd, s, s2));
-        SPN_TRY(tn_grad<T>(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s2, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
+        if (!c.defer || !SPN_DEFER_SUNV)
+            SPN_TRY(tn_grad<T>(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s2, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
         NT g2 = g;
         g2.A = dS2; g2.B = G::w(c, c.k.Ws2T, c.k.Ws2T16); g2.C = dZQ; g2.ldc = d.NQ; g2.Dmul = buf(c.w.DQ); g2.ld_dmul = d.NQ;
         SPN_TRY(G::nt(g2, s));
@@ -1711,8 +1719,8 @@ static bool trunk_wgrad_ok(const Ctx& c) {
 }
 
 // The trunk layers' weight gradients (fc_net.2i weight / bias, without the per-ray semantic
-// columns, which each backward adds itself) over the points of up to two deferred backwards'
-// workspaces per GEMM, added into grad (spnerf_mlp_trunk_wgrad).
+// columns, which each backward adds itself) and sun_v_net.2 / .4's over the points of up to two
+// deferred backwards' workspaces per GEMM, added into grad (spnerf_mlp_trunk_wgrad).
 static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int64_t* n_rays, const int32_t* S,
                            const int32_t* flags, float* grad, hipStream_t s) {
     PIdx x;
@@ -1733,6 +1741,17 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
         Ctx c2 = two ? ctx(j + 1) : c;
         if (two) SPN_ARG(wss[j + 1] && (flags[j + 1] & SPNERF_MLP_SAVE), "spnerf_mlp_trunk_wgrad: bad segment");
         if (c.w.P + (two ? c2.w.P : 0) == 0) continue;
+        // sun_v_net.4 and .2 (sun-visibility head, in every pass): dW = dZᵀ · input over all points
+        if (SPN_DEFER_SUNV) {
+            const int H = d.H;
+            const TnSeg s3{c2.hb(c2.w.dS3), c2.hb(c2.w.S2), nullptr, c2.w.P};
+            SPN_TRY(tn_grad<bf16>(c, c.hb(c.w.dS3), H, H, c.hb(c.w.S2), H, nullptr, 0, H, H, s,
+                                  {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}, false, two ? &s3 : nullptr));
+            const TnSeg s2g{c2.hb(c2.w.dS2), c2.hb(c2.w.Q), nullptr, c2.w.P};
+            SPN_TRY(tn_grad<bf16>(c, c.hb(c.w.dS2), H, H, c.hb(c.w.Q), d.NQ, nullptr, 0, H, H, s,
+                                  {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}, false, two ? &s2g : nullptr));
+            SPN_TRY(grad_mark(0, s));   // the heads' gradients are final again
+        }
         for (int i = d.L - 1; i >= 0; --i) {
             auto dz = [&](const Ctx& q) { return q.hb(i == d.L - 1 ? q.w.dZa : q.w.Db[i]); };
             auto in = [&](const Ctx& q) { return q.hb(i == 0 ? q.w.X0b : q.w.Hb[i - 1]); };
