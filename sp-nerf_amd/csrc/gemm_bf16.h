@@ -44,6 +44,7 @@ struct TN16Args {
     int p_per_split = 0;  // set by gemm_tn_bf16
     int b_sin = 0;        // B's columns [0, K1) hold a saved Z (fp16): staged as bf16(sin(Z)) (= the layer's H)
     int dbg = 0;          // ablations (tools only; wide tiles): 1 = no MFMAs
+    int bias_split = 0;   // k_gemm_tn_bf16d: the bias sums shared by the nK = 2 tiles of a column range (g_tn16_bias_split)
     // Second point segment (one weight gradient over two passes' points, spnerf_mlp_trunk_wgrad):
     // rows p >= P1 read A_s2 / B_s2 / B2_s2 + p * ld — pointers the host shifted back by P1 rows,
     // same leading dimensions.  P1 >= P (the default) = one segment.
@@ -54,7 +55,8 @@ struct TN16Args {
 // variant: prefetch depth in K-steps (1 or 2); <= 0 = library default (g_nt16_variant)
 extern int g_nt16_variant;
 extern int g_nt16_epi;  // option nt_bf16_epi
-extern int g_nt16_ip, g_tn16_ip, g_nt16_ip_gen;  // DMA kernels: issue placement of the next K-step (options nt_bf16_ip, tn_bf16_ip)
+extern int g_nt16_ip, g_tn16_ip, g_nt16_ip_gen;
+extern int g_tn16_bias_split;  // option tn_bf16_bias_split  // DMA kernels: issue placement of the next K-step (options nt_bf16_ip, tn_bf16_ip)
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);
 // variant: 1 = 128x128 tiles, 2 = 256x256 tiles where N, K are multiples of 256, 3 = the same
 // tiles fed by LDS-DMA (when P % 32 == 0 as well);

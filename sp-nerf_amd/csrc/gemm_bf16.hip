@@ -1118,7 +1118,13 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
     const int n0 = (t / nK) * TW, k0 = (t % nK) * TW;
     const int p_beg = split * g.p_per_split;
     const int p_end = min(g.P, p_beg + g.p_per_split);
-    const bool do_bias = g.slab_b != nullptr && k0 == 0;
+    // bias_split (nK == 2): the two tiles of a column range [n0, n0 + 256) read the same A rows;
+    // each sums the bias of one 128-column half (k-tile kt: half kt), so both do the same work and
+    // stay in step — with the whole bias on the k0 == 0 tile it fell behind its partner and the
+    // shared A rows were fetched twice (PMC: 1.46x the algorithmic bytes)
+    const bool bsplit = g.bias_split && nK == 2;
+    const int kt = t % nK;
+    const bool do_bias = g.slab_b != nullptr && (bsplit || k0 == 0);
     const int ns = p_end > p_beg ? (p_end - p_beg) / TD_STEP : 0;  // whole steps (host-checked)
 
     // this lane's 4 DMA sources (instructions q = wid + 8 i: i < 2 → A, else B), advanced by
@@ -1219,11 +1225,19 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
             if (ks == 0) mid();
         }
     };
-    // bias: thread (chunk ch of 32, row phase lrow of 16) sums rows lrow, lrow + 16 of each step
-    const int ch = tid & 31, lrow = tid >> 5;
+    // bias: thread (chunk ch of 32, row phase lrow of 16) sums rows lrow, lrow + 16 of each step;
+    // bsplit: thread (chunk ch of the tile's 16, row phase lrow of 32) sums row lrow
+    const int ch = bsplit ? 16 * kt + (tid & 15) : tid & 31, lrow = bsplit ? tid >> 4 : tid >> 5;
     float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     auto bias_rows = [&](int stg) {
         const char* sA = smem + stg * TD_STG + (ch >> 4) * HALF;
+        if (bsplit) {  // block-uniform
+            float f[8];
+            unpack8(*reinterpret_cast<const u32x4*>(sA + tn_off(lrow, ch & 15)), f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bs[e] += f[e];
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < TD_STEP / 16; ++i) {
             float f[8];
@@ -1272,7 +1286,20 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
                 if (n < g.N) slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
             }
     }
-    if (do_bias) {
+    if (do_bias && bsplit) {
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);  // [32 phases][128 features]
+        const int cl = ch & 15;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[lrow * 128 + 8 * cl + e] = bs[e];
+        __syncthreads();
+        const int n = n0 + 128 * kt + tid;
+        if (tid < 128 && n < g.N) {
+            float s = 0.f;
+            for (int ph = 0; ph < 32; ++ph) s += red[ph * 128 + tid];
+            g.slab_b[(int64_t)split * g.N + n] = s;
+        }
+    } else if (do_bias) {
         __syncthreads();
         float* red = reinterpret_cast<float*>(smem);  // [16 phases][256 features]
 #pragma unroll
@@ -1292,6 +1319,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 int g_nt16_variant = 8;
 int g_nt16_ip = 2;  // DMA NT / TN: where a K-step issues the next step's DMAs (0 before its MFMAs, 1 after, 2 between the k-halves)
 int g_tn16_ip = 2;
+int g_tn16_bias_split = 1;
 int g_nt16_ip_gen = 2;  // the same for the general (bias / sine / rank-1) epilogue instances
 int g_nt16_epi = 1;     // option "nt_bf16_epi": 1 = compile-time epilogue variants of the DMA NT, 0 = the generic one
 int g_tn16_variant = 3;
@@ -1430,6 +1458,7 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
         const int nb = cdiv(a.N, TW) * cdiv(a.K, TW);
         if (dma)  // B staged as is
         {
+            a.bias_split = g_tn16_bias_split;
             const int ip = (a.dbg & 4) ? 2 : (a.dbg & 2) ? 1 : g_tn16_ip;
             if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, dim3(nb * splits), dim3(512), 0, s, a);
             else if (ip == 1) hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, dim3(nb * splits), dim3(512), 0, s, a);

@@ -352,6 +352,8 @@ static Marks* marks_of_device() {
     return &m;
 }
 
+int g_tile_rowsum = 1;  // 1 = per-ray dZ sums by 64-point tiles (fused into the dX chain); 0 = k_ray_rowsum16
+
 static int32_t grad_mark(int k, hipStream_t s) {
     if (!g_marks_armed) return SPNERF_OK;
     Marks* m = marks_of_device();
@@ -793,6 +795,37 @@ __global__ __launch_bounds__(256) void k_ray_rowsum16(const bf16* __restrict__ i
 #pragma unroll
         for (int e = 0; e < 8; ++e) out[ray * ldo + 8 * threadIdx.x + e] = r[e];
     }
+}
+
+// The per-ray sums of the 512-wide trunk dZ in the fused backward's order (S % 64 == 0): per
+// 64-point tile the column sums of tile_colsum_part / _final (trunk.h), read from HBM here (the
+// layer-by-layer backward; k_trunk_bwd_bf16 forms them from its LDS image) ...
+__global__ __launch_bounds__(512) void k_tile_rowsum16(const bf16* __restrict__ in, float* __restrict__ part_out) {
+    __shared__ float part[8 * 512];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const bf16* src = in + ((int64_t)blockIdx.x * 64 + 8 * w) * 512 + 8 * lane;
+    u32x4 rows[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) rows[r] = ldg16(src + r * 512);
+    float a[8];
+    tile_colsum_part(rows, a);
+    *reinterpret_cast<f32x4*>(part + w * 512 + lane * 8) = f32x4{a[0], a[1], a[2], a[3]};
+    *reinterpret_cast<f32x4*>(part + w * 512 + lane * 8 + 4) = f32x4{a[4], a[5], a[6], a[7]};
+    __syncthreads();
+    part_out[(int64_t)blockIdx.x * 512 + tid] = tile_colsum_final(part, tid);
+}
+
+// ... and the T tiles of a ray added in tile order: out[ray][c] = Σ_t part[ray·T + t][c]
+__global__ __launch_bounds__(256) void k_ray_tiles_sum(const float* __restrict__ part, int T, int64_t n_rays,
+                                                       float* __restrict__ out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n_rays * 512) return;
+    const int64_t ray = i >> 9;
+    const int c = (int)(i & 511);
+    const float* p = part + ray * T * 512 + c;
+    float s = p[0];
+    for (int t = 1; t < T; ++t) s += p[t * 512];
+    out[i] = s;
 }
 
 struct RayBwdArgs {
@@ -1649,6 +1682,24 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     }
     // 6. trunk, top to bottom
     const T* X0 = BF ? buf(c.w.X0b) : buf(c.w.X0);
+    // the per-ray sums of dZ_0 / dZ_skip (semantic columns) by 64-point tiles: the fused dX chain
+    // forms the tiles' column sums from its LDS image (no re-read of dZ), the layer-by-layer chain
+    // from HBM in the same order (bit-identical), then one launch adds each ray's tiles
+    const bool tsum = BF && g_tile_rowsum && d.sem && W == 512 && S % 64 == 0;
+    auto ray_tiles = [&](int i, const T* dZi, bool parts_done) -> int32_t {
+        float* part = c.at(i == 0 ? c.w.Rp0 : c.w.Rp4);
+        ProfScope prof("ray_rowsum", s2, 0.0, (parts_done ? 0.0 : 2.0 * P * W) + 4.0 * (P / 64 + n_rays) * W);
+        if (!parts_done) {
+            hipLaunchKernelGGL(k_tile_rowsum16, dim3((unsigned)(P / 64)), dim3(512), 0, s2,
+                               reinterpret_cast<const bf16*>(dZi), part);
+            SPN_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_ray_tiles_sum, dim3((unsigned)cdiv(n_rays * 512, 256)), dim3(256), 0, s2, part, S / 64,
+                           n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4));
+        SPN_HIP(hipGetLastError());
+        return SPNERF_OK;
+    };
+    bool parts_in_bwd = false;  // the fused chain wrote the tile sums
     // layer i's weight gradient (and the per-ray sums of its dZ at layer 0 / the skip layer)
     auto layer_grads = [&](int i, const T* dZi) -> int32_t {
         // dZi holds dL/d(pre-activation of layer i).  The input of layer i >= 2 is saved as Z
@@ -1664,8 +1715,10 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         else
             SPN_TRY(tn_grad<T>(c, dZi, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s2,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
-        if (d.sem && (i == 0 || i == d.skip))
-            SPN_TRY(ray_rowsum<T>(dZi, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
+        if (d.sem && (i == 0 || i == d.skip)) {
+            if (tsum) SPN_TRY(ray_tiles(i, dZi, parts_in_bwd));
+            else SPN_TRY(ray_rowsum<T>(dZi, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
+        }
         return grad_mark(1 + (d.L - 1 - i), s2);
     };
     if (BF && !zs && g_fused_bwd && !c.k.Wb16.empty() && c.k.Wb16[1] >= 0) {
@@ -1680,6 +1733,11 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
             a.dZ[i - 1] = c.hb(c.w.Db[i - 1]);
         }
         a.P = P; a.L = d.L;
+        if (tsum && d.skip > 0 && d.skip < d.L) {
+            a.Rsum[0] = c.at(c.w.Rp0); a.rs_layer[0] = 0;
+            a.Rsum[1] = c.at(c.w.Rp4); a.rs_layer[1] = d.skip;
+            parts_in_bwd = true;
+        }
         // algorithmic HBM bytes: dZ_{L-1} in, per layer D_{i-1} in and dZ_{i-1} out
         SPN_TRY(trunk_bwd_bf16(a, s, 2.0 * P * W * W * (d.L - 1), 2.0 * P * W * (1.0 + 2.0 * (d.L - 1))));
         SPN_TRY(stream_dep(sd, s, s2));
@@ -1872,6 +1930,7 @@ static int* option_slot(const char* name) {
     if (n == "nt_bf16_variant") return &g_nt16_variant;
     if (n == "nt_bf16_ip") return &g_nt16_ip;
     if (n == "tn_bf16_ip") return &g_tn16_ip;
+    if (n == "tn_bf16_bias_split") return &g_tn16_bias_split;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;
     if (n == "grad_marks_flags") return &g_marks_flags;
@@ -1886,6 +1945,7 @@ static int* option_slot(const char* name) {
     if (n == "pe_inline") return &g_pe_inline;
     if (n == "tn_split_tail") return &g_tn_split_tail;
     if (n == "fused_bwd") return &g_fused_bwd;
+    if (n == "tile_rowsum") return &g_tile_rowsum;
     if (n == "trunk2") return &g_trunk2;
     if (n == "trunk2_tile") return &g_trunk2_tile;
     if (n == "emu_bf16") return &g_emu_bf16;

@@ -65,7 +65,33 @@ struct TrunkBwdArgs {
     int64_t P = 0;
     int L = 0;
     int dbg = 0;  // g_trunk_dbg (profiling ablations, outputs invalid): 1 = no dZ copy-outs, 2 = no D loads
+    // per-tile column sums of dZ_l for l = rs_layer[k] (-1: none) into Rsum[k][tile][512]: the
+    // per-ray sums of layer 0's and the skip layer's dZ (semantic columns) from the LDS image
+    // instead of a re-read of dZ (k_ray_rowsum16).  Needs P % 64 == 0; the order is tile_colsum's
+    float* Rsum[2] = {nullptr, nullptr};
+    int rs_layer[2] = {-1, -1};
 };
+
+// Column sums of a 64-row bf16 [64][512] tile in a fixed order shared by the fused backward (LDS
+// image) and k_tile_rowsum16 (HBM): wave w adds rows 8w .. 8w+7 of its 8 columns (lane = 16-B
+// chunk) in row order, then column c = Σ_w part[w][c] in wave order.
+__device__ __forceinline__ void tile_colsum_part(const u32x4 (&rows)[8], float (&a)[8]) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        float f[8];
+        unpack8(rows[r], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += f[e];
+    }
+}
+__device__ __forceinline__ float tile_colsum_final(const float* part, int c) {
+    float s = part[c];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) s += part[k * 512 + c];
+    return s;
+}
 
 // Offset (bf16 elements) of W[n][k] of a [512][Kp] layer in MFMA A-fragment order: wave w =
 // n / 64 streams k-steps of 16; per k-step its two 32-feature tiles are 1 KB each, lane

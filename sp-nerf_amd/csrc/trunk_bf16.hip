@@ -435,7 +435,7 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
     using Geo = TrunkGeo<64>;
     constexpr int TMt = 64, NJ = Geo::NJ, IMG = Geo::IMG, CPT = Geo::CPT, TPD = Geo::TPD;
     constexpr int nks = TW / 16;
-    __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
+    __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 8 * TW * 4];  // + the column-sum partials
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     const int sw = r32 & 15;
     typedef const __attribute__((address_space(4))) TrunkBwdArgs* KArgs;
@@ -465,6 +465,21 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
             const int c = ct + 512 * (q0 + q);
             if (p0 + (c >> 6) < g.P) *reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8) = v[q];
         }
+    };
+    // per-tile column sums of the image (dZ_l, complete: called after a barrier, by every thread)
+    // into dst[512]; the partials sit beyond the two images
+    auto colsum = [&](float* dst) {
+        const int cl = opaque(lane);
+        u32x4 rows[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) rows[r] = *reinterpret_cast<const u32x4*>(smem + act_off(8 * w + r, cl));
+        float a[8];
+        tile_colsum_part(rows, a);
+        float* part = reinterpret_cast<float*>(smem + 2 * IMG);
+        *reinterpret_cast<f32x4*>(part + w * TW + cl * 8) = f32x4{a[0], a[1], a[2], a[3]};
+        *reinterpret_cast<f32x4*>(part + w * TW + cl * 8 + 4) = f32x4{a[4], a[5], a[6], a[7]};
+        __syncthreads();
+        dst[tid] = tile_colsum_final(part, tid);
     };
 
     int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -519,6 +534,9 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
 #pragma unroll
                     for (int r = 0; r < 16; ++r) acc[a][j][r] = 0.f;
             __syncthreads();  // the dZ_i image is complete; the D image is free
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (i == g.rs_layer[k]) colsum(g.Rsum[k] + tile * TW);  // block-uniform
             const char* brow = smem + r32 * 1024;
             bf16x8 bc[NJ];
 #pragma unroll
@@ -595,6 +613,9 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
         }
         __syncthreads();  // dZ_0 is complete
 #pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (g.rs_layer[k] == 0) colsum(g.Rsum[k] + tile * TW);  // block-uniform
+#pragma unroll
         for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(pend, p0, q0, std::integral_constant<int, 4>{});
         __syncthreads();  // the next tile restages the image
     }
@@ -609,6 +630,9 @@ int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double
     SPN_ARG(a.dZtop != nullptr, "trunk_bwd_bf16: NULL dZ_{L-1}");
     for (int i = 1; i < a.L; ++i)
         SPN_ARG(a.Wb[i] && a.D[i - 1] && a.dZ[i - 1], "trunk_bwd_bf16: NULL pointer at layer %d", i);
+    for (int k = 0; k < 2; ++k)
+        SPN_ARG(a.rs_layer[k] < 0 || (a.rs_layer[k] < a.L && a.Rsum[k] && a.P % 64 == 0),
+                "trunk_bwd_bf16: column sums of layer %d need a buffer and whole 64-point tiles", a.rs_layer[k]);
     const int ntiles = cdiv(a.P, 64);
     TrunkBwdArgs ad = a;
     ad.dbg = g_trunk_dbg;

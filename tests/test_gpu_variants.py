@@ -148,3 +148,40 @@ def test_bf16_nt_epilogue_variants_bitwise_equal(opts, n, ns):
     assert sorted(g0) == sorted(g1)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), (opts, k)
+
+
+@pytest.mark.parametrize("n,ns", [(300, 64), (301, 40)])
+def test_bf16_tile_rowsum_agrees(n, ns):
+    """The per-ray sums of dZ_0 / dZ_skip (the semantic columns' gradients) by 64-point tiles —
+    formed from the fused dX chain's LDS image (option tile_rowsum 1) — against the per-ray
+    k_ray_rowsum16 over HBM (0): a different fp32 summation order, so gradients agree to 1e-4 of
+    their largest entry and renders bit for bit; 40 + 40 samples per ray is not a whole number of
+    tiles (falls back to the per-ray sums: bit-identical)."""
+    r0, g0 = _render_bf16({"tile_rowsum": 0}, n=n, ns=ns)
+    r1, g1 = _render_bf16({"tile_rowsum": 1}, n=n, ns=ns)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    assert sorted(g0) == sorted(g1)
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        scale = g0[k].abs().max().item()
+        assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
+        if ns % 64:
+            assert torch.equal(g0[k], g1[k]), k
+
+
+def test_bf16_tn_bias_split_agrees():
+    """The DMA weight-gradient GEMM's bias sums split over the two k-tiles of each column range
+    (option tn_bf16_bias_split 1, so partner tiles do equal work and share the A rows in L2)
+    against the whole bias on the k0 = 0 tile (0): another fp32 order of the same bf16 sums —
+    gradients within 1e-4 of their largest entry, renders bit for bit.  2 048 rays: the
+    256x256 DMA tiling runs."""
+    r0, g0 = _render_bf16({"tn_bf16_bias_split": 0}, n=2048)
+    r1, g1 = _render_bf16({"tn_bf16_bias_split": 1}, n=2048)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    assert sorted(g0) == sorted(g1)
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        scale = g0[k].abs().max().item()
+        assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
