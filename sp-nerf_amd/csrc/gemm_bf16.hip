@@ -1324,13 +1324,18 @@ int g_nt16_ip_gen = 2;  // the same for the general (bias / sine / rank-1) epilo
 int g_nt16_epi = 1;     // option "nt_bf16_epi": 1 = compile-time epilogue variants of the DMA NT, 0 = the generic one
 int g_tn16_variant = 3;
 
-static bool tn_wide(int N, int K, int variant) {
+int g_tn16_few_tiles = 1;  // option tn_bf16_few_tiles: 256x256 tiles also for 1-3 tile shapes, with more splits
+
+static bool tn_wide(int N, int K, int variant, int few = -1) {
     const int v = variant > 0 ? variant : g_tn16_variant;
     // fewer than 4 wide tiles cannot fill the chip within the 64-split cap (N = K = 256: 64
-    // blocks, 76 us against 40 us for 256 blocks of the 128x128 kernel).  A skip-layer K (512 +
-    // K0p) stays on the 128x128 kernel too: a wide part + narrow tail re-reads dZ for the tail
-    // and needs 64 splits (K = 576: 143 + 18 us reduction against 152 + 7)
-    return (v == 2 || v == 3) && N % TW == 0 && K % TW == 0 && (N / TW) * (K / TW) >= 4;
+    // blocks, 76 us against 40 us for 256 blocks of the 128x128 kernel) — so such shapes take
+    // 256 / tiles splits instead (tn_splits_bf16, option tn_bf16_few_tiles): every operand row is
+    // then read once (the 128x128 tiling of N = K = 256 reads each twice).  A skip-layer K (512 +
+    // K0p) stays on the 128x128 kernel: a wide part + narrow tail re-reads dZ for the tail and
+    // needs 64 splits (K = 576: 143 + 18 us reduction against 152 + 7)
+    const int tiles = (N / TW) * (K / TW);
+    return (v == 2 || v == 3) && N % TW == 0 && K % TW == 0 && (tiles >= 4 || ((few < 0 ? g_tn16_few_tiles : few) && tiles >= 1));
 }
 
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
@@ -1426,14 +1431,15 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
 
 int g_tn16_min_points = 1024;  // fewest points per split of a bf16 weight-gradient GEMM
 
-int tn_splits_bf16(int P, int N, int K, int variant) {
-    const bool wide = tn_wide(N, K, variant);
+int tn_splits_bf16(int P, int N, int K, int variant, int few) {
+    const bool wide = tn_wide(N, K, variant, few);
     const int tiles = wide ? cdiv(N, TW) * cdiv(K, TW) : cdiv(N, HB) * cdiv(K, HB);
     // one wide block per CU, two 128x128 ones: as many splits as fill the 256 CUs WITHOUT a
     // second round (N = 768, K = 512 rounded up to 258 wide blocks: 221 us, two rounds)
     int splits = (wide ? 256 : 512) / tiles;
-    if (splits > 64) splits = 64;
-    const int max_splits = cdiv(P, g_tn16_min_points);
+    if (splits > (wide && tiles < 4 ? 256 : 64)) splits = wide && tiles < 4 ? 256 : 64;
+    // (few wide tiles: half the points per split, so small batches still spread over the chip)
+    const int max_splits = cdiv(P, wide && tiles < 4 ? g_tn16_min_points / 2 : g_tn16_min_points);
     if (splits > max_splits) splits = max_splits;
     return splits < 1 ? 1 : splits;
 }

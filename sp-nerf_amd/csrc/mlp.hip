@@ -1931,6 +1931,7 @@ static int* option_slot(const char* name) {
     if (n == "nt_bf16_ip") return &g_nt16_ip;
     if (n == "tn_bf16_ip") return &g_tn16_ip;
     if (n == "tn_bf16_bias_split") return &g_tn16_bias_split;
+    if (n == "tn_bf16_few_tiles") return &g_tn16_few_tiles;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;
     if (n == "grad_marks_flags") return &g_marks_flags;

@@ -232,7 +232,7 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         int64_t slab = 0, slab_b = 0;
         auto need = [&](int N, int K) {
             // bf16: either TN tiling may run (tn_bf16_variant can change after the layout is made)
-            const int sp = d.bf ? std::max(tn_splits_bf16((int)P, N, K, 1), tn_splits_bf16((int)P, N, K, 2))
+            const int sp = d.bf ? std::max(tn_splits_bf16((int)P, N, K, 1), tn_splits_bf16((int)P, N, K, 2, 1))
                                 : tn_splits((int)P, N, K);
             slab = std::max(slab, (int64_t)sp * N * K);
             slab_b = std::max(slab_b, (int64_t)sp * N);

@@ -185,3 +185,20 @@ def test_bf16_tn_bias_split_agrees():
         assert torch.isfinite(g1[k]).all(), k
         scale = g0[k].abs().max().item()
         assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
+
+
+@pytest.mark.parametrize("n", [300, 2048])
+def test_bf16_tn_few_tiles_agrees(n):
+    """Weight gradients of 256-wide layers (sun_v_net.2 / .4, the solar pass's sun_v_net.0) on
+    the 256x256 DMA tiling with more point splits (option tn_bf16_few_tiles 1) against the
+    128x128 tiling (0): other point splits, so fp32 slab sums round differently — gradients within
+    1e-4 of their largest entry, renders bit for bit."""
+    r0, g0 = _render_bf16({"tn_bf16_few_tiles": 0}, n=n)
+    r1, g1 = _render_bf16({"tn_bf16_few_tiles": 1}, n=n)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    assert sorted(g0) == sorted(g1)
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        scale = g0[k].abs().max().item()
+        assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
