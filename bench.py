@@ -59,6 +59,8 @@ GEMM_CLASSES = {
     "gemm_tn_bf16d": ("k_gemm_tn_bf16d<2> (bf16 MFMA weight-gradient GEMM, 256x256 tiles, LDS-DMA)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16w": ("k_gemm_tn_bf16w (bf16 MFMA weight-gradient GEMM, 256x256 register-staged)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA weight-gradient GEMM, 128x128 tiles)", BF16_MFMA_PEAK_TFLOPS),
+    "gemm_tn_bf16k": ("k_gemm_tn_bf16_k64 (bf16 MFMA weight gradient N = 512, K = 64: fc_net.0 and the skip "
+                      "layer's PE tail, whole 512x64 output per split)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bf16": ("k_trunk2_bf16<128> (fused bf16 trunk, inference: 128-point LDS-resident tiles, option trunk2 3; "
                    "k_trunk_bf16<128> with trunk2 0)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bf16_train": ("k_trunk_bf16<64> (fused bf16 trunk, training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),

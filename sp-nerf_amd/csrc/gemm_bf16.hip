@@ -948,6 +948,148 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
     }
 }
 
+// Narrow TN (option tn_bf16_k64): N = 512 A features x K = 64 B features — fc_net.0's weight
+// gradient over the PE and the skip layer's PE tail.  One block per split holds the whole
+// 512 x 64 output (8 waves of 64 x 64, 2x2 32x32 accumulators), so every operand row is read
+// from HBM exactly once; the 128x128 kernel above ran 4 N-tiles per split, each with a 128-wide
+// K tile of which 64 columns were clamped duplicates (twice the MFMA work, dZ fetched per tile).
+// 32-point steps: A as four [32][128] tn_off images, B in a fifth (its chunks 0..7), two LDS
+// stages (80 KB); register loads two steps ahead (two sets, 72 KB in flight per CU) — the
+// kernel is HBM-bound (1.1 KB per point, 64 K MAC per point).  Steps past the split read
+// clamped rows that are stored as zeros (an even step count, so the loop has no branch).
+constexpr int T64_STEP = 32, T64_IMG = T64_STEP * 256, T64_STG = 5 * T64_IMG;
+__global__ __launch_bounds__(512) void k_gemm_tn_bf16_k64(TN16Args g) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * T64_STG];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int split = blockIdx.x;
+    const int p_beg = split * g.p_per_split;
+    const int p_end = min(g.P, p_beg + g.p_per_split);
+    const int ach = tid & 63, arow = tid >> 6;         // A: features 8·ach.., rows arow + 8i
+    const int bch = tid & 7, brow = (tid >> 3) & 31;   // B: features 8·bch.., row brow (tid >= 256 repeat tid - 256)
+    const bool do_bias = g.slab_b != nullptr;
+    float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+    u32x4 ra0[4], ra1[4], rb0, rb1;
+    auto gload = [&](u32x4 (&ra)[4], u32x4& rb, int p0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pc = min(p0 + arow + 8 * i, p_end - 1);
+            ra[i] = ldg16((pc >= g.P1 ? g.A_s2 : g.A) + (int64_t)pc * g.lda + 8 * ach);
+        }
+        const int pb = min(p0 + brow, p_end - 1);
+        rb = ldg16((pb >= g.P1 ? g.B_s2 : g.B) + (int64_t)pb * g.ldb + 8 * bch);
+    };
+    auto sstore = [&](int stg, const u32x4 (&ra)[4], const u32x4& rb, int p0) {
+        char* sA = smem + stg * T64_STG;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = arow + 8 * i;
+            const u32x4 v = p0 + row < p_end ? ra[i] : z;
+            if (do_bias) {  // block-uniform
+                float f[8];
+                unpack8(v, f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bs[e] += f[e];
+            }
+            *reinterpret_cast<u32x4*>(sA + (ach >> 4) * T64_IMG + tn_off(row, ach & 15)) = v;
+        }
+        // threads tid and tid + 256 write the same chunk (same value: no branch around the store)
+        *reinterpret_cast<u32x4*>(sA + 4 * T64_IMG + tn_off(brow, bch)) = p0 + brow < p_end ? rb : z;
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int h = lane >> 5, grp = (lane >> 4) & 1;
+    const int q = (lane & 15) >> 2, pp = lane & 3;
+    auto trd = [&](const char* base, int r0, int col) -> s16x4 {
+        const int o = tn_off(r0 + q, (col >> 3) + (pp >> 1)) + 8 * (pp & 1);
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + o));
+    };
+    auto operand = [&](const char* base, int r0, int col) -> bf16x8 {
+        const s16x4 lo = trd(base, r0, col), hi = trd(base, r0 + 4, col);
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    // wave w: A features [64w, 64w + 64) = image w / 2, columns 64·(w & 1) ..; all 64 B features
+    const int aimg = wid >> 1, acol = (wid & 1) * 64;
+    auto compute = [&](int stg) {
+        const char* sA = smem + stg * T64_STG + aimg * T64_IMG;
+        const char* sB = smem + stg * T64_STG + 4 * T64_IMG;
+#pragma unroll
+        for (int ks = 0; ks < T64_STEP / 16; ++ks) {
+            const int r0 = 16 * ks + 8 * h;
+            const bf16x8 a0 = operand(sA, r0, acol + 16 * grp);
+            const bf16x8 a1 = operand(sA, r0, acol + 32 + 16 * grp);
+            const bf16x8 b0 = operand(sB, r0, 16 * grp);
+            const bf16x8 b1 = operand(sB, r0, 32 + 16 * grp);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+        }
+    };
+
+    if (p_beg < p_end) {  // block-uniform
+        const int ns = ((p_end - p_beg + T64_STEP - 1) / T64_STEP + 1) & ~1;  // even
+        gload(ra0, rb0, p_beg);
+        gload(ra1, rb1, p_beg + T64_STEP);
+        sstore(0, ra0, rb0, p_beg);
+        __syncthreads();
+        for (int st = 0; st < ns; st += 2) {
+            const int p = p_beg + T64_STEP * st;
+            gload(ra0, rb0, p + 2 * T64_STEP);
+            __builtin_amdgcn_sched_barrier(0);  // issue the loads before the MFMAs
+            compute(0);
+            __builtin_amdgcn_sched_barrier(0);  // LDS writes (and their waits) after the MFMAs
+            sstore(1, ra1, rb1, p + T64_STEP);
+            __syncthreads();
+            gload(ra1, rb1, p + 3 * T64_STEP);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(1);
+            __builtin_amdgcn_sched_barrier(0);
+            sstore(0, ra0, rb0, p + 2 * T64_STEP);
+            __syncthreads();
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) prefetch
+    }
+
+    float* slab = g.slab + (int64_t)split * g.slab_stride;
+    const int r32 = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int k = j * 32 + r32;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = 64 * wid + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
+            }
+    }
+    if (do_bias) {  // block-uniform; the 8 row phases of every chunk in a fixed order
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);  // [8 phases][512 features]
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[arow * 512 + 8 * ach + e] = bs[e];
+        __syncthreads();
+        float s = 0.f;
+#pragma unroll
+        for (int ph = 0; ph < 8; ++ph) s += red[ph * 512 + tid];
+        g.slab_b[(int64_t)split * 512 + tid] = s;
+    }
+}
+
+int g_tn16_k64 = 1;  // option tn_bf16_k64: the narrow kernel above for N = 512, K = 64
+static bool tn_k64(int N, int K) { return g_tn16_k64 && N == 512 && K == 64; }
+
 // Wide TN: 256 (A features) x 256 (B features) per block, 8 waves of 128x64 (4x2 32x32
 // accumulators, 128 AGPRs), one block per CU.  Per 64-point step a block stages 2 x 32 KB and
 // runs 8 x 32 MFMAs: half the L2 bytes per FLOP of the 128x128 kernel above, whose two
@@ -1432,6 +1574,8 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
 int g_tn16_min_points = 1024;  // fewest points per split of a bf16 weight-gradient GEMM
 
 int tn_splits_bf16(int P, int N, int K, int variant, int few) {
+    // the narrow kernel: one block per CU, at least half the usual points per split
+    if (tn_k64(N, K)) return std::max(1, std::min(256, cdiv(P, g_tn16_min_points / 2)));
     const bool wide = tn_wide(N, K, variant, few);
     const int tiles = wide ? cdiv(N, TW) * cdiv(K, TW) : cdiv(N, HB) * cdiv(K, HB);
     // one wide block per CU, two 128x128 ones: as many splits as fill the 256 CUs WITHOUT a
@@ -1456,6 +1600,13 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     const bool wide = tn_wide(a.N, a.K, -1);
     const bool two = a.P1 < a.P;
     SPN_ARG(!two || (a.A_s2 && a.B_s2 && (a.K1 >= a.K || a.B2_s2)), "gemm_tn_bf16: second segment incomplete");
+    if (tn_k64(a.N, a.K) && a.K1 >= a.K && !a.b_sin && a.ld_slab == a.K) {
+        ProfScope prof("gemm_tn_bf16k", s, 2.0 * a.P * a.N * a.K,
+                       2.0 * (double)a.P * (a.N + a.K) + 4.0 * splits * ((double)a.N * a.K + a.N));
+        hipLaunchKernelGGL(k_gemm_tn_bf16_k64, dim3(splits), dim3(512), 0, s, a);
+        SPN_HIP(hipGetLastError());
+        return SPNERF_OK;
+    }
     // DMA: whole 32-point steps (and a segment boundary on a step)
     const bool dma = wide && g_tn16_variant == 3 && a.P % TD_STEP == 0 && !a.b_sin && (!two || a.P1 % TD_STEP == 0);
     ProfScope prof(dma ? "gemm_tn_bf16d" : wide ? "gemm_tn_bf16w" : "gemm_tn_bf16", s, 2.0 * a.P * a.N * a.K,

@@ -1135,6 +1135,8 @@ static int32_t tn_grad(const Ctx& c, const T* A, int lda, int N, const T* B, int
     // on the 128x128 kernel at 710 us per 524 288 points; split into the wide K = 512 part and
     // the K0p tail (two passes over dZ, the tail's slab reduced into columns K1..) it is ≈470.
     // Below 2^18 points the single launch is as fast
+    // (with the narrow N = 512, K = 64 kernel for the tail, tn_bf16_k64, splitting below 2^18
+    // points measured level too: C4 at 512 rays 4.468 / 4.491 against 4.469 / 4.465 ms)
     bool split = std::is_same<T, bf16>::value && g_tn_split_tail && B2 && K > K1 && P >= (1 << 18) &&
                  N % 256 == 0 && K1 % 256 == 0 && (N / 256) * (K1 / 256) >= 4;
     for (const ReduceArgs& r : outs) split = split && !r.transpose;
@@ -1932,6 +1934,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_ip") return &g_tn16_ip;
     if (n == "tn_bf16_bias_split") return &g_tn16_bias_split;
     if (n == "tn_bf16_few_tiles") return &g_tn16_few_tiles;
+    if (n == "tn_bf16_k64") return &g_tn16_k64;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;
     if (n == "grad_marks_flags") return &g_marks_flags;
