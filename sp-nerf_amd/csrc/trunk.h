@@ -148,6 +148,7 @@ extern int g_fused_trunk;  // 1 = bf16 forwards use the fused trunk where suppor
 extern int g_trunk_tile;   // 0 = tile by mode; 64 / 128 = force
 extern int g_trunk_dbg;    // profiling ablations (outputs invalid): 1 = no HBM copy-outs
 extern int g_trunk_var;    // profiling ablations of the 128-point trunk (outputs invalid)
+extern int g_trunk_dreg;   // 64-point training tiles: D stored from the registers in the epilogue
 extern int g_trunk_nt;     // 1 = trunk H stores non-temporal, 2 = fused heads' H loads non-temporal
 bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 // layer 0 inside the launch (TrunkArgs::X0) for this PE width when saving / not saving

@@ -45,6 +45,8 @@ int g_fused_trunk = 1;
 int g_trunk_tile = 0;  // 0 = by mode (64 when saving, else 128); 64 / 128 force a tiling (A/B runs)
 int g_trunk_nt = 0;
 int g_trunk_var = 0;  // profiling ablations of the 128-point tiling (k_trunk_bf16 VAR)
+int g_trunk_dreg = 1;  // 64-point training tiles: D = cos leaves from the accumulators in the epilogue
+                       // (VAR 512) instead of through the D image behind the next k-loop
 int g_trunk_dbg = 0;   // profiling ablations, outputs invalid when set: 1 = skip the HBM copy-outs,
                        // (options trunk_var 16 / 32: no MFMAs in the main k-loop / no sine in the
                        // inference epilogue)
@@ -77,6 +79,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     constexpr int NJ = Geo::NJ, IMG = Geo::IMG, CPT = Geo::CPT;
     constexpr int TPD = Geo::TPD;
     constexpr bool NOMF = VAR & 16, NOSIN = VAR & 32, NOW = VAR & 64, NOB = VAR & 128, NOEPI = VAR & 256;
+    constexpr bool DREG = Geo::DIMG && (VAR & 512);  // D from the registers (see epilogue_dreg)
     __shared__ __attribute__((aligned(16))) char smem[Geo::LDS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     float* sbias = reinterpret_cast<float*>(smem + Geo::BIAS_OFF);
@@ -393,16 +396,74 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                     epilogue(kpass, std::false_type{}, std::false_type{});
                 }
             };
+            // DREG: sin → the image as above, D = cos (×w0 at layer 0) straight from the registers
+            // to HBM during the epilogue — the 8-byte pieces of feature groups (0, 1) and (2, 3) of
+            // a row joined by v_permlane32_swap into one 16-B buffer store per lane (the store of
+            // k_trunk2_bf16).  The k-loop then drains only H, and D's HBM writes run while the
+            // epilogue's VALU work does (HBM was idle through every epilogue); layers with per-ray
+            // rows (whose loads would wait behind the stores) or a saved Z keep the D image.
+            auto epilogue_dreg = [&](auto kl0) {
+                constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
+                const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
+                const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
+                const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(Ds + p0 * TW, 0, rows * TW * 2, 0x00020000);
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        const int row = 32 * j + er32;
+                        u32x2 cq[4];
+#pragma unroll
+                        for (int gq = 0; gq < 4; ++gq) {
+                            const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                            const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + f0);
+                            float y[4], c[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const float v = acc[a][j][4 * gq + e] + bv[e];
+                                const float x = w0 == 1.f ? v : w0 * v;
+                                fast_sincos(x, &y[e], &c[e]);
+                                if (w0 != 1.f) c[e] = w0 * c[e];
+                            }
+                            *reinterpret_cast<u32x2*>(smem + act_off(row, f0 >> 3) + 8 * eh) =
+                                u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                            cq[gq] = u32x2{pack2(c[0], c[1]), pack2(c[2], c[3])};
+                        }
+#pragma unroll
+                        for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+                            for (int e = 0; e < 2; ++e) {
+                                const auto r = __builtin_amdgcn_permlane32_swap(cq[k][e], cq[k + 1][e], false, false);
+                                cq[k][e] = r[0];
+                                cq[k + 1][e] = r[1];
+                            }
+                            // lanes 0..31: features 8k..8k+7 of the pair, lanes 32..63: 8k+8..8k+15
+                            const int fb = 64 * w + 32 * a + 8 * k + 8 * eh;
+                            if (!(g.dbg & 1))  // block-uniform (ablation: no copy-outs)
+                                __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]},
+                                                                       dr, (row * TW + fb) * 2, 0, 0);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
+                }
+            };
             if constexpr (Geo::DIMG) {
-                if (Ds) epi(std::integral_constant<int, 2>{});  // block-uniform
-                else epi(std::integral_constant<int, 1>{});
+                const bool dreg = DREG && Ds && !rb && !zr;  // block-uniform
+                if (dreg) {
+                    if (i == 0) epilogue_dreg(std::true_type{});
+                    else epilogue_dreg(std::false_type{});
+                } else if (Ds) {
+                    epi(std::integral_constant<int, 2>{});  // block-uniform
+                } else {
+                    epi(std::integral_constant<int, 1>{});
+                }
                 if (last) {
                     __syncthreads();
                     copy_all(smem, Hs, p0);
-                    if (Ds) copy_all(smem + IMG, Ds, p0);
+                    if (Ds && !dreg) copy_all(smem + IMG, Ds, p0);
                 }
                 hpend = last ? nullptr : Hs;
-                dpend = last ? nullptr : Ds;
+                dpend = last || dreg ? nullptr : Ds;
             } else {
                 if (Ds) {  // block-uniform
                     epi(std::integral_constant<int, 0>{});
@@ -675,7 +736,8 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     // the saving 64-point tiling (training) is its own profiling class: its roofline (HBM-heavy,
     // H and D of every layer out) is not the inference tiling's (MFMA-bound)
     ProfScope prof(tm == 64 ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
-    if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    if (tm == 64 && g_trunk_dreg) hipLaunchKernelGGL((k_trunk_bf16<64, 512>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 64) hipLaunchKernelGGL((k_trunk_bf16<128, 64>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);

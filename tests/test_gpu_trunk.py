@@ -140,3 +140,17 @@ def test_two_workgroup_trunk_bitwise(dims, n_rays, guided, sc, n_samples):
         for t2 in (1, 2, 3):
             _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples,
                                     options={"trunk2": t2, "trunk2_tile": tile}), base)
+
+
+@pytest.mark.parametrize("dims,n_rays,guided,sc,n_samples,l0", [
+    (ModelDims(width=512, sem=True), 257, True, 0.1, 64, 1),  # C3 flags: the skip layer keeps the D image
+    (ModelDims(width=512), 33, False, 0.1, 32, 1),            # the last 64-point tile half full
+    (ModelDims(width=512), 40, False, 0.0, 64, 2),            # layer 0 in the launch (w0 = 30, no rows)
+])
+def test_training_trunk_register_d_bitwise(dims, n_rays, guided, sc, n_samples, l0):
+    """k_trunk_bf16<64> with D = cos stored from the accumulators during the epilogue (option
+    trunk_dreg 1, the default; layers with per-ray rows keep the D image) against the D image
+    drained behind the next k-loop (0): the same values, so renders and gradients bit for bit."""
+    opts = {"trunk_l0": l0}
+    base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_dreg=0))
+    _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_dreg=1)), base)
