@@ -337,16 +337,33 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(T
                             const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + fa + 8 * gq);
                             const f32x4 rv = *reinterpret_cast<const f32x4*>(sr + fa + 8 * gq);
                             float y[4], c[4];
+                            if constexpr (w0 == 1.f && SPN_PK_EPI) {
+                                // (acc + bias) + row, then · 1/2π (fast_sin's argument in
+                                // revolutions) as packed pairs: the same roundings per element,
+                                // half the VALU issue slots
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) {
-                                // (acc + bias) + row, as the layer-by-layer epilogue adds them
-                                const float v = (acc[a][j][4 * gq + e] + bv[e]) + rv[e];
-                                const float x = w0 == 1.f ? v : w0 * v;
-                                if constexpr (save) {
-                                    fast_sincos(x, &y[e], &c[e]);
-                                    if (w0 != 1.f) c[e] = w0 * c[e];
-                                } else {
-                                    y[e] = fast_sin(x);
+                                for (int e = 0; e < 4; e += 2) {
+                                    const f32x2 v2 = (f32x2{acc[a][j][4 * gq + e], acc[a][j][4 * gq + e + 1]} + f32x2{bv[e], bv[e + 1]}) +
+                                                     f32x2{rv[e], rv[e + 1]};
+                                    const f32x2 r2 = v2 * f32x2{0.15915494309189535f, 0.15915494309189535f};
+#pragma unroll
+                                    for (int u = 0; u < 2; ++u) {
+                                        y[e + u] = __builtin_amdgcn_sinf(r2[u]);
+                                        if constexpr (save) c[e + u] = __builtin_amdgcn_cosf(r2[u]);
+                                    }
+                                }
+                            } else {
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) {
+                                    // (acc + bias) + row, as the layer-by-layer epilogue adds them
+                                    const float v = (acc[a][j][4 * gq + e] + bv[e]) + rv[e];
+                                    const float x = w0 * v;
+                                    if constexpr (save) {
+                                        fast_sincos(x, &y[e], &c[e]);
+                                        c[e] = w0 * c[e];
+                                    } else {
+                                        y[e] = fast_sin(x);
+                                    }
                                 }
                             }
                             *reinterpret_cast<u32x2*>(smem + act_off(row, (fa + 8 * gq) >> 3) + 8 * eh) =

@@ -406,26 +406,44 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
                 const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
-                const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(Ds + p0 * TW, 0, rows * TW * 2, 0x00020000);
+                // (dbg 1, no copy-outs: an empty range drops every store — no branch around them)
+                const __amdgpu_buffer_rsrc_t dr =
+                    __builtin_amdgcn_make_buffer_rsrc(Ds + p0 * TW, 0, (g.dbg & 1) ? 0 : rows * TW * 2, 0x00020000);
+                // act_off(32j + er32, 8w + 4a + gq) + 8eh without per-piece index math: the row's
+                // swizzle (row & 15 = er32 & 15) only touches the chunk's low 4 bits
+                char* lbase = smem + er32 * 1024 + 256 * (w >> 1) + 8 * eh;
+                const int sw4 = er32 & 15, c8 = 8 * (w & 1);
 #pragma unroll
                 for (int a = 0; a < 2; ++a) {
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
-                        const int row = 32 * j + er32;
                         u32x2 cq[4];
 #pragma unroll
                         for (int gq = 0; gq < 4; ++gq) {
                             const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
                             const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + f0);
                             float y[4], c[4];
+                            if constexpr (w0 == 1.f && SPN_PK_EPI) {
+                                // (acc + b) · 1/2π as packed pairs: the same two roundings per
+                                // element as fast_sincos's, half the VALU issue slots
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) {
-                                const float v = acc[a][j][4 * gq + e] + bv[e];
-                                const float x = w0 == 1.f ? v : w0 * v;
-                                fast_sincos(x, &y[e], &c[e]);
-                                if (w0 != 1.f) c[e] = w0 * c[e];
+                                for (int e = 0; e < 4; e += 2) {
+                                    const f32x2 v2 = f32x2{acc[a][j][4 * gq + e], acc[a][j][4 * gq + e + 1]} + f32x2{bv[e], bv[e + 1]};
+                                    const f32x2 r2 = v2 * f32x2{0.15915494309189535f, 0.15915494309189535f};
+                                    y[e] = __builtin_amdgcn_sinf(r2[0]);
+                                    y[e + 1] = __builtin_amdgcn_sinf(r2[1]);
+                                    c[e] = __builtin_amdgcn_cosf(r2[0]);
+                                    c[e + 1] = __builtin_amdgcn_cosf(r2[1]);
+                                }
+                            } else {
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) {
+                                    const float v = acc[a][j][4 * gq + e] + bv[e];
+                                    fast_sincos(w0 * v, &y[e], &c[e]);
+                                    c[e] = w0 * c[e];
+                                }
                             }
-                            *reinterpret_cast<u32x2*>(smem + act_off(row, f0 >> 3) + 8 * eh) =
+                            *reinterpret_cast<u32x2*>(lbase + j * 32768 + (((c8 + 4 * a + gq) ^ sw4) << 4)) =
                                 u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
                             cq[gq] = u32x2{pack2(c[0], c[1]), pack2(c[2], c[3])};
                         }
@@ -439,9 +457,8 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                             }
                             // lanes 0..31: features 8k..8k+7 of the pair, lanes 32..63: 8k+8..8k+15
                             const int fb = 64 * w + 32 * a + 8 * k + 8 * eh;
-                            if (!(g.dbg & 1))  // block-uniform (ablation: no copy-outs)
-                                __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]},
-                                                                       dr, (row * TW + fb) * 2, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]},
+                                                                       dr, ((32 * j + er32) * TW + fb) * 2, 0, 0);
                         }
                     }
                     __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
