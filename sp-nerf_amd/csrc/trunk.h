@@ -164,6 +164,7 @@ extern int g_trunk2_tile;  // 64 or 128 points per tile
 bool trunk2_supported(const TrunkArgs& a, bool save);
 int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, double bytes);
 int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes);
+extern int g_trunk_bwd_dreg;  // the fused dX chain stores dZ from the epilogue's registers
 extern int g_fused_bwd;  // 1 = the bf16 training backward runs its dX chain in k_trunk_bwd_bf16
 
 }  // namespace spn

@@ -509,6 +509,10 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 // before the epilogue; dZ_i leaves for HBM (the weight gradients read it) behind the NEXT
 // layer's MFMAs, which read the same image.  Per point and layer: 1 KB of D in, 1 KB of dZ out
 // (the layer-by-layer GEMM also re-reads dZ_i: 3 KB).
+// DREG (option trunk_bwd_dreg, off: measured slower): dZ_{i-1} also leaves straight from the epilogue's registers
+// (permlane32-joined 16-B buffer stores, as the forward's D) instead of from the image behind the
+// next layer's k-loop, which then streams only the D rows and the weights.
+template <bool DREG>
 __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntiles) {
     using Geo = TrunkGeo<64>;
     constexpr int TMt = 64, NJ = Geo::NJ, IMG = Geo::IMG, CPT = Geo::CPT, TPD = Geo::TPD;
@@ -667,7 +671,45 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
             }
             if (i > 1) load_d(i - 2);  // block-uniform
             __syncthreads();  // every wave is done reading dZ_i; the D image is complete
-            {
+            if constexpr (DREG) {
+                const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
+                const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
+                // (dbg 1, no copy-outs: an empty range drops every store)
+                const __amdgpu_buffer_rsrc_t dr =
+                    __builtin_amdgcn_make_buffer_rsrc(ka->dZ[i - 1] + p0 * TW, 0, (g.dbg & 1) ? 0 : rows * TW * 2, 0x00020000);
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        const int row = 32 * j + er32;
+                        u32x2 cq[4];
+#pragma unroll
+                        for (int gq = 0; gq < 4; ++gq) {
+                            const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                            const int o = act_off(row, f0 >> 3) + 8 * eh;
+                            const f32x4 dm = ld4(reinterpret_cast<const bf16*>(smem + IMG + o));
+                            float v[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] * dm[e];
+                            cq[gq] = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+                            *reinterpret_cast<u32x2*>(smem + o) = cq[gq];
+                        }
+#pragma unroll
+                        for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+                            for (int e = 0; e < 2; ++e) {
+                                const auto r = __builtin_amdgcn_permlane32_swap(cq[k][e], cq[k + 1][e], false, false);
+                                cq[k][e] = r[0];
+                                cq[k + 1][e] = r[1];
+                            }
+                            const int fb = 64 * w + 32 * a + 8 * k + 8 * eh;
+                            __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]}, dr,
+                                                                   (row * TW + fb) * 2, 0, 0);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            } else {
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
@@ -687,19 +729,25 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
                         __builtin_amdgcn_sched_barrier(0);
                     }
             }
-            pend = ka->dZ[i - 1];
+            pend = DREG ? nullptr : ka->dZ[i - 1];
         }
         __syncthreads();  // dZ_0 is complete
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             if (g.rs_layer[k] == 0) colsum(g.Rsum[k] + tile * TW);  // block-uniform
+        if constexpr (!DREG) {
 #pragma unroll
-        for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(pend, p0, q0, std::integral_constant<int, 4>{});
+            for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(pend, p0, q0, std::integral_constant<int, 4>{});
+        }
         __syncthreads();  // the next tile restages the image
     }
 }
 
 int g_fused_bwd = 1;
+// k_trunk_bwd_bf16<true>: dZ stored from the epilogue's registers — measured SLOWER (C4: dX chain
+// 5.05-5.10 -> 5.25-5.27 ms per step, C4@512 4.42 -> 4.47 ms): unlike the forward's sin/cos, the
+// x D epilogue is too short to cover the stores, which then hold up the next k-loop's refills
+int g_trunk_bwd_dreg = 0;
 
 int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes) {
     SPN_ARG(a.P >= 0 && a.L >= 2 && a.L <= kTrunkMaxL, "trunk_bwd_bf16: bad sizes (P=%lld L=%d)", (long long)a.P, a.L);
@@ -715,7 +763,8 @@ int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double
     TrunkBwdArgs ad = a;
     ad.dbg = g_trunk_dbg;
     ProfScope prof("trunk_bwd_bf16", s, flop, bytes);
-    hipLaunchKernelGGL(k_trunk_bwd_bf16, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    if (g_trunk_bwd_dreg) hipLaunchKernelGGL(k_trunk_bwd_bf16<true>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else hipLaunchKernelGGL(k_trunk_bwd_bf16<false>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

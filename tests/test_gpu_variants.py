@@ -220,3 +220,19 @@ def test_bf16_tn_k64_agrees(n, ns):
         assert torch.isfinite(g1[k]).all(), k
         scale = g0[k].abs().max().item()
         assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
+
+
+@pytest.mark.parametrize("n,ns", [(300, 64), (301, 40), (1, 16)])
+def test_bf16_fused_backward_register_dz_bitwise_equal(n, ns):
+    """The fused dX chain storing each dZ from its epilogue's registers (option trunk_bwd_dreg 1;
+    measured slower, off by default) against the copy-out from the LDS image behind the next
+    k-loop (0, the default): the same
+    values in the same rows — renders and gradients bit for bit (ragged and half-empty tiles)."""
+    r0, g0 = _render_bf16({"trunk_bwd_dreg": 0}, n=n, ns=ns)
+    r1, g1 = _render_bf16({"trunk_bwd_dreg": 1}, n=n, ns=ns)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    assert sorted(g0) == sorted(g1)
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        assert torch.equal(g0[k], g1[k]), k
