@@ -99,6 +99,9 @@ __device__ __forceinline__ u32x4 pack8(const float (&f)[8]) {
 // as LLVM lowers native sin for gfx9 (whose sine unit reduces the full input range itself: no
 // v_fract, unlike GCN1-3).  Absolute error ~1e-6 for |x| < 1e3, far below the bf16 rounding of
 // the result (2^-9 relative).
+#ifndef SPN_PK_EPI
+#define SPN_PK_EPI 1  // sine epilogues: (acc + b [+ row]) · 1/2π as packed fp32 pairs (0: scalar, A/B builds)
+#endif
 __device__ __forceinline__ float revs(float x) { return x * 0.15915494309189535f; }
 __device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
     const float r = revs(x);

@@ -7,10 +7,6 @@ namespace spn {
 
 constexpr int kTrunkMaxL = 16;
 
-#ifndef SPN_PK_EPI
-#define SPN_PK_EPI 1  // sine epilogues: (acc + b [+ row]) · 1/2π as packed fp32 pairs (0: scalar, A/B builds)
-#endif
-
 // fc_net layers 1 .. L-1 over P points: H1 (layer-0 output, [P][512] bf16) in, the output of
 // layer i to Hs[i] and its derivative cos(z) (with zround: Z itself) to Ds[i] where non-null
 // (the last layer's Hs is required).  The skip layer reads [H | X0b] and adds the per-ray rows rb_skip[p / S].

@@ -17,7 +17,7 @@ RUNS = sys.argv[3:] or ["c4:4096", "c5:32768"]
 # rocprof kernel name → the library's profiling class (one class per kernel function)
 CLASSES = [(r"k_gemm_nt_bf16d<true", "gemm_nt_bf16d_dmul"), (r"k_gemm_nt_bf16d<", "gemm_nt_bf16d"),
            (r"k_gemm_nt_bf16w", "gemm_nt_bf16w"), (r"k_gemm_nt_bf16<", "gemm_nt_bf16"),
-           (r"k_gemm_tn_bf16d", "gemm_tn_bf16d"), (r"k_gemm_tn_bf16w", "gemm_tn_bf16w"), (r"k_gemm_tn_bf16\b", "gemm_tn_bf16"),
+           (r"k_gemm_tn_bf16_k64", "gemm_tn_bf16k"), (r"k_gemm_tn_bf16d", "gemm_tn_bf16d"), (r"k_gemm_tn_bf16w", "gemm_tn_bf16w"), (r"k_gemm_tn_bf16\b", "gemm_tn_bf16"),
            (r"k_gemm_nt_w<|k_gemm_nt<", "gemm_nt_f32"), (r"k_gemm_tn<", "gemm_tn_f32"),
            (r"k_trunk_bf16<128", "trunk_bf16"), (r"k_trunk_bf16<64", "trunk_bf16_train"),
            (r"k_trunk2_bf16<\d+, (true|false), true", "trunk_bf16_train"), (r"k_trunk2_bf16<", "trunk_bf16"),
