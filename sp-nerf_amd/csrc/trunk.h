@@ -40,7 +40,7 @@ struct TrunkArgs {
     int64_t P = 0;
     int S = 1, L = 0, skip = -1, K0p = 0;
     int dbg = 0;  // set from g_trunk_dbg by trunk_bf16
-    int nt = 0;   // set from g_trunk_nt: non-temporal copy-out stores of H
+    int nt = 0;   // set from g_trunk_nt: 1 = non-temporal copy-out stores of H, 2 = of the register-D stores
     // layers >= 1 (w0 = 1): H = sin(Z), Z = the pre-activation rounded to fp16; when saving, Ds[i]
     // receives Z as fp16 (consumers recompute cos(Z) and sin(Z)) and Hs[i] may be null
     int zround = 0;
@@ -149,7 +149,7 @@ extern int g_trunk_tile;   // 0 = tile by mode; 64 / 128 = force
 extern int g_trunk_dbg;    // profiling ablations (outputs invalid): 1 = no HBM copy-outs
 extern int g_trunk_var;    // profiling ablations of the 128-point trunk (outputs invalid)
 extern int g_trunk_dreg;   // 64-point training tiles: D stored from the registers in the epilogue
-extern int g_trunk_nt;     // 1 = trunk H stores non-temporal, 2 = fused heads' H loads non-temporal
+extern int g_trunk_nt;     // 1 = trunk H stores non-temporal, 2 = fused heads' H loads non-temporal, 4 = training D stores
 bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 // layer 0 inside the launch (TrunkArgs::X0) for this PE width when saving / not saving
 bool trunk_l0_supported(int K0p, bool save);

@@ -50,7 +50,8 @@ int g_trunk_dreg = 1;  // 64-point training tiles: D = cos leaves from the accum
                        // epilogue on 128-point training tiles (no D image needed: 148 KB of LDS)
                        // measured 3.65 ms per 524 288 points against 2.96 (64) and 3.13 (128 with the
                        // two-barrier cos pass): 128 KB of D stores per epilogue hold up the refills
-int g_trunk_dbg = 0;   // profiling ablations, outputs invalid when set: 1 = skip the HBM copy-outs,
+int g_trunk_dbg = 0;   // profiling ablations, outputs invalid when set: 1 = skip the HBM copy-outs
+                       // (4 = only the register-D stores, 8 = only the H copy-outs in the k-loop),
                        // (options trunk_var 16 / 32: no MFMAs in the main k-loop / no sine in the
                        // inference epilogue)
 
@@ -133,12 +134,12 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             const int c = ct + 512 * (q0 + q);
 #if SPN_TRUNK_BUFSTORE
             const int off = ((c >> 6) * TW + (c & 63) * 8) * 2;
-            if (g.nt) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // block-uniform: glc slc
+            if (g.nt & 1) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // block-uniform: glc slc
             else __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 0);
 #else  // A/B build: the guarded stores
             if (p0 + (c >> 6) < g.P) {
                 u32x4* o = reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8);
-                if (g.nt) __builtin_nontemporal_store(v[q], o);
+                if (g.nt & 1) __builtin_nontemporal_store(v[q], o);
                 else *o = v[q];
             }
 #endif
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 // drain the previous layer's outputs: CPT / (nmain / TPD) chunks per thread
                 constexpr int per = CPT / (nmain / TPD);
                 static_assert(per * (nmain / TPD) == CPT && per >= 1, "copy slices");
-                if (hpend && !(g.dbg & 1)) copy_out(smem, hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                if (hpend && !(g.dbg & 9)) copy_out(smem, hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
                 if (Geo::DIMG && dpend && !(g.dbg & 1)) copy_out(smem + IMG, dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
             }
             // the x0 columns of the skip layer's input [h | x0] (nks == nmain elsewhere)
@@ -411,7 +412,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
                 // (dbg 1, no copy-outs: an empty range drops every store — no branch around them)
                 const __amdgpu_buffer_rsrc_t dr =
-                    __builtin_amdgcn_make_buffer_rsrc(Ds + p0 * TW, 0, (g.dbg & 1) ? 0 : rows * TW * 2, 0x00020000);
+                    __builtin_amdgcn_make_buffer_rsrc(Ds + p0 * TW, 0, (g.dbg & 5) ? 0 : rows * TW * 2, 0x00020000);
                 // act_off(32j + er32, 8w + 4a + gq) + 8eh without per-piece index math: the row's
                 // swizzle (row & 15 = er32 & 15) only touches the chunk's low 4 bits
                 char* lbase = smem + er32 * 1024 + 256 * (w >> 1) + 8 * eh;
@@ -460,8 +461,15 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                             }
                             // lanes 0..31: features 8k..8k+7 of the pair, lanes 32..63: 8k+8..8k+15
                             const int fb = 64 * w + 32 * a + 8 * k + 8 * eh;
-                            __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]},
-                                                                       dr, ((32 * j + er32) * TW + fb) * 2, 0, 0);
+                            // (option trunk_nt bit 4: glc slc — measured 3.50-3.57 against 2.92 ms per
+                            // 524 288 points: without L2 write-combining the 32-B row pieces reach HBM
+                            // as partial lines.  H non-temporal, bit 1: 2.88 against 2.92, not default)
+                            if (g.nt & 2)  // block-uniform
+                                __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]},
+                                    dr, ((32 * j + er32) * TW + fb) * 2, 0, 3);
+                            else
+                                __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]},
+                                    dr, ((32 * j + er32) * TW + fb) * 2, 0, 0);
                         }
                     }
                     __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
@@ -800,7 +808,7 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
             a.K0p);
     TrunkArgs ad = a;
     ad.dbg = g_trunk_dbg;
-    ad.nt = g_trunk_nt & 1;
+    ad.nt = (g_trunk_nt & 1) | ((g_trunk_nt & 4) ? 2 : 0);  // H copy-outs / register-D stores non-temporal
     const int ntiles = cdiv(a.P, tm);
     // the saving 64-point tiling (training) is its own profiling class: its roofline (HBM-heavy,
     // H and D of every layer out) is not the inference tiling's (MFMA-bound)
