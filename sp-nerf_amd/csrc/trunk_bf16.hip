@@ -43,7 +43,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 int g_fused_trunk = 1;
 int g_trunk_tile = 0;  // 0 = by mode (64 when saving, else 128); 64 / 128 force a tiling (A/B runs)
-int g_trunk_nt = 0;
+// bit 1: the training trunk's H copy-outs non-temporal (glc slc), the default: C4@512 4.41 -> 4.30 and
+// 4.18 / 4.20 -> 4.09 / 4.09 ms, C4 26.63 / 26.64 -> 26.60 / 26.57, C3 7.36 -> 7.26, C5 level (pairs in
+// one call each, tools/gpu_r3u.sh, tools/gpu_r3v.sh); bit 4: the register-D
+// stores too (slower); bit 2: the fused heads' H loads
+int g_trunk_nt = 1;
 int g_trunk_var = 0;  // profiling ablations of the 128-point tiling (k_trunk_bf16 VAR)
 int g_trunk_dreg = 1;  // 64-point training tiles: D = cos leaves from the accumulators in the epilogue
                        // (VAR 512) instead of through the D image behind the next k-loop.  The same
