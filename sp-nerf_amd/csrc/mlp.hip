@@ -1928,6 +1928,7 @@ static int* option_slot(const char* name) {
     if (n == "trunk_var") return &g_trunk_var;
     if (n == "trunk_dreg") return &g_trunk_dreg;
     if (n == "trunk_bwd_dreg") return &g_trunk_bwd_dreg;
+    if (n == "trunk_bwd_nt") return &g_trunk_bwd_nt;
     if (n == "heads_dbg") return &g_heads_dbg;
     if (n == "nt_f32_variant") return &g_nt_variant;
     if (n == "tn_f32_variant") return &g_tn_variant;

@@ -65,6 +65,7 @@ struct TrunkBwdArgs {
     int64_t P = 0;
     int L = 0;
     int dbg = 0;  // g_trunk_dbg (profiling ablations, outputs invalid): 1 = no dZ copy-outs, 2 = no D loads
+    int nt = 0;   // g_trunk_bwd_nt: 1 = non-temporal dZ copy-outs, 2 = non-temporal D loads
     // per-tile column sums of dZ_l for l = rs_layer[k] (-1: none) into Rsum[k][tile][512]: the
     // per-ray sums of layer 0's and the skip layer's dZ (semantic columns) from the LDS image
     // instead of a re-read of dZ (k_ray_rowsum16).  Needs P % 64 == 0; the order is tile_colsum's
@@ -160,6 +161,7 @@ extern int g_trunk2_tile;  // 64 or 128 points per tile
 bool trunk2_supported(const TrunkArgs& a, bool save);
 int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, double bytes);
 int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes);
+extern int g_trunk_bwd_nt;    // the dX chain's non-temporal dZ stores (1) / D loads (2)
 extern int g_trunk_bwd_dreg;  // the fused dX chain stores dZ from the epilogue's registers
 extern int g_fused_bwd;  // 1 = the bf16 training backward runs its dX chain in k_trunk_bwd_bf16
 

@@ -560,7 +560,11 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
 #pragma unroll
         for (int q = 0; q < n; ++q) {
             const int c = ct + 512 * (q0 + q);
-            if (p0 + (c >> 6) < g.P) *reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8) = v[q];
+            if (p0 + (c >> 6) < g.P) {
+                u32x4* o = reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8);
+                if (g.nt & 1) __builtin_nontemporal_store(v[q], o);  // block-uniform (option trunk_bwd_nt)
+                else *o = v[q];
+            }
         }
     };
     // per-tile column sums of the image (dZ_l, complete: called after a barrier, by every thread)
@@ -613,7 +617,8 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
 #pragma unroll
             for (int q = 0; q < CPT; ++q) {
                 const int c = st + 512 * q;
-                dv[q] = ldg16(dsrc + std::min<int64_t>(p0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
+                const u32x4* src = reinterpret_cast<const u32x4*>(dsrc + std::min<int64_t>(p0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
+                dv[q] = (g.nt & 2) ? __builtin_nontemporal_load(src) : *src;  // block-uniform
             }
         };
         load_d(g.L - 2);
@@ -763,6 +768,9 @@ int g_fused_bwd = 1;
 // 5.05-5.10 -> 5.25-5.27 ms per step, C4@512 4.42 -> 4.47 ms): unlike the forward's sin/cos, the
 // x D epilogue is too short to cover the stores, which then hold up the next k-loop's refills
 int g_trunk_bwd_dreg = 0;
+// dX chain: 1 = non-temporal dZ copy-outs, 2 = non-temporal D loads — level either way (C4 26.27 /
+// 26.27 / 26.22 / 26.23 ms for 0 / 1 / 2 / 3, C4@512 4.09 / 4.08 / 4.09 / 4.10: tools/gpu_r3w.sh)
+int g_trunk_bwd_nt = 0;
 
 int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes) {
     SPN_ARG(a.P >= 0 && a.L >= 2 && a.L <= kTrunkMaxL, "trunk_bwd_bf16: bad sizes (P=%lld L=%d)", (long long)a.P, a.L);
@@ -777,6 +785,7 @@ int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double
     const int ntiles = cdiv(a.P, 64);
     TrunkBwdArgs ad = a;
     ad.dbg = g_trunk_dbg;
+    ad.nt = g_trunk_bwd_nt;
     ProfScope prof("trunk_bwd_bf16", s, flop, bytes);
     if (g_trunk_bwd_dreg) hipLaunchKernelGGL(k_trunk_bwd_bf16<true>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else hipLaunchKernelGGL(k_trunk_bwd_bf16<false>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
