@@ -461,6 +461,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_bf16w(NT16Args g, in
 // Same k order as k_gemm_nt_bf16w (16-wide k blocks in increasing k): bit-identical outputs.
 // K and K1 must be multiples of 32 (host-checked).
 constexpr int ND_K = 32, ND_STAGES = 4, ND_STG = 512 * 64;
+#ifndef SPN_NT16_NT
+// the DMA NT GEMM's C / Dout stores non-temporal (glc slc; A/B builds): C4 26.20 / 26.19 -> 26.13 /
+// 26.11 ms, C4@512 level (tools/gpu_r3x.sh) — within the box's spread, so off
+#define SPN_NT16_NT 0
+#endif
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 #ifdef ND_STAMPS
 // diagnostic build only (tools/gemm_bench_bf16 -DND_STAMPS): lane 0 of waves 0 and 4 of block 0
@@ -775,10 +780,10 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             for (int q4 = 0; q4 < 4; ++q4) {
                 const int lr = wr * 128 + erow + i * 32 + 8 * q4;   // row within the tile
                 const uint32_t oc_off = colok ? (uint32_t)(((int64_t)lr * g.ldc + col) * 2) : 0x7FFFFFF0u;
-                __builtin_amdgcn_raw_buffer_store_b128(oc[q4], rsC, oc_off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(oc[q4], rsC, oc_off, 0, SPN_NT16_NT ? 3 : 0);
                 if constexpr (!DM && !R1D) {
                     const uint32_t od_off = (colok && sine_cols) ? (uint32_t)(((int64_t)lr * g.ld_dout + col) * 2) : 0x7FFFFFF0u;
-                    __builtin_amdgcn_raw_buffer_store_b128(od[q4], rsD, od_off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(od[q4], rsD, od_off, 0, SPN_NT16_NT ? 3 : 0);
                 }
             }
             ND_STAMP(8);
