@@ -743,21 +743,24 @@ def run_train(a, config, rank, world, dev, secondary=False):
         """render + losses + backward for the batch in idx_s / gidx_s (grads are written, not
         accumulated: the caller clears them before an eager call)."""
         idx, gidx = idx_s, gidx_s
+        # each per-ray field gathered once, shared by the render and the loss (the guided clamp's
+        # global first ray is this batch's first row on one rank)
         rays = R["rays"][idx]
+        depths, valid, dstd = R["depths"][idx], R["valid_depth"][idx], R["depth_std"][idx]
         kw = {}
         if c["guided"]:
-            kw = dict(valid_depth=R["valid_depth"][idx], target_depths=R["depths"][idx], target_std=R["depth_std"][idx],
-                      clamp_near_far=R["rays"].index_select(0, gidx[:1])[0, 6:8])
+            first = rays[0, 6:8] if world == 1 else R["rays"].index_select(0, gidx[:1])[0, 6:8]
+            kw = dict(valid_depth=valid, target_depths=depths, target_std=dstd, clamp_near_far=first)
         sem = R["sems"][idx] if c["sem"] else None
         res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sem, mode="train", **kw)
         if floss is not None:   # the trainer's loss sum (main.py:143-174) in two kernels
-            loss, _ = floss(res, R["rgbs"][idx], R["depths"][idx], R["valid_depth"][idx], R["depth_std"][idx], sem,
+            loss, _ = floss(res, R["rgbs"][idx], depths, valid, dstd, sem,
                             labels_global=R["sems"][gidx] if (world > 1 and sem is not None) else None, world=world)
             loss.backward()
             return loss.detach()
         loss, _ = sloss(res, R["rgbs"][idx])
         if dloss is not None:
-            loss = loss + dloss(res, R["depths"][idx, 0], R["depths"][idx, 1], R["valid_depth"][idx], R["depth_std"][idx])[0]
+            loss = loss + dloss(res, depths[:, 0], depths[:, 1], valid, dstd)[0]
         if semloss is not None:
             sl = semloss(res, sem)[0]
             loss = loss + (dp.shard_ce(sl, sem, R["sems"][gidx], world) if world > 1 else sl)
