@@ -144,7 +144,10 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(T
 #pragma unroll
         for (int q = 0; q < n; ++q) {
             const int c = ct + NT * (q0 + q);
-            __builtin_amdgcn_raw_buffer_store_b128(v[q], r, (c >> 6) * ROWB + (c & 63) * 16, 0, 0);
+            if (SAVE && (g.nt & 1))  // block-uniform: non-temporal H copy-outs of training (trunk_nt 1)
+                __builtin_amdgcn_raw_buffer_store_b128(v[q], r, (c >> 6) * ROWB + (c & 63) * 16, 0, 3);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(v[q], r, (c >> 6) * ROWB + (c & 63) * 16, 0, 0);
         }
     };
 
@@ -451,6 +454,7 @@ int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, d
     const int ntiles = cdiv(a.P, TM);
     TrunkArgs ad = a;
     ad.dbg = g_trunk_dbg;
+    ad.nt = save ? (g_trunk_nt & 1) : 0;
     const bool l0 = a.X0 || a.rays;
     if (!l0) ad.rb0 = nullptr;
     ProfScope prof(save ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
