@@ -378,22 +378,6 @@ int g_l0_split = 1;       // bf16 MLP: fc_net.0 on bf16 hi/lo planes (0 = fp32 M
 int g_trunk_l0 = 1;       // ... and inside the fused trunk launch: 1 = when nothing is saved (inference;
                           // saving, 64-point tiles, it measured slower than the separate GEMM), 2 = always
 
-// Sum over the wavefront, returned to every lane: DPP adds inside each row of 16 lanes, then
-// the four row sums read out as scalars (no LDS traffic, unlike a shuffle butterfly).
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float wave_total(float v) {
-    v += dpp_f<0xb1>(v);   // quad_perm [1,0,3,2]
-    v += dpp_f<0x4e>(v);   // quad_perm [2,3,0,1]
-    v += dpp_f<0x124>(v);  // row_ror:4
-    v += dpp_f<0x128>(v);  // row_ror:8
-    const int b = __float_as_int(v);
-    return (__int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16))) +
-           (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
-}
-
 template <typename T> struct RawOf;
 template <> struct RawOf<float> { using type = f32x4; };
 template <> struct RawOf<bf16> { using type = u32x2; };
@@ -401,18 +385,13 @@ template <typename T>
 __device__ __forceinline__ typename RawOf<T>::type ld_raw(const T* p) {
     return *reinterpret_cast<const typename RawOf<T>::type*>(p);
 }
-__device__ __forceinline__ f32x4 raw_f32(f32x4 v) { return v; }
-__device__ __forceinline__ f32x4 raw_f32(u32x2 v) {
-    return f32x4{__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u), __uint_as_float(v[1] << 16),
-                 __uint_as_float(v[1] & 0xffff0000u)};
-}
-__device__ __forceinline__ float dot4(f32x4 a, f32x4 b) { return (a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3]); }
 
 // The rows one point's heads read: its last trunk row (σ), sun_v.3 output, rgb / β hidden
 // (Q) and semantic hidden (G); lane `l` holds columns 4l + 256i.
 template <typename T, int NC, int NH>
 struct HeadRows {
     typename RawOf<T>::type hl[NC], s3[NH], r1[NH], b1[NH], m1[NH];
+    float sp;  // k_heads_fwd_v<…, SIGB>: the σ pre-activation from hsave
 };
 
 // Narrow output heads (spnerf.py:333-367): σ = softplus, albedo = sigmoid·1.002−0.001,
@@ -424,7 +403,9 @@ struct HeadRows {
 // registers or LDS (σ / sun / rgb / β weights in VGPRs, semantic weights staged in LDS) so no
 // vector-memory load is issued behind the prefetch.  A point's output row leaves as one
 // coalesced store.
-template <typename T, int NC>
+// SIGB: the σ pre-activation comes from hsave[p·8], written by the fused training trunk with this
+// kernel's own arithmetic (TrunkArgs::sig_hsave) — no H_L row is loaded
+template <typename T, int NC, bool SIGB = false>
 __global__ __launch_bounds__(256) void k_heads_fwd_v(HeadsArgs<T> a, PackedOffs k) {
     constexpr int NH = (NC + 1) / 2;
     extern __shared__ float wsem[];  // [C][H] semantic weights + [C] biases (mode 0, semantic model)
@@ -466,16 +447,20 @@ __global__ __launch_bounds__(256) void k_heads_fwd_v(HeadsArgs<T> a, PackedOffs 
     const float br0 = full ? Pk[k.br2] : 0.f, br1 = full ? Pk[k.br2 + 1] : 0.f, br2 = full ? Pk[k.br2 + 2] : 0.f;
     const float bb = beta ? Pk[k.bb2] : 0.f;
 
-    // row bases of point p; unused rows alias the σ row
+    // row bases of point p; unused rows alias the σ row (SIGB: the Q row)
     auto load = [&](int64_t p, HeadRows<T, NC, NH>& r) {
-        const T* hl = a.HL + p * W;
         const T* q = a.Q + p * d.NQ;
+        const T* hl = SIGB ? q : a.HL + p * W;
         const T* s3 = sun_on ? a.S3 + p * H : hl;
         const T* r1 = full ? q + H : hl;
         const T* b1 = beta ? q + 2 * H : hl;
         const T* m1 = sem ? a.G + p * d.NG + W : hl;
+        if constexpr (SIGB) {
+            r.sp = a.hsave[p * 8];
+        } else {
 #pragma unroll
-        for (int i = 0; i < NC; ++i) r.hl[i] = ld_raw(hl + cw[i]);
+            for (int i = 0; i < NC; ++i) r.hl[i] = ld_raw(hl + cw[i]);
+        }
 #pragma unroll
         for (int i = 0; i < NH; ++i) {
             r.s3[i] = ld_raw(s3 + ch[i]);
@@ -492,8 +477,10 @@ __global__ __launch_bounds__(256) void k_heads_fwd_v(HeadsArgs<T> a, PackedOffs 
         load(std::min(p + nw, a.P - 1), nxt);
         // lane-partial dot products (masked columns carry zero weights)
         float ps = 0.f, pu = 0.f, pr0 = 0.f, pr1 = 0.f, pr2 = 0.f, pb = 0.f;
+        if constexpr (!SIGB) {
 #pragma unroll
-        for (int i = 0; i < NC; ++i) ps += dot4(raw_f32(cur.hl[i]), wsg[i]);
+            for (int i = 0; i < NC; ++i) ps += dot4(raw_f32(cur.hl[i]), wsg[i]);
+        }
 #pragma unroll
         for (int i = 0; i < NH; ++i) {
             pu += dot4(raw_f32(cur.s3[i]), w4[i]);
@@ -503,7 +490,7 @@ __global__ __launch_bounds__(256) void k_heads_fwd_v(HeadsArgs<T> a, PackedOffs 
             pr2 += dot4(r, wr[2][i]);
             pb += dot4(raw_f32(cur.b1[i]), wb[i]);
         }
-        const float spre = wave_total(ps) + bsig;
+        const float spre = SIGB ? cur.sp : wave_total(ps) + bsig;
         float ov = lane == 3 ? softplusf_(spre) : 0.f;  // this lane's output column
         float hv = spre;                                // this lane's hsave column (lane 0: σ pre-activation)
         float* o = a.out + p * d.NO;
@@ -1306,7 +1293,7 @@ static bool trunk_l0_on(const Ctx& c, bool save) {
 }
 
 template <typename T>
-static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
+static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, bool* sig_done) {
     using G = Gemms<T>;
     using NT = typename G::NT;
     const Dims& d = c.d;
@@ -1346,6 +1333,14 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s) {
             a.rb_skip = d.sem ? c.at(c.w.rb4) : nullptr;
             a.P = P; a.S = S; a.L = d.L; a.skip = d.skip; a.K0p = d.K0p;
             a.zround = zs ? 1 : 0;
+            // the σ head's pre-activation from the last layer's LDS image (the wave-per-point
+            // heads then skip H_L); option trunk_sigma
+            if (sig_done && !heads_fused_on(c, save, mode) && g_heads_variant != 0 && W == 512 && trunk_sigma_ok(a, save)) {
+                a.sig_hsave = c.at(c.w.hsave);
+                a.wsig = c.pk(c.k.wsig);
+                a.bsig = c.pk(c.k.bsig);
+                *sig_done = true;
+            }
             // algorithmic HBM bytes: the first layer's input (fp32 PE, or H_1 and the bf16 PE)
             // in; out when saving H and D of every layer, or Z of every layer and the last H
             const double in = first == 0 ? (a.rays ? 4.0 * P : 4.0 * P * d.K0p) : 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0));
@@ -1492,8 +1487,9 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
                            d.bf ? c.hb(c.w.X0b) : nullptr, planes ? c.hb(c.w.X0s) : nullptr);
         SPN_HIP(hipGetLastError());
     }
-    if (d.bf) SPN_TRY(forward_gemms<bf16>(c, save, mode, s));
-    else SPN_TRY(forward_gemms<float>(c, save, mode, s));
+    bool sig_done = false;  // hsave[p·8] (σ pre-activation) written by the fused trunk
+    if (d.bf) SPN_TRY(forward_gemms<bf16>(c, save, mode, s, &sig_done));
+    else SPN_TRY(forward_gemms<float>(c, save, mode, s, nullptr));
     if (heads_fused_on(c, save, mode)) {
         const int64_t hl = c.w.Hb[(d.L - 1) & 1];
         HeadsFusedArgs a;
@@ -1516,6 +1512,10 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
         const size_t lds = mode == 0 && d.sem ? sizeof(float) * d.C * (H + 1) : 0;  // ≤ 32 × 513 floats when nc ≤ 4
         auto launch = [&](auto a) {
             using T = std::remove_cv_t<std::remove_pointer_t<decltype(a.HL)>>;
+            if (sig_done && nc == 2) {  // σ from hsave (W = 512, bf16)
+                hipLaunchKernelGGL((k_heads_fwd_v<T, 2, true>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k);
+                return;
+            }
             switch (nc) {
                 case 1: hipLaunchKernelGGL((k_heads_fwd_v<T, 1>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k); break;
                 case 2: hipLaunchKernelGGL((k_heads_fwd_v<T, 2>), dim3(grid), dim3(256), lds, s, a, (PackedOffs)c.k); break;
@@ -1929,6 +1929,7 @@ static int* option_slot(const char* name) {
     if (n == "trunk_dreg") return &g_trunk_dreg;
     if (n == "trunk_bwd_dreg") return &g_trunk_bwd_dreg;
     if (n == "trunk_bwd_nt") return &g_trunk_bwd_nt;
+    if (n == "trunk_sigma") return &g_trunk_sigma;
     if (n == "heads_dbg") return &g_heads_dbg;
     if (n == "nt_f32_variant") return &g_nt_variant;
     if (n == "tn_f32_variant") return &g_tn_variant;

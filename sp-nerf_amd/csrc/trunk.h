@@ -27,6 +27,29 @@ __device__ __forceinline__ float pe_value(const float* ray, int dir_off, float z
     return j < 3 ? sinf(arg) : cosf(arg);
 }
 
+// Sum over the wavefront, returned to every lane: DPP adds inside each row of 16 lanes, then
+// the four row sums read out as scalars (no LDS traffic, unlike a shuffle butterfly).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_total(float v) {
+    v += dpp_f<0xb1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4e>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x124>(v);  // row_ror:4
+    v += dpp_f<0x128>(v);  // row_ror:8
+    const int b = __float_as_int(v);
+    return (__int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16))) +
+           (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
+}
+
+__device__ __forceinline__ f32x4 raw_f32(f32x4 v) { return v; }
+__device__ __forceinline__ f32x4 raw_f32(u32x2 v) {
+    return f32x4{__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u), __uint_as_float(v[1] << 16),
+                 __uint_as_float(v[1] & 0xffff0000u)};
+}
+__device__ __forceinline__ float dot4(f32x4 a, f32x4 b) { return (a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3]); }
+
 struct TrunkArgs {
     const bf16* H1 = nullptr;
     const bf16* X0b = nullptr;
@@ -49,6 +72,12 @@ struct TrunkArgs {
     const float* rays = nullptr;
     const float* z = nullptr;
     int rs = 0, dir_off = 0, n_freq = 0, K0 = 0;
+    // training (64-point tiles, trunk_sigma_ok): the σ head's pre-activation of every point from the
+    // last layer's LDS image, hsave[p·8] = w_σ·H_L + b_σ in k_heads_fwd_v's arithmetic (lane l:
+    // features 4l.. and 256 + 4l.., dot4, wave_total), so the heads kernel skips H_L (1 KB / point)
+    float* sig_hsave = nullptr;
+    const float* wsig = nullptr;  // [512]
+    const float* bsig = nullptr;  // [1]
 };
 
 // Backward dX chain of the bf16 trunk in one persistent launch (k_trunk_bwd_bf16): from
@@ -155,6 +184,9 @@ bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 // layer 0 inside the launch (TrunkArgs::X0) for this PE width when saving / not saving
 bool trunk_l0_supported(int K0p, bool save);
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes);
+// the launch trunk_bf16 would make for a (saving) computes the σ rows (TrunkArgs::sig_hsave)
+bool trunk_sigma_ok(const TrunkArgs& a, bool save);
+extern int g_trunk_sigma;  // option trunk_sigma
 // the two-workgroups-per-CU tiling (trunk2_bf16.hip): D stored from the registers, 76 KB of LDS
 extern int g_trunk2;       // 0 = off, 1 = saving (training) launches, 2 = every launch
 extern int g_trunk2_tile;  // 64 or 128 points per tile

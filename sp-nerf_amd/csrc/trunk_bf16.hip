@@ -157,6 +157,26 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
         for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(img, dst, p0, q0, std::integral_constant<int, 4>{});
     };
 
+    // σ pre-activation of the tile's points from the last layer's image (TrunkArgs::sig_hsave):
+    // wave w takes rows [TMt/8 · w, +TMt/8); lane l the features 4l.. and 256 + 4l.. — the lane
+    // layout, dot4 order and wave_total of k_heads_fwd_v, so hsave[p·8] is bit-identical to it
+    auto sigma_rows = [&](int64_t p0) {
+        const int l = opaque(lane);
+        const f32x4 w0v = ld4(g.wsig + 4 * l), w1v = ld4(g.wsig + 256 + 4 * l);
+        const float bs = *g.bsig;
+#pragma unroll 1
+        for (int r = 0; r < TMt / 8; ++r) {
+            const int row = (TMt / 8) * w + r;
+            const u32x2 h0 = *reinterpret_cast<const u32x2*>(smem + act_off(row, l >> 1) + 8 * (l & 1));
+            const u32x2 h1 = *reinterpret_cast<const u32x2*>(smem + act_off(row, 32 + (l >> 1)) + 8 * (l & 1));
+            float ps = 0.f;
+            ps += dot4(raw_f32(h0), w0v);
+            ps += dot4(raw_f32(h1), w1v);
+            const float spre = wave_total(ps) + bs;
+            if (l == 0 && p0 + row < g.P) g.sig_hsave[(p0 + row) * 8] = spre;
+        }
+    };
+
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
     prime(first, std::integral_constant<int, 0>{}, std::integral_constant<int, TPD>{});
@@ -493,6 +513,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                     __syncthreads();
                     copy_all(smem, Hs, p0);
                     if (Ds && !dreg) copy_all(smem + IMG, Ds, p0);
+                    if (g.sig_hsave) sigma_rows(p0);  // block-uniform
                 }
                 hpend = last ? nullptr : Hs;
                 dpend = last || dreg ? nullptr : Ds;
@@ -802,6 +823,14 @@ static int trunk_tile(bool save) { return g_trunk_tile ? g_trunk_tile : (save ? 
 bool trunk_l0_supported(int K0p, bool save) {
     const int tpd = trunk_tile(save) == 64 ? TrunkGeo<64>::TPD : TrunkGeo<128>::TPD;
     return K0p % 4 == 0 && (K0p / 4) % tpd == 0;  // layer 0's k-loop in whole prefetch rounds
+}
+
+// σ rows from the training trunk's last image (TrunkArgs::sig_hsave): k_heads_fwd_v 0.66 -> 0.56 ms per
+// C4 step (no H_L reads), trunk +0.03 ms, C4 26.83 / 26.77 -> 26.81 / 26.70 ms (tools/gpu_r3zb.sh)
+int g_trunk_sigma = 1;
+
+bool trunk_sigma_ok(const TrunkArgs& a, bool save) {
+    return g_trunk_sigma && save && !a.zround && !trunk2_supported(a, save) && trunk_tile(save) == 64;
 }
 
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes) {

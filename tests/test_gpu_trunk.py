@@ -154,3 +154,16 @@ def test_training_trunk_register_d_bitwise(dims, n_rays, guided, sc, n_samples, 
     opts = {"trunk_l0": l0}
     base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_dreg=0))
     _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_dreg=1)), base)
+
+
+@pytest.mark.parametrize("dims,n_rays,guided,sc,n_samples", [
+    (ModelDims(width=512, sem=True), 257, True, 0.1, 64),   # C3 flags: main (all heads) and solar (σ + sun) passes
+    (ModelDims(width=512), 33, False, 0.1, 32),             # the last 64-point tile half full
+])
+def test_training_trunk_sigma_rows_bitwise(dims, n_rays, guided, sc, n_samples):
+    """The training trunk writing each point's σ pre-activation from its last layer's LDS image
+    (option trunk_sigma 1, the default: k_heads_fwd_v's lane layout, dot4 order and wave_total, so
+    the wave-per-point heads skip H_L) against the heads computing it from H_L (0): renders and
+    gradients bit for bit."""
+    base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 0})
+    _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 1}), base)
