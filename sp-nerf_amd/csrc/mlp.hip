@@ -1506,8 +1506,8 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
         const int64_t hl = save ? c.w.Hb[L] : c.w.Hb[L & 1];
         const int64_t s3 = save ? c.w.S3 : c.w.Hb[2];
         const int grid = (int)std::min<int64_t>(cdiv(P, 4), 8192);
-        ProfScope prof("heads_fwd", s, 2.0 * P * (W + (mode != 1 ? 4 * H + H * d.C : 0)),
-                       (d.bf ? 2.0 : 4.0) * P * (W + 3 * H) + 4.0 * P * d.NO);
+        ProfScope prof("heads_fwd", s, 2.0 * P * ((sig_done ? 0 : W) + (mode != 1 ? 4 * H + H * d.C : 0)),
+                       (d.bf ? 2.0 : 4.0) * P * ((sig_done ? 0 : W) + 3 * H) + 4.0 * P * (d.NO + (sig_done ? 1 : 0)));
         const int nc = g_heads_variant == 0 ? 0 : cdiv(W, 256);
         const size_t lds = mode == 0 && d.sem ? sizeof(float) * d.C * (H + 1) : 0;  // ≤ 32 × 513 floats when nc ≤ 4
         auto launch = [&](auto a) {
