@@ -1465,7 +1465,10 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
 // ------------------------------------------------------------------------------------------
 int g_nt16_variant = 8;
 int g_nt16_ip = 2;  // DMA NT / TN: where a K-step issues the next step's DMAs (0 before its MFMAs, 1 after, 2 between the k-halves)
-int g_tn16_ip = 2;
+// the weight-gradient GEMM: 1 (after a step's MFMAs) re-measured on the final round-3 tree: C4 26.69 /
+// 26.72 / 26.71 -> 26.62 / 26.64 / 26.61 ms, the TN class 6.20 -> 6.09 ms per step, C4@512 level
+// (tools/gpu_r3zf.sh); 2 was the better placement when the TN was measured in isolation (r02)
+int g_tn16_ip = 1;
 int g_tn16_bias_split = 1;
 int g_nt16_ip_gen = 2;  // the same for the general (bias / sine / rank-1) epilogue instances
 int g_nt16_epi = 1;     // option "nt_bf16_epi": 1 = compile-time epilogue variants of the DMA NT, 0 = the generic one
