@@ -33,6 +33,9 @@
 
 #include "trunk.h"
 
+#ifndef SPN_BIAS_HOIST
+#define SPN_BIAS_HOIST 1  // register-D epilogue: the biases of a feature tile read once for both point tiles
+#endif
 #ifndef SPN_TRUNK_BUFSTORE
 #define SPN_TRUNK_BUFSTORE 1  // copy-outs through buffer descriptors (0: guarded stores, A/B builds)
 #endif
@@ -431,6 +434,15 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             // epilogue's VALU work does (HBM was idle through every epilogue); layers with per-ray
             // rows (whose loads would wait behind the stores) or a saved Z keep the D image.
             auto epilogue_dreg = [&](auto kl0) {
+                if constexpr (NOEPI) {  // ablation: keep the accumulators (and so the MFMAs) live
+                    float t = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) t += acc[a][j][0];
+                    if (t == 1234.5f) *reinterpret_cast<float*>(smem + 4 * tid) = t;
+                    return;
+                }
                 constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
                 const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
@@ -443,13 +455,22 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 const int sw4 = er32 & 15, c8 = 8 * (w & 1);
 #pragma unroll
                 for (int a = 0; a < 2; ++a) {
+#if SPN_BIAS_HOIST
+                    // this feature tile's biases once for both point tiles (one LDS read per group)
+                    f32x4 bva[4];
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) bva[gq] = *reinterpret_cast<const f32x4*>(sb + 64 * w + 32 * a + 8 * gq + 4 * eh);
+#endif
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         u32x2 cq[4];
 #pragma unroll
                         for (int gq = 0; gq < 4; ++gq) {
-                            const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
-                            const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + f0);
+#if SPN_BIAS_HOIST
+                            const f32x4 bv = bva[gq];
+#else
+                            const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + 64 * w + 32 * a + 8 * gq + 4 * eh);
+#endif
                             float y[4], c[4];
                             if constexpr (w0 == 1.f && SPN_PK_EPI) {
                                 // (acc + b) · 1/2π as packed pairs: the same two roundings per
@@ -458,10 +479,14 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                                 for (int e = 0; e < 4; e += 2) {
                                     const f32x2 v2 = f32x2{acc[a][j][4 * gq + e], acc[a][j][4 * gq + e + 1]} + f32x2{bv[e], bv[e + 1]};
                                     const f32x2 r2 = v2 * f32x2{0.15915494309189535f, 0.15915494309189535f};
-                                    y[e] = __builtin_amdgcn_sinf(r2[0]);
-                                    y[e + 1] = __builtin_amdgcn_sinf(r2[1]);
-                                    c[e] = __builtin_amdgcn_cosf(r2[0]);
-                                    c[e + 1] = __builtin_amdgcn_cosf(r2[1]);
+                                    if constexpr (NOSIN) {  // ablation (outputs invalid): no transcendentals
+                                        y[e] = r2[0]; y[e + 1] = r2[1]; c[e] = -r2[0]; c[e + 1] = -r2[1];
+                                    } else {
+                                        y[e] = __builtin_amdgcn_sinf(r2[0]);
+                                        y[e + 1] = __builtin_amdgcn_sinf(r2[1]);
+                                        c[e] = __builtin_amdgcn_cosf(r2[0]);
+                                        c[e + 1] = __builtin_amdgcn_cosf(r2[1]);
+                                    }
                                 }
                             } else {
 #pragma unroll
@@ -855,7 +880,11 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     // the saving 64-point tiling (training) is its own profiling class: its roofline (HBM-heavy,
     // H and D of every layer out) is not the inference tiling's (MFMA-bound)
     ProfScope prof(tm == 64 ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
-    if (tm == 64 && g_trunk_dreg) hipLaunchKernelGGL((k_trunk_bf16<64, 512>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    if (tm == 64 && g_trunk_dreg && g_trunk_var == 32)  // ablation: no sin / cos in the epilogue
+        hipLaunchKernelGGL((k_trunk_bf16<64, 544>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (tm == 64 && g_trunk_dreg && g_trunk_var == 256)  // ablation: no epilogue at all
+        hipLaunchKernelGGL((k_trunk_bf16<64, 768>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    else if (tm == 64 && g_trunk_dreg) hipLaunchKernelGGL((k_trunk_bf16<64, 512>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
