@@ -3,12 +3,12 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out/final5 gpurun_out/prof
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/final5/gputest.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAILED|Error" gpurun_out/final5/gputest.log | head -20; tail -20 gpurun_out/final5/gputest.log; exit 1; }
-tail -1 gpurun_out/final5/gputest.log
-timeout -k 10 560 python -u bench.py > gpurun_out/final5/bench_default.json 2> gpurun_out/final5/bench_default.err || { echo "BENCH FAILED"; tail -20 gpurun_out/final5/bench_default.err; exit 1; }
-timeout -k 10 200 python bench.py --config c4 --global-batch 512 --no-cpu-baseline --no-secondary > gpurun_out/final5/bench_c4_512.json 2>/dev/null || exit 1
-timeout -k 10 200 python bench.py --config c3 --no-cpu-baseline --no-secondary > gpurun_out/final5/bench_c3.json 2>/dev/null || exit 1
-timeout -k 10 200 python bench.py --config c5 --no-cpu-baseline --no-secondary > gpurun_out/final5/bench_c5.json 2>/dev/null || exit 1
-for f in default c4_512 c3 c5; do python -c "import json; d=json.load(open('gpurun_out/final5/bench_$f.json')); print('$f', round(d['ms_per_step'],3), round(d['value']/1e6,2), d['roofline']['kernel'][:22], round(d['roofline']['frac'],3), (d.get('mlp_mfma_utilisation') or {}).get('frac'))"; done
+mkdir -p gpurun_out/final6 gpurun_out/prof
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/final6/gputest.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAILED|Error" gpurun_out/final6/gputest.log | head -20; tail -20 gpurun_out/final6/gputest.log; exit 1; }
+tail -1 gpurun_out/final6/gputest.log
+timeout -k 10 560 python -u bench.py > gpurun_out/final6/bench_default.json 2> gpurun_out/final6/bench_default.err || { echo "BENCH FAILED"; tail -20 gpurun_out/final6/bench_default.err; exit 1; }
+timeout -k 10 200 python bench.py --config c4 --global-batch 512 --no-cpu-baseline --no-secondary > gpurun_out/final6/bench_c4_512.json 2>/dev/null || exit 1
+timeout -k 10 200 python bench.py --config c3 --no-cpu-baseline --no-secondary > gpurun_out/final6/bench_c3.json 2>/dev/null || exit 1
+timeout -k 10 200 python bench.py --config c5 --no-cpu-baseline --no-secondary > gpurun_out/final6/bench_c5.json 2>/dev/null || exit 1
+for f in default c4_512 c3 c5; do python -c "import json; d=json.load(open('gpurun_out/final6/bench_$f.json')); print('$f', round(d['ms_per_step'],3), round(d['value']/1e6,2), d['roofline']['kernel'][:22], round(d['roofline']['frac'],3), (d.get('mlp_mfma_utilisation') or {}).get('frac'))"; done
 bash tools/gpu_profiles.sh
