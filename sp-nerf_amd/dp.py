@@ -25,13 +25,26 @@ def env_rank():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
 
+def pg_timeout_seconds() -> float:
+    """Collective timeout of the process group: SPNERF_PG_TIMEOUT seconds (default 300).  A
+    collective that does not complete in that time aborts the rank (RCCL's watchdog) instead of
+    hanging the job — a step is milliseconds, so minutes mean a deadlock."""
+    return float(os.environ.get("SPNERF_PG_TIMEOUT", "300"))
+
+
 def init_from_env(backend: str = "nccl", device=None):
     """Join the process group torchrun describes in the environment.  Call it AFTER
-    ``torch.cuda.set_device``; with RCCL the rank's device is bound eagerly (``device_id``)."""
+    ``torch.cuda.set_device``; with RCCL the rank's device is bound eagerly (``device_id``).
+    Every group gets a finite ``timeout`` (``pg_timeout_seconds``)."""
+    import datetime
     rank, local, world = env_rank()
     if world > 1 and not dist.is_initialized():
         kw = {"device_id": torch.device(device)} if (backend == "nccl" and device is not None) else {}
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        if backend == "nccl":
+            # fail fast: a hung collective raises on the host instead of waiting forever
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=pg_timeout_seconds()), **kw)
     return rank, local, world
 
 

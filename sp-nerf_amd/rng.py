@@ -82,13 +82,26 @@ class PhiloxRandom:
         self._state = None
         self._snap = None
         self._slot = 0
+        self._host_step = -1   # host mirror of the device step (eager renders only; see _gen)
 
     def begin_render(self, device):
         if self._state is None or self._state.device != torch.device(device):
-            self._state = torch.tensor([self.seed, -1], dtype=torch.int64, device=device)
+            self._state = torch.tensor([self.seed, self._host_step], dtype=torch.int64, device=device)
         self._state[1:].add_(1)
+        self._host_step += 1
         self._snap = self._state.clone()
         self._slot = 0
+
+    def reset_step(self, step: int = -1) -> None:
+        """Set the step counter (device and host mirror): the next render draws as step + 1."""
+        self._host_step = int(step)
+        if self._state is not None:
+            self._state[1].fill_(int(step))
+
+    def copy_state_from(self, other: "PhiloxRandom") -> None:
+        """Continue from ``other``'s step (same draws from the next render on)."""
+        self._host_step = other._host_step
+        self._state = None if other._state is None else other._state.clone()
 
     def key(self, device, nslots: int = 1):
         """(spnerf_rng, the tensor it points at — keep it alive while a kernel may read it)"""
@@ -100,11 +113,12 @@ class PhiloxRandom:
         return r, self._snap
 
     # draws a host-side caller asks for as tensors (the standalone drop-ins, e.g. sample_3sigma):
-    # a generator seeded from the key, not rank-keyed per ray
+    # a generator seeded from (seed, step, slot), not rank-keyed per ray.  The step is the HOST
+    # mirror (no device read, so no sync); these fallbacks cannot be captured into a HIP graph
+    # (a replay would not advance the mirror and torch generators are host state).
     def _gen(self, device):
-        step = int(self._state[1]) if self._state is not None else 0
         g = torch.Generator(device=device)
-        g.manual_seed((self.seed * 1000003 + step * 8191 + self._slot) & ((1 << 63) - 1))
+        g.manual_seed(_mix64(self.seed, max(self._host_step, 0), self._slot) & ((1 << 63) - 1))
         self._slot += 1
         return g
 
@@ -118,6 +132,20 @@ class PhiloxRandom:
 
     def gt_uniform(self, valid_mask, n, device):
         return self.rand((valid_mask.shape[0], n), device)
+
+
+def _splitmix64(x: int) -> int:
+    m = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & m
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
+    return x ^ (x >> 31)
+
+
+def _mix64(seed: int, step: int, slot: int) -> int:
+    """(seed, step, slot) -> 64-bit generator seed; distinct triples do not collide the way a
+    linear combination does."""
+    return _splitmix64(_splitmix64(_splitmix64(seed & ((1 << 64) - 1)) ^ (step & ((1 << 64) - 1))) ^ slot)
 
 
 def begin_render(device) -> None:

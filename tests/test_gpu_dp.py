@@ -229,8 +229,7 @@ def bucket_runs(rank, world):
     def reset():
         for p in params:
             p.grad = None
-        if src._state is not None:
-            src._state[1].fill_(-1)
+        src.reset_step(-1)
 
     out = []
     with spnerf_amd.random_source(src):
@@ -252,7 +251,7 @@ def bucket_runs(rank, world):
         with torch.cuda.graph(graph):
             fwd_bwd()
         flat = model._flat_grad
-        src._state[1].fill_(-1)
+        src.reset_step(-1)
         graph.replay()
         buckets.launch(flat, overlap=False)   # the replay's marks are the graph's own edges
         buckets.finish(flat)

@@ -49,7 +49,9 @@ def test_oracle_outputs_match_reference(name):
         # (here the fine depths themselves too: the inverse CDF of computed weights)
         fine_derived = "fine" in name and not k.endswith("_coarse")
         got = res[k].detach().numpy()
-        gu.assert_close(k, got, data["out_" + k], rtol=1e-4, atol_frac=1e-4 if fine_derived else 1e-5)
+        # the looser floor only where the fine pass's computed depths amplify host rounding
+        gu.assert_close(k, got, data["out_" + k], rtol=1e-4 if fine_derived else 2e-5,
+                        atol_frac=1e-4 if fine_derived else 1e-5)
         assert gu.rel_err(got, data["out_" + k]) < 1e-5, (k, gu.rel_err(got, data["out_" + k]))
 
 
@@ -67,7 +69,11 @@ def test_oracle_grads_match_reference(name):
     if any(k.startswith("grad_") for k in data):
         for n, t in params.items():
             g = t.grad.numpy() if t.grad is not None else np.zeros(tuple(t.shape), np.float32)
+            # measured host noise (fp32 sums over rays with cancellation): coarse cases up to 4.4e-5
+            # of the largest entry (c3_w64 sky_color.2.weight), the fine cases 6.5e-5: the 1e-4
+            # floor for both, and a norm-wise bound per parameter that keeps the coarse cases tight
             gu.assert_close("grad " + n, g, data["grad_" + n], rtol=1e-4, atol_frac=1e-4)
+            assert gu.rel_err(g, data["grad_" + n]) < (1e-4 if "fine" in name else 5e-5), (n, gu.rel_err(g, data["grad_" + n]))
     else:
         Q = gu.param_projections([(n, tuple(t.shape)) for n, t in params.items()])
         for n, t in params.items():

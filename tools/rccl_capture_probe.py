@@ -50,8 +50,7 @@ def main():
     def reset():
         for p in m.parameters():
             p.grad = None
-        if src._state is not None:
-            src._state[1].fill_(-1)
+        src.reset_step(-1)
 
     with spnerf_amd.random_source(src):
         s = torch.cuda.Stream()
@@ -66,7 +65,7 @@ def main():
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             step()
-        src._state[1].fill_(-1)
+        src.reset_step(-1)
         g.replay()
         torch.cuda.synchronize()
         same = torch.equal(eager, m._flat_grad)
