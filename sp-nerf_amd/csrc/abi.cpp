@@ -45,6 +45,20 @@ static hipEvent_t take_event() {
     return e;
 }
 
+int g_prof_shapes = 0;
+
+int num_cus() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cached[dev] <= 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
 ProfScope::ProfScope(const char* cls, hipStream_t s, double flop, double bytes) : rec_(nullptr), s_(s) {
     if (!g_on) return;
     std::lock_guard<std::mutex> lk(g_mu);
@@ -53,7 +67,9 @@ ProfScope::ProfScope(const char* cls, hipStream_t s, double flop, double bytes) 
         delete r;
         return;
     }
-    auto& st = g_stats[cls];
+    std::string key(cls);
+    if (g_prof_shapes) key += "#" + std::to_string((long long)(flop / 1e6 + 0.5)) + "MF";
+    auto& st = g_stats[key];
     st.pending.push_back(*r);
     delete r;
     rec_ = (void*)&st;

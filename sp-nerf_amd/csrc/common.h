@@ -37,6 +37,13 @@ void set_error(const char* fmt, ...);
     } while (0)
 
 // ---- profiling: HIP events around each launch of a kernel class, on the launch stream ----
+// compute units of the current device (hipDeviceProp_t::multiProcessorCount, cached per device):
+// the resident grid of the persistent kernels
+int num_cus();
+
+// option prof_shapes: each launch's class is keyed by its FLOP count too ("class#<MFLOP>"), so
+// the in-library timer separates the launch shapes of one kernel function
+extern int g_prof_shapes;
 struct ProfScope {
     ProfScope(const char* cls, hipStream_t s, double flop, double bytes);
     ~ProfScope();

@@ -1515,7 +1515,7 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     if (v == 8) {
         const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
         const int ip = (a.dbg & 64) ? 2 : (a.dbg & 32) ? 1 : g_nt16_ip;
-        const dim3 grid(std::min(nt, 256)), block(512);
+        const dim3 grid(std::min(nt, num_cus())), block(512);
         if (dm) {
             const bool z = a.dmul_z != 0;   // zsave: Dmul holds Z
             if (ip == 2) {
@@ -1560,18 +1560,18 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     if (v >= 5) {  // generalised tiles, persistent with one block per CU
         if (v == 5) {
             const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
-            hipLaunchKernelGGL((k_gemm_nt_bf16w<256, 256, 2, 4>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+            hipLaunchKernelGGL((k_gemm_nt_bf16w<256, 256, 2, 4>), dim3(std::min(nt, num_cus())), dim3(512), 0, s, a, nt);
         } else if (v == 6) {
             const int nt = cdiv(a.M, 256) * cdiv(a.N, 128);
-            hipLaunchKernelGGL((k_gemm_nt_bf16w<256, 128, 4, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+            hipLaunchKernelGGL((k_gemm_nt_bf16w<256, 128, 4, 2>), dim3(std::min(nt, num_cus())), dim3(512), 0, s, a, nt);
         } else {
             const int nt = cdiv(a.M, 128) * cdiv(a.N, 256);
-            hipLaunchKernelGGL((k_gemm_nt_bf16w<128, 256, 2, 2>), dim3(std::min(nt, 256)), dim3(256), 0, s, a, nt);
+            hipLaunchKernelGGL((k_gemm_nt_bf16w<128, 256, 2, 2>), dim3(std::min(nt, num_cus())), dim3(256), 0, s, a, nt);
         }
         SPN_HIP(hipGetLastError());
         return SPNERF_OK;
     }
-    const int resident = 2 * 256;
+    const int resident = 2 * num_cus();
     const int grid = v >= 3 ? std::min(ntiles, resident) : ntiles;
     if (v == 1 || v == 3) hipLaunchKernelGGL(k_gemm_nt_bf16<1>, dim3(grid), dim3(256), 0, s, a, ntiles);
     else hipLaunchKernelGGL(k_gemm_nt_bf16<2>, dim3(grid), dim3(256), 0, s, a, ntiles);
@@ -1583,13 +1583,14 @@ int g_tn16_min_points = 1024;  // fewest points per split of a bf16 weight-gradi
 
 int tn_splits_bf16(int P, int N, int K, int variant, int few) {
     // the narrow kernel: one block per CU, at least half the usual points per split
-    if (tn_k64(N, K)) return std::max(1, std::min(256, cdiv(P, g_tn16_min_points / 2)));
+    const int cus = num_cus();
+    if (tn_k64(N, K)) return std::max(1, std::min(cus, cdiv(P, g_tn16_min_points / 2)));
     const bool wide = tn_wide(N, K, variant, few);
     const int tiles = wide ? cdiv(N, TW) * cdiv(K, TW) : cdiv(N, HB) * cdiv(K, HB);
-    // one wide block per CU, two 128x128 ones: as many splits as fill the 256 CUs WITHOUT a
-    // second round (N = 768, K = 512 rounded up to 258 wide blocks: 221 us, two rounds)
-    int splits = (wide ? 256 : 512) / tiles;
-    if (splits > (wide && tiles < 4 ? 256 : 64)) splits = wide && tiles < 4 ? 256 : 64;
+    // one wide block per CU, two 128x128 ones: as many splits as fill the CUs (256 on MI355X)
+    // WITHOUT a second round (N = 768, K = 512 rounded up to 258 wide blocks: 221 us, two rounds)
+    int splits = (wide ? cus : 2 * cus) / tiles;
+    if (splits > (wide && tiles < 4 ? cus : 64)) splits = wide && tiles < 4 ? cus : 64;
     // (few wide tiles: half the points per split, so small batches still spread over the chip)
     const int max_splits = cdiv(P, wide && tiles < 4 ? g_tn16_min_points / 2 : g_tn16_min_points);
     if (splits > max_splits) splits = max_splits;

@@ -970,11 +970,11 @@ int32_t gemm_nt(const NTArgs& a0, hipStream_t s, int variant) {
     if (v >= 4 && v <= 8) {
         const int bm = 256, bn = v == 4 ? 256 : 128;
         const int nt = cdiv(a.M, bm) * cdiv(a.N, bn);
-        if (v == 4) hipLaunchKernelGGL((k_gemm_nt_w<256, 256, 2, 4>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
-        else if (v == 6) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 1>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
-        else if (v == 7) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        if (v == 4) hipLaunchKernelGGL((k_gemm_nt_w<256, 256, 2, 4>), dim3(std::min(nt, num_cus())), dim3(512), 0, s, a, nt);
+        else if (v == 6) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 1>), dim3(std::min(nt, num_cus())), dim3(512), 0, s, a, nt);
+        else if (v == 7) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2, 2>), dim3(std::min(nt, num_cus())), dim3(512), 0, s, a, nt);
         else if (v == 8) hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 2, 2, 3>), dim3(std::min(nt, 512)), dim3(256), 0, s, a, nt);
-        else hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2>), dim3(std::min(nt, 256)), dim3(512), 0, s, a, nt);
+        else hipLaunchKernelGGL((k_gemm_nt_w<256, 128, 4, 2>), dim3(std::min(nt, num_cus())), dim3(512), 0, s, a, nt);
     } else if (v == 1 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 1>), dim3(nb), dim3(256), 0, s, a);
     else if (v == 2) hipLaunchKernelGGL((k_gemm_nt<32, 2>), dim3(nb), dim3(256), 0, s, a);
     else if (v == 3 && a.K % 64 == 0 && a.K1 % 64 == 0) hipLaunchKernelGGL((k_gemm_nt<64, 2>), dim3(nb), dim3(256), 0, s, a);

@@ -387,7 +387,7 @@ int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, 
     ad.nt = (g_trunk_nt >> 1) & 1;
     ad.dbg = g_heads_dbg;
     ProfScope prof("heads_fused", s, flop, bytes);
-    hipLaunchKernelGGL(k_heads_bf16, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, k, ntiles);
+    hipLaunchKernelGGL(k_heads_bf16, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, k, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -1672,7 +1672,9 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
                                {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
         else
             SPN_TRY(tn_grad<T>(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s2, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
-        SPN_TRY(grad_mark(0, s2));   // every output head's gradient is final (spnerf_grad_marks)
+        // every output head's gradient is final (spnerf_grad_marks) — unless sun_v_net.2 / .4's
+        // are deferred: then spnerf_mlp_trunk_wgrad records the mark once they are
+        if (!c.defer || !SPN_DEFER_SUNV) SPN_TRY(grad_mark(0, s2));
         NT g;
         g.A = dZG; g.lda = d.NG; g.K1 = NG; g.B = G::w(c, c.k.WGT, c.k.WGT16); g.ldb = d.NG; g.C = dZ; g.ldc = W;
         g.M = (int)P; g.N = W; g.K = NG;
@@ -1721,7 +1723,9 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
             if (tsum) SPN_TRY(ray_tiles(i, dZi, parts_in_bwd));
             else SPN_TRY(ray_rowsum<T>(dZi, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
         }
-        return grad_mark(1 + (d.L - 1 - i), s2);
+        // a mark is recorded only once its gradients are final: deferred layers get theirs from
+        // spnerf_mlp_trunk_wgrad
+        return c.defer ? SPNERF_OK : grad_mark(1 + (d.L - 1 - i), s2);
     };
     if (BF && !zs && g_fused_bwd && !c.k.Wb16.empty() && c.k.Wb16[1] >= 0) {
         // the whole dX chain in one launch (k_trunk_bwd_bf16): dZ_{i-1} overwrites D_{i-1} in
@@ -1923,14 +1927,19 @@ static int* option_slot(const char* name) {
     const std::string n(name);
     if (n == "fused_trunk") return &g_fused_trunk;
     if (n == "trunk_tile") return &g_trunk_tile;
+#ifdef SPN_ABLATIONS
+    // profiling ablations whose outputs are INVALID: only in a -DSPN_ABLATIONS build
+    // (make variant VDEF=-DSPN_ABLATIONS VLIB=libspnerf_amd_abl.so), never in the product library
     if (n == "trunk_dbg") return &g_trunk_dbg;
-    if (n == "trunk_nt") return &g_trunk_nt;
     if (n == "trunk_var") return &g_trunk_var;
+    if (n == "heads_dbg") return &g_heads_dbg;
+#endif
+    if (n == "prof_shapes") return &g_prof_shapes;
+    if (n == "trunk_nt") return &g_trunk_nt;
     if (n == "trunk_dreg") return &g_trunk_dreg;
     if (n == "trunk_bwd_dreg") return &g_trunk_bwd_dreg;
     if (n == "trunk_bwd_nt") return &g_trunk_bwd_nt;
     if (n == "trunk_sigma") return &g_trunk_sigma;
-    if (n == "heads_dbg") return &g_heads_dbg;
     if (n == "nt_f32_variant") return &g_nt_variant;
     if (n == "tn_f32_variant") return &g_tn_variant;
     if (n == "nt_bf16_variant") return &g_nt16_variant;

@@ -442,7 +442,7 @@ bool trunk2_supported(const TrunkArgs& a, bool save) {
 template <int TM>
 static void launch_trunk2(const TrunkArgs& ad, hipStream_t s, bool l0, bool save, int ntiles) {
     using Geo = T2Geo<TM>;
-    const dim3 grid(std::min(ntiles, 256 * Geo::WGS)), block(Geo::NT);
+    const dim3 grid(std::min(ntiles, num_cus() * Geo::WGS)), block(Geo::NT);
     if (l0 && save) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, true>), grid, block, 0, s, ad, ntiles);
     else if (l0) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, false>), grid, block, 0, s, ad, ntiles);
     else if (save) hipLaunchKernelGGL((k_trunk2_bf16<TM, false, true>), grid, block, 0, s, ad, ntiles);

@@ -833,8 +833,8 @@ int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double
     ad.dbg = g_trunk_dbg;
     ad.nt = g_trunk_bwd_nt;
     ProfScope prof("trunk_bwd_bf16", s, flop, bytes);
-    if (g_trunk_bwd_dreg) hipLaunchKernelGGL(k_trunk_bwd_bf16<true>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else hipLaunchKernelGGL(k_trunk_bwd_bf16<false>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+    if (g_trunk_bwd_dreg) hipLaunchKernelGGL(k_trunk_bwd_bf16<true>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else hipLaunchKernelGGL(k_trunk_bwd_bf16<false>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
@@ -881,18 +881,18 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     // H and D of every layer out) is not the inference tiling's (MFMA-bound)
     ProfScope prof(tm == 64 ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
     if (tm == 64 && g_trunk_dreg && g_trunk_var == 32)  // ablation: no sin / cos in the epilogue
-        hipLaunchKernelGGL((k_trunk_bf16<64, 544>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+        hipLaunchKernelGGL((k_trunk_bf16<64, 544>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     else if (tm == 64 && g_trunk_dreg && g_trunk_var == 256)  // ablation: no epilogue at all
-        hipLaunchKernelGGL((k_trunk_bf16<64, 768>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (tm == 64 && g_trunk_dreg) hipLaunchKernelGGL((k_trunk_bf16<64, 512>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 64) hipLaunchKernelGGL((k_trunk_bf16<128, 64>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 128) hipLaunchKernelGGL((k_trunk_bf16<128, 128>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 256) hipLaunchKernelGGL((k_trunk_bf16<128, 256>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 464) hipLaunchKernelGGL((k_trunk_bf16<128, 464>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
-    else hipLaunchKernelGGL((k_trunk_bf16<128, 0>), dim3(std::min(ntiles, 256)), dim3(512), 0, s, ad, ntiles);
+        hipLaunchKernelGGL((k_trunk_bf16<64, 768>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (tm == 64 && g_trunk_dreg) hipLaunchKernelGGL((k_trunk_bf16<64, 512>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 64) hipLaunchKernelGGL((k_trunk_bf16<128, 64>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 128) hipLaunchKernelGGL((k_trunk_bf16<128, 128>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 256) hipLaunchKernelGGL((k_trunk_bf16<128, 256>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (g_trunk_var == 464) hipLaunchKernelGGL((k_trunk_bf16<128, 464>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else hipLaunchKernelGGL((k_trunk_bf16<128, 0>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -132,3 +132,8 @@ def test_kernel_options_roundtrip_and_reject_unknown_names():
     assert b"unknown option" in L.spnerf_last_error()
     with pytest.raises(_lib.SpnerfError):
         _lib.get_option("no_such_option")
+    # profiling ablations that make the library compute invalid outputs exist only in a
+    # -DSPN_ABLATIONS build, never in the product library
+    for name in (b"trunk_dbg", b"trunk_var", b"heads_dbg"):
+        assert L.spnerf_set_option(name, 1) < 0, name
+    _lib.set_option("prof_shapes", 0)
