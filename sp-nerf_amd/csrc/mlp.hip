@@ -1952,6 +1952,7 @@ static int* option_slot(const char* name) {
     if (n == "nt_bf16_epi") return &g_nt16_epi;
     if (n == "grad_marks_flags") return &g_marks_flags;
     if (n == "tn_bf16_variant") return &g_tn16_variant;
+    if (n == "tn_bf16_lw") return &g_tn16_lw;
     if (n == "heads_variant") return &g_heads_variant;
     if (n == "l0_split") return &g_l0_split;
     if (n == "trunk_l0") return &g_trunk_l0;
