@@ -64,7 +64,6 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);
 // tiles fed by LDS-DMA (when P % 32 == 0 as well);
 // <= 0 = library default (g_tn16_variant)
 extern int g_tn16_variant;
-extern int g_tn16_lw;           // option tn_bf16_lw: loader waves of the DMA weight-gradient GEMM (0 or 4)
 extern int g_tn16_min_points;  // fewest points per split (option "tn_bf16_min_points")
 // few: the tn_bf16_few_tiles choice (-1: the option; the workspace layout takes the larger, 1)
 int tn_splits_bf16(int P, int N, int K, int variant = -1, int few = -1);

@@ -1460,204 +1460,9 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
     }
 }
 
-// k_gemm_tn_bf16d with the LDS-DMA issued by NLW dedicated loader waves (option tn_bf16_lw):
-// the 8 MFMA waves (same tiling, same transposed reads, same k order: bit-identical slabs) never
-// issue a DMA — an issue costs the issuing wave 60-185 cycles beside MFMAs (MI355X_MICROARCH.md
-// 'LDS-DMA piece issue cost'), 32 pieces per 32-point step, and halving the DMAs of the NT GEMM
-// took 30% off it.  Loader wave l issues pieces l, l + NLW, ... of every step into the same
-// 4-stage ring, three steps in flight; one s_barrier per step (all 8 + NLW waves) both publishes
-// step st (each loader waits for its own pieces first) and retires the MFMA waves' reads of the
-// stage step st + 3 lands in.
-template <int NLW>
-__global__ __launch_bounds__(512 + 64 * NLW) void k_gemm_tn_bf16l(TN16Args g) {
-    static_assert(NLW == 4, "pieces per loader; the bias mapping assumes 256 loader threads");
-    constexpr int PPL = 32 / NLW;  // pieces per loader wave per step
-    __shared__ __attribute__((aligned(16))) char smem[TD_STAGES * TD_STG];  // [stage][A0|A1|B0|B1]
-    typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    typedef __attribute__((address_space(1))) void* gbl_ptr_t;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int nK = (g.K + TW - 1) / TW;
-    const int ntiles = cdiv(g.N, TW) * nK;
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
-    const int split = w / ntiles, t = w % ntiles;
-    const int n0 = (t / nK) * TW, k0 = (t % nK) * TW;
-    const int p_beg = split * g.p_per_split;
-    const int p_end = min(g.P, p_beg + g.p_per_split);
-    const bool bsplit = g.bias_split && nK == 2;
-    const int kt = t % nK;
-    const bool do_bias = g.slab_b != nullptr && (bsplit || k0 == 0);
-    const int ns = p_end > p_beg ? (p_end - p_beg) / TD_STEP : 0;  // whole steps (host-checked)
-    constexpr int HALF = TD_STEP * 256;
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    // bias sums (do_bias) by the loader threads lt = tid - 512: two row phases each, kept apart so
-    // every phase sums its rows in the order of k_gemm_tn_bf16d (bit-identical).  bsplit: chunk
-    // 16 kt + (lt & 15) of A, phases lt >> 4 and 16 + (lt >> 4) (one row each per step); else
-    // chunk lt & 31, phases lt >> 5 and 8 + (lt >> 5) (rows ph and ph + 16 each per step)
-    const int lt = tid - 512;
-    const int ch = bsplit ? 16 * kt + (lt & 15) : lt & 31;
-    const int ph0 = bsplit ? lt >> 4 : lt >> 5, ph1 = ph0 + (bsplit ? 16 : 8);
-    float bs0[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bs1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-
-    if (wid >= 8) {  // ---- loader wave (wave-uniform branch)
-        const int l = wid - 8;
-        // piece q of a step: 4 rows x 256 B of half (q >> 3) & 1 of operand q >> 4 (as k_gemm_tn_bf16d)
-        auto issue = [&](int st, int stg) {
-            const int64_t p0 = p_beg + (int64_t)TD_STEP * st;
-            const bool sg2 = p0 >= g.P1;
-#pragma unroll
-            for (int i = 0; i < PPL; ++i) {
-                const int q = l + NLW * i;
-                const int X = q >> 4, hf = (q >> 3) & 1, rg = q & 7;
-                const int row = rg * 4 + (lane >> 4);
-                const int chl = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-                const int f = (X ? k0 : n0) + hf * 128 + 8 * chl;
-                const bf16* src;
-                if (X == 0) {
-                    src = (sg2 ? g.A_s2 : g.A) + (row + p0) * g.lda + min(f, g.N - 8);
-                } else {
-                    const int kc = min(f, g.K - 8);
-                    const bool s2 = kc >= g.K1;
-                    const int ldq = s2 ? g.ldb2 : g.ldb;
-                    src = (s2 ? (sg2 ? g.B2_s2 : g.B2) + (kc - g.K1) : (sg2 ? g.B_s2 : g.B) + kc) + (row + p0) * ldq;
-                }
-                __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
-            }
-        };
-        auto bias_rows = [&](int stg) {
-            const char* sA = smem + stg * TD_STG + (ch >> 4) * HALF;
-            auto add = [&](float (&acc8)[8], int row) {
-                float f[8];
-                unpack8(*reinterpret_cast<const u32x4*>(sA + tn_off(row, ch & 15)), f);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc8[e] += f[e];
-            };
-            if (bsplit) {  // block-uniform
-                add(bs0, ph0);
-                add(bs1, ph1);
-            } else {
-                add(bs0, ph0);
-                add(bs0, ph0 + 16);
-                add(bs1, ph1);
-                add(bs1, ph1 + 16);
-            }
-        };
-        if (ns > 0) {
-            issue(0, 0);
-            issue(min(1, ns - 1), 1);
-            issue(min(2, ns - 1), 2);
-            for (int st = 0; st < ns; ++st) {
-                // step st landed when at most steps st+1, st+2 (PPL pieces each) are outstanding
-                if constexpr (PPL == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                else if constexpr (PPL == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES);
-                if (do_bias) bias_rows(st % TD_STAGES);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
-            __builtin_amdgcn_s_barrier();
-        }
-    } else {  // ---- MFMA wave
-        const int wa = wid >> 2, wb = wid & 3, h = lane >> 5, grp = (lane >> 4) & 1;
-        const int q4 = (lane & 15) >> 2, pp = lane & 3;
-        auto operand = [&](const char* base, int r0, int col) -> bf16x8 {
-            const int c = (col >> 3) + (pp >> 1);
-            typedef __attribute__((address_space(3))) s16x4* lp;
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(base + tn_off(r0 + q4, c) + 8 * (pp & 1)));
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(base + tn_off(r0 + 4 + q4, c) + 8 * (pp & 1)));
-            typedef short s16x8 __attribute__((ext_vector_type(8)));
-            return __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        };
-        auto compute = [&](int stg) {
-            const char* sA = smem + stg * TD_STG + wa * HALF;
-            const char* sB = smem + stg * TD_STG + (2 + (wb >> 1)) * HALF;
-            const int cb = (wb & 1) * 64;
-#pragma unroll
-            for (int ks = 0; ks < TD_STEP / 16; ++ks) {
-                const int r0 = 16 * ks + 8 * h;
-                bf16x8 a[4], b[2];
-#pragma unroll
-                for (int j = 0; j < 2; ++j) b[j] = operand(sB, r0, cb + 32 * j + 16 * grp);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) a[i] = operand(sA, r0, 32 * i + 16 * grp);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-            }
-        };
-        if (ns > 0) {
-            for (int st = 0; st < ns; ++st) {
-                __builtin_amdgcn_s_barrier();
-                compute(st % TD_STAGES);
-            }
-            __builtin_amdgcn_s_barrier();
-        }
-        float* slab = g.slab + (int64_t)split * g.slab_stride;
-        const int r32 = lane & 31;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int k = k0 + wb * 64 + j * 32 + r32;
-            if (k >= g.K) continue;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int n = n0 + wa * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (n < g.N) slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
-                }
-        }
-    }
-    // bias sums: every wave takes part in the barriers; the MFMA waves' threads hold the partials
-    if (do_bias && bsplit) {
-        __syncthreads();
-        float* red = reinterpret_cast<float*>(smem);  // [32 phases][128 features]
-        const int cl = ch & 15;
-        if (tid >= 512) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                red[ph0 * 128 + 8 * cl + e] = bs0[e];
-                red[ph1 * 128 + 8 * cl + e] = bs1[e];
-            }
-        }
-        __syncthreads();
-        const int n = n0 + 128 * kt + tid;
-        if (tid < 128 && n < g.N) {
-            float s = 0.f;
-            for (int ph = 0; ph < 32; ++ph) s += red[ph * 128 + tid];
-            g.slab_b[(int64_t)split * g.N + n] = s;
-        }
-    } else if (do_bias) {
-        __syncthreads();
-        float* red = reinterpret_cast<float*>(smem);  // [16 phases][256 features]
-        if (tid >= 512) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                red[ph0 * 256 + 8 * ch + e] = bs0[e];
-                red[ph1 * 256 + 8 * ch + e] = bs1[e];
-            }
-        }
-        __syncthreads();
-        if (tid < 256 && n0 + tid < g.N) {
-            float s = 0.f;
-            for (int ph = 0; ph < 16; ++ph) s += red[ph * 256 + tid];
-            g.slab_b[(int64_t)split * g.N + n0 + tid] = s;
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
-int g_tn16_lw = 0;  // option tn_bf16_lw: loader waves of the DMA weight-gradient GEMM (0 = k_gemm_tn_bf16d)
 int g_nt16_variant = 8;
 int g_nt16_ip = 2;  // DMA NT / TN: where a K-step issues the next step's DMAs (0 before its MFMAs, 1 after, 2 between the k-halves)
 // the weight-gradient GEMM: 1 (after a step's MFMAs) re-measured on the final round-3 tree: C4 26.69 /
@@ -1821,8 +1626,7 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
         {
             a.bias_split = g_tn16_bias_split;
             const int ip = (a.dbg & 4) ? 2 : (a.dbg & 2) ? 1 : g_tn16_ip;
-            if (g_tn16_lw == 4) hipLaunchKernelGGL(k_gemm_tn_bf16l<4>, dim3(nb * splits), dim3(768), 0, s, a);
-            else if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, dim3(nb * splits), dim3(512), 0, s, a);
+            if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, dim3(nb * splits), dim3(512), 0, s, a);
             else if (ip == 1) hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, dim3(nb * splits), dim3(512), 0, s, a);
             else hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, dim3(nb * splits), dim3(512), 0, s, a);
         }

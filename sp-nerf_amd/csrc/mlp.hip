@@ -1066,6 +1066,8 @@ struct Ctx {
     const float* rays = nullptr;
     const float* z = nullptr;
     int rs = 0, dir_off = 0;
+    float* out = nullptr;           // the forward's output rows (the fused trunk + heads write them)
+    bool* heads_done = nullptr;     // set when the trunk launch ran the fused heads too
     float* at(int64_t off) const { return ws + off; }
     const float* pk(int64_t off) const { return P + off; }
     bf16* hb(int64_t off) const { return reinterpret_cast<bf16*>(ws + off); }          // bf16 workspace buffer
@@ -1292,6 +1294,20 @@ static bool trunk_l0_on(const Ctx& c, bool save) {
            trunk_l0_supported(c.d.K0p, save);
 }
 
+// the fused heads' arguments and counted work (k_heads_bf16, or inside the inference trunk)
+static HeadsFusedArgs heads_args(const Ctx& c, int mode, int64_t hl, double* flop, double* bytes) {
+    const Dims& d = c.d;
+    const int64_t P = c.w.P;
+    const int W = d.W, H = d.H;
+    HeadsFusedArgs a;
+    a.HL = hl >= 0 ? c.hb(hl) : nullptr; a.packed = c.P; a.rbQ = c.at(c.w.rbQ); a.sky = c.at(c.w.sky); a.out = c.out;
+    a.P = P; a.S = c.S; a.NO = d.NO; a.C = d.sem ? d.C : 0; a.sem_col = d.sem_col; a.mode = mode;
+    *flop = mode == 1 ? 2.0 * P * W
+                      : 2.0 * P * ((double)W * (W + 2 * H) + 2.0 * H * H + (d.sem ? (double)H * W + H * d.C : 0.0) + W + 4.0 * H);
+    *bytes = 2.0 * P * W + 4.0 * P * (mode == 1 ? 1 : d.NO);
+    return a;
+}
+
 template <typename T>
 static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, bool* sig_done) {
     using G = Gemms<T>;
@@ -1346,6 +1362,17 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
             const double in = first == 0 ? (a.rays ? 4.0 * P : 4.0 * P * d.K0p) : 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0));
             const double nout = !save ? 1.0 : (zs ? d.L - first + 1.0 : 2.0 * (d.L - first));
             const double bytes = in + 2.0 * P * W * nout;
+            if constexpr (BF) {
+                // inference: the fused heads on the trunk's last LDS image (no H_L in HBM)
+                if (c.heads_done && c.out && heads_fused_on(c, save, mode) && trunk2_heads_ok(a)) {
+                    double hflop = 0.0, hbytes = 0.0;
+                    const HeadsFusedArgs h = heads_args(c, mode, -1, &hflop, &hbytes);
+                    // algorithmic bytes: the trunk's input, the output rows (H_L never leaves)
+                    SPN_TRY(trunk2_heads_bf16(a, h, c.k, s, 2.0 * P * W * ksum + hflop, in + (hbytes - 2.0 * P * W)));
+                    *c.heads_done = true;
+                    return SPNERF_OK;
+                }
+            }
             SPN_TRY(trunk_bf16(a, s, 2.0 * P * W * ksum, bytes));
             HL = reinterpret_cast<T*>(a.Hs[d.L - 1]);
             break;
@@ -1488,17 +1515,16 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
         SPN_HIP(hipGetLastError());
     }
     bool sig_done = false;  // hsave[p·8] (σ pre-activation) written by the fused trunk
+    bool heads_done = false;  // the trunk launch ran the fused heads
+    c.out = out;
+    c.heads_done = &heads_done;
     if (d.bf) SPN_TRY(forward_gemms<bf16>(c, save, mode, s, &sig_done));
     else SPN_TRY(forward_gemms<float>(c, save, mode, s, nullptr));
+    if (heads_done) return SPNERF_OK;
     if (heads_fused_on(c, save, mode)) {
-        const int64_t hl = c.w.Hb[(d.L - 1) & 1];
-        HeadsFusedArgs a;
-        a.HL = c.hb(hl); a.packed = packed; a.rbQ = c.at(c.w.rbQ); a.sky = c.at(c.w.sky); a.out = out;
-        a.P = P; a.S = S; a.NO = d.NO; a.C = d.sem ? d.C : 0; a.sem_col = d.sem_col; a.mode = mode;
-        const double flop = mode == 1 ? 2.0 * P * W
-                                      : 2.0 * P * ((double)W * (W + 2 * H) + 2.0 * H * H + (d.sem ? (double)H * W + H * d.C : 0.0) +
-                                                   W + 4.0 * H);
-        SPN_TRY(heads_bf16(a, c.k, s, flop, 2.0 * P * W + 4.0 * P * (mode == 1 ? 1 : d.NO)));
+        double flop = 0.0, bytes = 0.0;
+        const HeadsFusedArgs a = heads_args(c, mode, c.w.Hb[(d.L - 1) & 1], &flop, &bytes);
+        SPN_TRY(heads_bf16(a, c.k, s, flop, bytes));
         return SPNERF_OK;
     }
     {
@@ -1952,7 +1978,6 @@ static int* option_slot(const char* name) {
     if (n == "nt_bf16_epi") return &g_nt16_epi;
     if (n == "grad_marks_flags") return &g_marks_flags;
     if (n == "tn_bf16_variant") return &g_tn16_variant;
-    if (n == "tn_bf16_lw") return &g_tn16_lw;
     if (n == "heads_variant") return &g_heads_variant;
     if (n == "l0_split") return &g_l0_split;
     if (n == "trunk_l0") return &g_trunk_l0;
@@ -1966,6 +1991,7 @@ static int* option_slot(const char* name) {
     if (n == "tile_rowsum") return &g_tile_rowsum;
     if (n == "trunk2") return &g_trunk2;
     if (n == "trunk2_tile") return &g_trunk2_tile;
+    if (n == "trunk_heads") return &g_trunk_heads;
     if (n == "emu_bf16") return &g_emu_bf16;
     return nullptr;
 }

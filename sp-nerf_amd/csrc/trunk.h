@@ -171,6 +171,11 @@ struct Dims;
 bool heads_bf16_shape_ok(const Dims& d);   // the packed layout carries the fused heads' weights
 bool heads_bf16_supported(const Dims& d);  // ... and the option is on
 int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes);
+// the inference trunk with the fused heads on its last LDS image (k_trunk2_bf16 HEADS): no H_L in HBM
+extern int g_trunk_heads;
+bool trunk2_heads_ok(const TrunkArgs& a);
+int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const PackedOffs& k, hipStream_t s, double flop,
+                          double bytes);
 
 extern int g_heads_dbg;    // HeadsFusedArgs::dbg
 extern int g_fused_heads;  // 1 = bf16 inference runs the fused heads where supported (default)

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "heads_tile.h"
 #include "trunk.h"
 
 namespace spn {
@@ -91,13 +92,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(bf16* t, int64_t p0,
 }
 }  // namespace
 
-// SAVE: every layer's D out (training; Ds[i] all set); L0: layer 0 in the launch
-template <int TM, bool L0, bool SAVE>
-__global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(TrunkArgs g, int ntiles) {
+// SAVE: every layer's D out (training; Ds[i] all set); L0: layer 0 in the launch.
+// HEADS (inference, TM = 128, option trunk_heads): the fused heads (heads_tile.h) run on the
+// last layer's LDS image, so H_L never leaves the chip (≈1 KB per point written and read back
+// by k_heads_bf16); their output staging is 8 KB beyond the trunk's LDS, their partials overlay
+// the PE tile (restaged by the next tile), and the weight ring is primed per tile instead of
+// running on through the heads.
+template <int TM, bool L0, bool SAVE, bool HEADS = false>
+__global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(TrunkArgs g, int ntiles, HeadsFusedArgs hg,
+                                                                              PackedOffs hk) {
     using Geo = T2Geo<TM>;
+    static_assert(!HEADS || (TM == 128 && !SAVE), "the fused heads: 128-point inference tiles");
     constexpr int NT = Geo::NT, NA = Geo::NA, NJ = Geo::NJ, CPT = Geo::CPT, PT = Geo::PT;
     constexpr int X0_OFF = Geo::X0_OFF, BIAS_OFF = Geo::BIAS_OFF, RB_OFF = Geo::RB_OFF;
-    __shared__ __attribute__((aligned(16))) char smem[Geo::LDS];
+    constexpr int OST_OFF = Geo::LDS;  // (HEADS) the heads' output staging
+    static_assert(!HEADS || (Geo::RB_OFF - Geo::X0_OFF >= hd::PART_BYTES && Geo::LDS + hd::OST_BYTES <= 160 * 1024),
+                  "heads LDS");
+    __shared__ __attribute__((aligned(16))) char smem[Geo::LDS + (HEADS ? hd::OST_BYTES : 0)];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     float* sbias = reinterpret_cast<float*>(smem + BIAS_OFF);
     float* srb = reinterpret_cast<float*>(smem + RB_OFF);
@@ -163,15 +174,23 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(T
             sbias[t + q * NT] = ka->bias[first][t + q * NT];
             srb[t + q * NT] = row ? rr[t + q * NT] : -0.f;
         }
-        const bf16* src = wstream(first);
-        const int nks = nks_of(first);
+        if constexpr (!HEADS) {
+            const bf16* src = wstream(first);
+            const int nks = nks_of(first);
 #pragma unroll
-        for (int d = 0; d < TPD; ++d) load_step(d, src + d * kTrunkKStride, nks);
+            for (int d = 0; d < TPD; ++d) load_step(d, src + d * kTrunkKStride, nks);
+        }
     }
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TM;
         const int nrows = (int)std::min<int64_t>(TM, g.P - p0);
         const int st = opaque(tid);
+        if constexpr (HEADS) {  // the first layer's stream, in flight through the tile's staging
+            const bf16* src = wstream(first);
+            const int nks = nks_of(first);
+#pragma unroll
+            for (int d = 0; d < TPD; ++d) load_step(d, src + d * kTrunkKStride, nks);
+        }
         // stage the first layer's input and the PE tile; rows past P read a clamped row (their
         // outputs are dropped by the store descriptors)
         if constexpr (L0) {
@@ -235,7 +254,7 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(T
             const bf16* wsrc = wstream(i);
             const int nks = nks_of(i);
             const bool last = i == g.L - 1;
-            const int inext = last ? (tile + (int)gridDim.x < ntiles ? first : -1) : i + 1;
+            const int inext = last ? (!HEADS && tile + (int)gridDim.x < ntiles ? first : -1) : i + 1;
             const bf16* wnxt = inext >= 0 ? wstream(inext) : wsrc;
             const int nks_nxt = inext >= 0 ? nks_of(inext) : nks;
             const int nkm = i == 0 ? nk0 : NMAIN;
@@ -410,7 +429,10 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(T
             const __amdgpu_buffer_rsrc_t hr = rows_rsrc(ka->Hs[i], p0, nrows);
             if (last) {
                 __syncthreads();
-                if (!(g.dbg & 1)) {
+                if constexpr (HEADS) {  // H_L stays on chip: the heads on this image
+                    hd::heads_tile<false>(hg, hk, smem, reinterpret_cast<float*>(smem + OST_OFF),
+                                          reinterpret_cast<float*>(smem + X0_OFF), nullptr, p0);
+                } else if (!(g.dbg & 1)) {
 #pragma unroll
                     for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(hr, q0, std::integral_constant<int, 4>{});
                 }
@@ -443,10 +465,12 @@ template <int TM>
 static void launch_trunk2(const TrunkArgs& ad, hipStream_t s, bool l0, bool save, int ntiles) {
     using Geo = T2Geo<TM>;
     const dim3 grid(std::min(ntiles, num_cus() * Geo::WGS)), block(Geo::NT);
-    if (l0 && save) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, true>), grid, block, 0, s, ad, ntiles);
-    else if (l0) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, false>), grid, block, 0, s, ad, ntiles);
-    else if (save) hipLaunchKernelGGL((k_trunk2_bf16<TM, false, true>), grid, block, 0, s, ad, ntiles);
-    else hipLaunchKernelGGL((k_trunk2_bf16<TM, false, false>), grid, block, 0, s, ad, ntiles);
+    const HeadsFusedArgs hg{};
+    const PackedOffs hk{};
+    if (l0 && save) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, true>), grid, block, 0, s, ad, ntiles, hg, hk);
+    else if (l0) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, false>), grid, block, 0, s, ad, ntiles, hg, hk);
+    else if (save) hipLaunchKernelGGL((k_trunk2_bf16<TM, false, true>), grid, block, 0, s, ad, ntiles, hg, hk);
+    else hipLaunchKernelGGL((k_trunk2_bf16<TM, false, false>), grid, block, 0, s, ad, ntiles, hg, hk);
 }
 
 int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, double bytes) {
@@ -460,6 +484,36 @@ int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, d
     ProfScope prof(save ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
     if (TM == 64) launch_trunk2<64>(ad, s, l0, save, ntiles);
     else launch_trunk2<128>(ad, s, l0, save, ntiles);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+// option trunk_heads: 1 = a bf16 inference forward whose trunk takes the 128-point two-workgroup
+// kernel runs the fused heads inside it (H_L stays in LDS); 0 = the trunk, then k_heads_bf16
+int g_trunk_heads = 1;
+
+bool trunk2_heads_ok(const TrunkArgs& a) {
+    return g_trunk_heads && g_trunk2_tile != 64 && trunk2_supported(a, false);
+}
+
+int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const PackedOffs& k, hipStream_t s, double flop,
+                          double bytes) {
+    SPN_ARG(trunk2_heads_ok(a), "trunk2_heads_bf16: unsupported shape or option");
+    SPN_ARG(h.P == a.P && h.S == a.S && h.NO <= hd::OST_LD && h.C <= 4 && k.Fnar16 >= 0, "trunk2_heads_bf16: bad heads");
+    if (a.P == 0) return SPNERF_OK;
+    const int ntiles = cdiv(a.P, 128);
+    TrunkArgs ad = a;
+    ad.dbg = 0;
+    ad.nt = 0;
+    const bool l0 = a.X0 || a.rays;
+    if (!l0) ad.rb0 = nullptr;
+    HeadsFusedArgs hd_ = h;
+    hd_.nt = 0;
+    hd_.dbg = 0;
+    const dim3 grid(std::min(ntiles, num_cus())), block(T2Geo<128>::NT);
+    ProfScope prof("trunk_heads_bf16", s, flop, bytes);
+    if (l0) hipLaunchKernelGGL((k_trunk2_bf16<128, true, false, true>), grid, block, 0, s, ad, ntiles, hd_, k);
+    else hipLaunchKernelGGL((k_trunk2_bf16<128, false, false, true>), grid, block, 0, s, ad, ntiles, hd_, k);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -169,3 +169,32 @@ def test_inline_encoding_bit_identical():
             _lib.set_option("pe_inline", 1)
         for k in outs[1]:
             assert torch.equal(outs[0][k], outs[1][k]), (sem, k)
+
+
+@pytest.mark.parametrize("sem,B,S", [(True, 3000, 128), (False, 301, 40), (True, 37, 128)])
+def test_trunk_with_fused_heads_bit_identical(sem, B, S):
+    """The inference trunk running the fused heads on its last LDS image (option trunk_heads 1:
+    H_L never goes to HBM; k_trunk2_bf16 HEADS) against the trunk launch followed by the heads
+    kernel (trunk_heads 0, H_L through HBM): the same bf16 H_L bits and the same heads code
+    (heads_tile.h), so every output is bit-identical.  301 x 40 points end in a ragged tile."""
+    from spnerf_amd import _lib
+    from oracle.weights import ModelDims
+    g = torch.Generator(device="cpu").manual_seed(11)
+    rays = torch.tensor(gu.synthetic_rays(B, 25), device=DEV)
+    u = torch.rand(B, S, generator=g).to(DEV)
+    labels = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    args = gu.args_of({"args": dict(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                                    sc_lambda=0.0, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+    model = make_model(ModelDims(width=512, sem=sem), 9, "bf16")
+    outs = []
+    try:
+        for th in (1, 0):
+            _lib.set_option("trunk_heads", th)
+            with torch.no_grad(), random_source(FixedU(u)):
+                outs.append(spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels if sem else None,
+                                                   mode="test"))
+    finally:
+        _lib.set_option("trunk_heads", 1)
+    for k in outs[1]:
+        assert torch.isfinite(outs[0][k]).all(), k
+        assert torch.equal(outs[0][k], outs[1][k]), (k, float((outs[0][k] - outs[1][k]).abs().max()))

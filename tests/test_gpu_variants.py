@@ -237,19 +237,3 @@ def test_bf16_fused_backward_register_dz_bitwise_equal(n, ns):
         assert torch.isfinite(g1[k]).all(), k
         assert torch.equal(g0[k], g1[k]), k
 
-
-@pytest.mark.parametrize("n,ns", [(300, 64), (2048, 64)])
-def test_bf16_tn_loader_waves_bitwise_equal(n, ns):
-    """The DMA weight-gradient GEMM with its LDS-DMA issued by 4 dedicated loader waves (option
-    tn_bf16_lw 4, k_gemm_tn_bf16l) against the default k_gemm_tn_bf16d: same tiles, same point
-    splits, same k order, bias sums in the same per-phase order — renders and every gradient bit for
-    bit.  2 048 x 128 points per pass take the >= 2^18-point paths (skip-layer tail split, the
-    deferred two-pass segments)."""
-    r0, g0 = _render_bf16({"tn_bf16_lw": 0}, n=n, ns=ns)
-    r1, g1 = _render_bf16({"tn_bf16_lw": 4}, n=n, ns=ns)
-    for k in r0:
-        assert torch.equal(r0[k], r1[k]), k
-    assert sorted(g0) == sorted(g1)
-    for k in g0:
-        assert torch.isfinite(g1[k]).all(), k
-        assert torch.equal(g0[k], g1[k]), k
