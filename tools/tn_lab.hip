@@ -1,0 +1,186 @@
+// Weight-gradient GEMM lab (tools only): slab[s][n][k] = Σ_p A[p][n]·B[p][k] over P points
+// (N = K = 512, bf16 operands, fp32 sums) — the library's LDS-DMA kernel (gemm_tn_bf16, row
+// layout [P][F]) against a kernel with NO LDS that loads its MFMA fragments straight from a
+// point-interleaved layout [P/8][F][8] (8 consecutive points of one feature = one 16-B lane
+// load, a wave's 64 lanes = 2 point groups x 32 features = two 512-B runs).
+//   make -C tools tn_lab && ./tools/tn_lab [P] [iters]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../sp-nerf_amd/csrc/common.h"
+#include "../sp-nerf_amd/csrc/gemm_bf16.h"
+
+using namespace spn;
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t e = (x);                                                \
+        if (e != hipSuccess) {                                             \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); \
+            exit(1);                                                       \
+        }                                                                  \
+    } while (0)
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// 256 x 256 tile per block, 8 waves of 128 x 64 (4 x 2 32x32 accumulators), one block per CU;
+// per 16-point k-step a wave loads its 4 A and 2 B fragments (16 B per lane each) from the
+// interleaved operands, DEPTH k-steps ahead in registers.
+template <int DEPTH>
+__global__ __launch_bounds__(512) void k_tn_direct(const bf16* __restrict__ A, const bf16* __restrict__ B, int P, int N,
+                                                   int K, int pps, float* slab, int resident) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nK = K / 256, ntiles = (N / 256) * nK;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = w / ntiles, t = w % ntiles;
+    const int n0 = (t / nK) * 256, k0 = (t % nK) * 256;
+    const int p_beg = resident ? 0 : split * pps, p_end = min(P, p_beg + pps);
+    const int nks = (p_end - p_beg) / 16;
+    const int wa = wid >> 2, wb = wid & 3, h = lane >> 5, m = lane & 31;
+    // lane bases: point group (p / 8 + h), feature n0 + 128 wa + m (+ 32 i) / k0 + 64 wb + m (+ 32 j)
+    const bf16* pa = A + ((int64_t)(p_beg / 8 + h) * N + n0 + 128 * wa + m) * 8;
+    const bf16* pb = B + ((int64_t)(p_beg / 8 + h) * K + k0 + 64 * wb + m) * 8;
+    const int64_t sa = (int64_t)2 * N * 8, sb = (int64_t)2 * K * 8;  // one k-step = 2 point groups
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    u32x4 ra[DEPTH][4], rb[DEPTH][2];
+    auto load = [&](int d, int ks) {
+        const int kc = min(ks, nks - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[d][i] = ldg16(pa + kc * sa + 32 * 8 * i);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) rb[d][j] = ldg16(pb + kc * sb + 32 * 8 * j);
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) load(d, d);
+    for (int ks0 = 0; ks0 < nks; ks0 += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            if (ks0 + d < nks) {  // block-uniform
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ra[d][i]),
+                                                                          __builtin_bit_cast(bf16x8, rb[d][j]), acc[i][j], 0, 0, 0);
+                load(d, ks0 + d + DEPTH);
+            }
+        }
+    }
+    float* out = slab + (int64_t)split * N * K;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int k = k0 + wb * 64 + j * 32 + m;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + wa * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                out[(int64_t)n * K + k] = acc[i][j][r];
+            }
+    }
+}
+
+__global__ void k_reduce(const float* slab, int splits, int64_t nk, float* out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nk) return;
+    float s = 0.f;
+    for (int q = 0; q < splits; ++q) s += slab[q * nk + e];
+    out[e] = s;
+}
+
+int main(int argc, char** argv) {
+    const int P = argc > 1 ? atoi(argv[1]) : 1 << 20;
+    const int iters = argc > 2 ? atoi(argv[2]) : 20;
+    const int N = 512, K = 512;
+    std::vector<uint16_t> a((size_t)P * N), b((size_t)P * K), ai(a.size()), bi(b.size());
+    srand(1);
+    auto rnd = [] {
+        float x = 2.f * (float)rand() / (float)RAND_MAX - 1.f;
+        uint32_t u;
+        memcpy(&u, &x, 4);
+        return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    };
+    for (auto& v : a) v = rnd();
+    for (auto& v : b) v = rnd();
+    for (int p = 0; p < P; ++p) {
+        for (int f = 0; f < N; ++f) ai[((size_t)(p / 8) * N + f) * 8 + p % 8] = a[(size_t)p * N + f];
+        for (int f = 0; f < K; ++f) bi[((size_t)(p / 8) * K + f) * 8 + p % 8] = b[(size_t)p * K + f];
+    }
+    bf16 *dA, *dB, *dAi, *dBi;
+    CK(hipMalloc(&dA, a.size() * 2));
+    CK(hipMalloc(&dB, b.size() * 2));
+    CK(hipMalloc(&dAi, a.size() * 2));
+    CK(hipMalloc(&dBi, b.size() * 2));
+    CK(hipMemcpy(dA, a.data(), a.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dB, b.data(), b.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dAi, ai.data(), ai.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dBi, bi.data(), bi.size() * 2, hipMemcpyHostToDevice));
+    const int splits = tn_splits_bf16(P, N, K);
+    float *slab, *slab_b, *ref, *got;
+    CK(hipMalloc(&slab, (size_t)splits * N * K * 4));
+    CK(hipMalloc(&slab_b, (size_t)splits * N * 4));
+    CK(hipMalloc(&ref, (size_t)N * K * 4));
+    CK(hipMalloc(&got, (size_t)N * K * 4));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](auto f) {
+        for (int i = 0; i < 3; ++i) f();
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; ++i) f();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        return 1e3 * ms / iters;
+    };
+    const double flop = 2.0 * P * N * K, bytes = 2.0 * P * (N + K);
+    // library kernel (row layout), its slab reduction on the side
+    TN16Args t;
+    t.A = dA; t.lda = N; t.B = dB; t.ldb = K; t.K1 = K;
+    t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K; t.slab_b = slab_b;
+    t.P = P; t.N = N; t.K = K;
+    const double ul = timeit([&] { gemm_tn_bf16(t, splits, 0); });
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, ref);
+    printf("P=%d splits=%d  library DMA TN: %8.1f us  %7.1f TF/s  %6.2f TB/s (operands)\n", P, splits, ul, flop / ul * 1e-6,
+           bytes / ul * 1e-6);
+    const int pps = (P + splits - 1) / splits;
+    auto run = [&](auto kern, const char* name, int resident = 0) {
+        const double us = timeit([&] { hipLaunchKernelGGL(kern, dim3(4 * splits), dim3(512), 0, 0, dAi, dBi, P, N, K, pps, slab, resident); });
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, got);
+        std::vector<float> hr((size_t)N * K), hg(hr.size());
+        CK(hipMemcpy(hr.data(), ref, hr.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hg.data(), got, hg.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0, mx = 0;
+        for (size_t i = 0; i < hr.size(); ++i) {
+            md = fmax(md, fabs((double)hr[i] - hg[i]));
+            mx = fmax(mx, fabs((double)hr[i]));
+        }
+        printf("%-24s %8.1f us  %7.1f TF/s  %6.2f TB/s  max|diff|/max|ref| %.2e\n", name, us, flop / us * 1e-6, bytes / us * 1e-6,
+               md / mx);
+    };
+    run(k_tn_direct<2>, "direct, 2 steps ahead");
+    run(k_tn_direct<3>, "direct, 3 steps ahead");
+    run(k_tn_direct<4>, "direct, 4 steps ahead");
+    run(k_tn_direct<2>, "direct 2, L2-resident", 1);
+    run(k_tn_direct<4>, "direct 4, L2-resident", 1);
+    CK(hipMemset(dAi, 0, a.size() * 2));
+    CK(hipMemset(dBi, 0, b.size() * 2));
+    run(k_tn_direct<2>, "direct 2, zero operands");
+    run(k_tn_direct<2>, "direct 2, zero + resident", 1);
+    return 0;
+}
