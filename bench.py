@@ -463,7 +463,7 @@ def measured_traffic(config, rays_per_rank, kernel_class):
     FETCH_SIZE / WRITE_SIZE passes, bytes = 2*FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md's
     gfx950 correction.  None when no profile of that (config, rays per rank) is committed (PMC
     counters cannot be read from inside the bench process, hence the profile file)."""
-    for rnd in ("r03",):
+    for rnd in ("r04",):
         rel = f"profiles/{rnd}/traffic_{config}_rays{rays_per_rank}.json"
         try:
             with open(os.path.join(ROOT, rel)) as f:
@@ -510,6 +510,18 @@ def roofline_of(dom, nt, traffic=None, traffic_src=None):
              algorithmic_bytes_per_launch=nt["bytes"] / max(1, nt["launches"]),
              avg_launch_us=1e3 * nt["ms"] / max(1, nt["launches"]))
     return r
+
+def top_rooflines(config, rays_per_rank, n):
+    """roofline_of for the n MFMA kernel functions with the most time in the profiled steps."""
+    classes = [k for k in _lib.prof_classes() if k in GEMM_CLASSES]
+    classes.sort(key=lambda k: -_lib.prof_read(k)["ms"])
+    out = {}
+    for k in classes[:n]:
+        r = roofline_of(k, _lib.prof_read(k), *measured_traffic(config, rays_per_rank, k))
+        out[k] = {f: r[f] for f in ("bound", "achieved", "unit", "frac", "mfma_frac", "hbm_frac", "avg_launch_us",
+                                    "traffic", "algorithmic_bytes_per_launch")}
+    return out
+
 
 def gemm_totals(steps):
     """Every MFMA launch of the profiled steps (GEMMs and fused trunk / heads kernels): counted
@@ -1050,6 +1062,9 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "config": {"workload": c["workload"], "global_batch": B * world, "rays_per_rank": B,
                    "samples_per_ray": ts.s_final, "parallelism": f"dp{world}"},
         "roofline": roofline_of(dom, nt, traffic, traffic_src),
+        # the same figures for the three MLP kernel functions with the most time (the dominant one
+        # first): which kernel is "dominant" can change between trees with nearly equal times
+        "rooflines_top3": top_rooflines(config, B, 3),
         "mlp_mfma_utilisation": gemm_totals(prof_steps),
         "allreduce_ms_per_step": allreduce_ms,
         "allreduce": (None if world == 1 else

@@ -375,8 +375,11 @@ int32_t stream_dep(Side* sd, hipStream_t from, hipStream_t to) {
 }
 }  // namespace
 int g_l0_split = 1;       // bf16 MLP: fc_net.0 on bf16 hi/lo planes (0 = fp32 MFMA GEMM)
-int g_trunk_l0 = 1;       // ... and inside the fused trunk launch: 1 = when nothing is saved (inference;
-                          // saving, 64-point tiles, it measured slower than the separate GEMM), 2 = always
+int g_trunk_l0 = 2;       // ... and inside the fused trunk launch: 1 = when nothing is saved (inference),
+                          // 2 = also when saving (the default since round 4: the 64-point register-D training
+                          // trunk with layer 0 against the separate hi/lo-plane GEMM + k_encode's planes:
+                          // C4 26.56 / 26.58 -> 26.44 / 26.36 ms, C4@512 4.248 -> 4.202 ms, same call; it had
+                          // measured 400 us slower on the round-2 trunk)
 
 template <typename T> struct RawOf;
 template <> struct RawOf<float> { using type = f32x4; };

@@ -93,14 +93,16 @@ def test_fused_trunk_matches_layerwise(dims, n_rays, guided, sc):
 
 
 def test_fused_trunk_with_layer0_when_saving_bitwise_vs_layerwise():
-    """trunk_l0=2: fc_net.0 inside the fused launch also when activations are saved (64-point
-    tiles, D = w0·cos(w0·z) of layer 0 from the trunk's epilogue); the default keeps it a
+    """trunk_l0=2 (the default): fc_net.0 inside the fused launch also when activations are saved
+    (64-point tiles, D = w0·cos(w0·z) of layer 0 from the trunk's epilogue); trunk_l0=1 keeps it a
     separate GEMM there."""
-    _lib.set_option("trunk_l0", 2)
+    old = _lib.get_option("trunk_l0")
     try:
-        test_fused_trunk_matches_layerwise(ModelDims(width=512, sem=True), 257, True, 0.1)
+        for l0 in (1, 2):   # the separate layer-0 GEMM when saving, and layer 0 inside the launch
+            _lib.set_option("trunk_l0", l0)
+            test_fused_trunk_matches_layerwise(ModelDims(width=512, sem=True), 257, True, 0.1)
     finally:
-        _lib.set_option("trunk_l0", 1)
+        _lib.set_option("trunk_l0", old)
 
 
 def test_fused_trunk_point_network_bitwise_vs_layerwise():
