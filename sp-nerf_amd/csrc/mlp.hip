@@ -1290,7 +1290,9 @@ static bool heads_fused_on(const Ctx& c, bool save, int mode) {
 }
 int g_pe_inline = 1;  // option "pe_inline": inference trunk with layer 0 encodes o + dir·z itself (no k_encode)
 static bool trunk_l0_on(const Ctx& c, bool save);
-static bool pe_inline_on(const Ctx& c, bool save) { return g_pe_inline && !save && trunk_l0_on(c, save); }
+// (training too since round 4: the trunk then writes the bf16 PE rows X0b the weight gradients read,
+// and no k_encode runs)
+static bool pe_inline_on(const Ctx& c, bool save) { return g_pe_inline && trunk_l0_on(c, save); }
 
 static bool trunk_l0_on(const Ctx& c, bool save) {
     return fused_trunk_on(c) && g_l0_split && (g_trunk_l0 == 2 || (g_trunk_l0 == 1 && !save)) && c.k.Wf16[0] >= 0 &&
@@ -1335,6 +1337,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
                 if (pe_inline_on(c, save)) {
                     a.rays = c.rays; a.rs = c.rs; a.dir_off = c.dir_off; a.z = c.z;
                     a.n_freq = d.K0 == 3 ? 0 : d.K0 / 6; a.K0 = d.K0;
+                    if (save) a.X0b_out = c.hb(c.w.X0b);
                 } else {
                     a.X0 = c.at(c.w.X0);
                 }
@@ -1364,7 +1367,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
             // in; out when saving H and D of every layer, or Z of every layer and the last H
             const double in = first == 0 ? (a.rays ? 4.0 * P : 4.0 * P * d.K0p) : 2.0 * P * (W + (d.skip > 0 ? d.K0p : 0));
             const double nout = !save ? 1.0 : (zs ? d.L - first + 1.0 : 2.0 * (d.L - first));
-            const double bytes = in + 2.0 * P * W * nout;
+            const double bytes = in + 2.0 * P * W * nout + (a.X0b_out ? 2.0 * P * d.K0p : 0.0);
             if constexpr (BF) {
                 // inference: the fused heads on the trunk's last LDS image (no H_L in HBM)
                 if (c.heads_done && c.out && heads_fused_on(c, save, mode) && trunk2_heads_ok(a)) {

@@ -72,6 +72,10 @@ struct TrunkArgs {
     const float* rays = nullptr;
     const float* z = nullptr;
     int rs = 0, dir_off = 0, n_freq = 0, K0 = 0;
+    // training with the inline encoding (k_trunk_bf16 only): the staging also writes each point's
+    // bf16 PE row (the hi plane = k_encode's X0b) here, for the weight gradients of layer 0 and the
+    // skip layer's PE columns
+    bf16* X0b_out = nullptr;
     // training (64-point tiles, trunk_sigma_ok): the σ head's pre-activation of every point from the
     // last layer's LDS image, hsave[p·8] = w_σ·H_L + b_σ in k_heads_fwd_v's arithmetic (lane l:
     // features 4l.. and 256 + 4l.., dot4, wave_total), so the heads kernel skips H_L (1 KB / point)

@@ -220,6 +220,8 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 *reinterpret_cast<u32x4*>(smem + act_off(row, 2 * x0ch + q)) = hi;
                 *reinterpret_cast<u32x4*>(smem + act_off(row, 3 * x0ch + q)) = lo;
                 if (g.skip > 0) *reinterpret_cast<u32x4*>(sx0 + x0_rel(row, q)) = hi;
+                // training, inline encoding: the bf16 PE row for the weight gradients (= X0b)
+                if (g.X0b_out && p0 + row < g.P) *reinterpret_cast<u32x4*>(g.X0b_out + (p0 + row) * g.K0p + q * 8) = hi;
             }
         } else {
 #pragma unroll
@@ -867,10 +869,10 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     SPN_ARG(a.P < (1ll << 31) / TW, "trunk_bf16: too many points (%lld)", (long long)a.P);
     bool save = false;
     for (int i = 1; i < a.L; ++i) save |= a.Ds[i] != nullptr;
-    SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0 && !save), "trunk_bf16: inline encoding needs z, rs, inference");
-    if (trunk2_supported(a, save)) return trunk2_bf16(a, s, save, flop, bytes);
+    SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0 && (!save || a.X0b_out)),
+            "trunk_bf16: inline encoding needs z, rs, and when saving the X0b output");
+    if (!a.X0b_out && trunk2_supported(a, save)) return trunk2_bf16(a, s, save, flop, bytes);
     const int tm = a.zround ? 64 : trunk_tile(save);  // the 128-point tiling has no fp16-Z path
-    SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0 && !save), "trunk_bf16: inline encoding needs z, rs, inference");
     SPN_ARG(!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, save)), "trunk_bf16: layer 0 unsupported for K0p=%d",
             a.K0p);
     TrunkArgs ad = a;

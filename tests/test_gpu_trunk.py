@@ -169,3 +169,16 @@ def test_training_trunk_sigma_rows_bitwise(dims, n_rays, guided, sc, n_samples):
     gradients bit for bit."""
     base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 0})
     _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 1}), base)
+
+
+@pytest.mark.parametrize("dims,n_rays,guided,sc,n_samples", [
+    (ModelDims(width=512, sem=True), 257, True, 0.1, 64),   # C3 flags: main + solar passes (sun directions)
+    (ModelDims(width=512), 33, False, 0.1, 32),             # ragged last tile
+])
+def test_training_trunk_inline_encoding_bitwise(dims, n_rays, guided, sc, n_samples):
+    """Training forwards with layer 0 in the trunk encode o + dir·z in the trunk's staging (option
+    pe_inline 1, the default: no k_encode launch, no fp32 [P][64] PE round trip; the trunk writes
+    the bf16 PE rows X0b the weight gradients read) against k_encode (pe_inline 0): the same
+    pe_value arithmetic, so renders and gradients bit for bit."""
+    base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"pe_inline": 0})
+    _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"pe_inline": 1}), base)
