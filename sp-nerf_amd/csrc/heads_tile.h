@@ -127,9 +127,10 @@ constexpr int RQ_BYTES = RQ_RAYS * 2 * HH * 4;     // per-ray Q rows of up to RQ
 // bf16 image at smem (img_off layout), complete and visible (after a barrier); ost / part (and,
 // RQ, srq) are LDS areas of the sizes above.  Writes the tile's output rows; every thread of the
 // 8-wave workgroup calls it (it contains barriers); on return the image may be overwritten.
-template <bool RQ>
-__device__ __forceinline__ void heads_tile(const HeadsFusedArgs& g, const PackedOffs& k, char* smem, float* ost,
-                                           float* part, float* srq, int64_t p0) {
+// GA / KA: HeadsFusedArgs / PackedOffs, possibly address-space qualified (the fused trunk passes
+// references into the kernarg segment)
+template <bool RQ, typename GA, typename KA>
+__device__ __forceinline__ void heads_tile(GA& g, KA& k, char* smem, float* ost, float* part, float* srq, int64_t p0) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const float* Pk = g.packed;
     const bf16* P16 = reinterpret_cast<const bf16*>(g.packed);
@@ -168,7 +169,7 @@ __device__ __forceinline__ void heads_tile(const HeadsFusedArgs& g, const Packed
     // samples per ray): the Q epilogue then reads LDS instead of an L2 round trip per row (read
     // after the barriers that follow the σ head)
     const int64_t ray0 = p0 / g.S;
-    const int nray = (int)((std::min<int64_t>(p0 + TM, g.P) - 1) / g.S - ray0) + 1;
+    const int nray = (int)((std::min<int64_t>(p0 + TM, (int64_t)g.P) - 1) / g.S - ray0) + 1;
     const bool rq_lds = RQ && full && nray <= RQ_RAYS && !(g.dbg & 4);  // block-uniform (dbg 4: A/B)
     if (rq_lds)
         for (int i = tid; i < nray * 2 * HH; i += 512) srq[i] = g.rbQ[ray0 * (2 * HH) + i];

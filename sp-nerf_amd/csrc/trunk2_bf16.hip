@@ -98,9 +98,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(bf16* t, int64_t p0,
 // by k_heads_bf16); their output staging is 8 KB beyond the trunk's LDS, their partials overlay
 // the PE tile (restaged by the next tile), and the weight ring is primed per tile instead of
 // running on through the heads.
+// The HEADS kernel's argument: the trunk's (first, so the kernarg-segment reads of TrunkArgs stay
+// valid) and the heads' — read per tile through an opaque kernarg pointer, so the compiler does not
+// hoist the heads' ~40 offsets out of the tile loop into registers live through the trunk layers
+struct Trunk2HeadsArgs : TrunkArgs {
+    HeadsFusedArgs hg;
+    PackedOffs hk;
+};
+
 template <int TM, bool L0, bool SAVE, bool HEADS = false>
-__global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(TrunkArgs g, int ntiles, HeadsFusedArgs hg,
-                                                                              PackedOffs hk) {
+__global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(
+    std::conditional_t<HEADS, Trunk2HeadsArgs, TrunkArgs> g, int ntiles) {
     using Geo = T2Geo<TM>;
     static_assert(!HEADS || (TM == 128 && !SAVE), "the fused heads: 128-point inference tiles");
     constexpr int NT = Geo::NT, NA = Geo::NA, NJ = Geo::NJ, CPT = Geo::CPT, PT = Geo::PT;
@@ -430,7 +438,10 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(T
             if (last) {
                 __syncthreads();
                 if constexpr (HEADS) {  // H_L stays on chip: the heads on this image
-                    hd::heads_tile<false>(hg, hk, smem, reinterpret_cast<float*>(smem + OST_OFF),
+                    typedef const __attribute__((address_space(4))) Trunk2HeadsArgs* KH;
+                    KH kh = (KH)__builtin_amdgcn_kernarg_segment_ptr();
+                    asm volatile("" : "+s"(kh));  // opaque per tile: the heads' argument loads stay here
+                    hd::heads_tile<false>(kh->hg, kh->hk, smem, reinterpret_cast<float*>(smem + OST_OFF),
                                           reinterpret_cast<float*>(smem + X0_OFF), nullptr, p0);
                 } else if (!(g.dbg & 1)) {
 #pragma unroll
@@ -465,12 +476,10 @@ template <int TM>
 static void launch_trunk2(const TrunkArgs& ad, hipStream_t s, bool l0, bool save, int ntiles) {
     using Geo = T2Geo<TM>;
     const dim3 grid(std::min(ntiles, num_cus() * Geo::WGS)), block(Geo::NT);
-    const HeadsFusedArgs hg{};
-    const PackedOffs hk{};
-    if (l0 && save) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, true>), grid, block, 0, s, ad, ntiles, hg, hk);
-    else if (l0) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, false>), grid, block, 0, s, ad, ntiles, hg, hk);
-    else if (save) hipLaunchKernelGGL((k_trunk2_bf16<TM, false, true>), grid, block, 0, s, ad, ntiles, hg, hk);
-    else hipLaunchKernelGGL((k_trunk2_bf16<TM, false, false>), grid, block, 0, s, ad, ntiles, hg, hk);
+    if (l0 && save) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, true>), grid, block, 0, s, ad, ntiles);
+    else if (l0) hipLaunchKernelGGL((k_trunk2_bf16<TM, true, false>), grid, block, 0, s, ad, ntiles);
+    else if (save) hipLaunchKernelGGL((k_trunk2_bf16<TM, false, true>), grid, block, 0, s, ad, ntiles);
+    else hipLaunchKernelGGL((k_trunk2_bf16<TM, false, false>), grid, block, 0, s, ad, ntiles);
 }
 
 int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, double bytes) {
@@ -502,18 +511,20 @@ int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const Pac
     SPN_ARG(h.P == a.P && h.S == a.S && h.NO <= hd::OST_LD && h.C <= 4 && k.Fnar16 >= 0, "trunk2_heads_bf16: bad heads");
     if (a.P == 0) return SPNERF_OK;
     const int ntiles = cdiv(a.P, 128);
-    TrunkArgs ad = a;
+    Trunk2HeadsArgs ad;
+    static_cast<TrunkArgs&>(ad) = a;
     ad.dbg = 0;
     ad.nt = 0;
     const bool l0 = a.X0 || a.rays;
     if (!l0) ad.rb0 = nullptr;
-    HeadsFusedArgs hd_ = h;
-    hd_.nt = 0;
-    hd_.dbg = 0;
+    ad.hg = h;
+    ad.hg.nt = 0;
+    ad.hg.dbg = 0;
+    ad.hk = k;
     const dim3 grid(std::min(ntiles, num_cus())), block(T2Geo<128>::NT);
     ProfScope prof("trunk_heads_bf16", s, flop, bytes);
-    if (l0) hipLaunchKernelGGL((k_trunk2_bf16<128, true, false, true>), grid, block, 0, s, ad, ntiles, hd_, k);
-    else hipLaunchKernelGGL((k_trunk2_bf16<128, false, false, true>), grid, block, 0, s, ad, ntiles, hd_, k);
+    if (l0) hipLaunchKernelGGL((k_trunk2_bf16<128, true, false, true>), grid, block, 0, s, ad, ntiles);
+    else hipLaunchKernelGGL((k_trunk2_bf16<128, false, false, true>), grid, block, 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
@@ -523,7 +534,7 @@ int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const Pac
 // resident workgroups per CU of the 64-point tiling (profiling aid: 2 expected)
 extern "C" int32_t spnerf_debug_trunk2_occupancy(int32_t save) {
     int n = -1;
-    const void* f = save ? (const void*)spn::k_trunk2_bf16<64, false, true> : (const void*)spn::k_trunk2_bf16<64, true, false>;
+    const void* f = save ? (const void*)spn::k_trunk2_bf16<64, false, true, false> : (const void*)spn::k_trunk2_bf16<64, true, false, false>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, spn::T2Geo<64>::NT, 0) != hipSuccess) return -1;
     return n;
 }
