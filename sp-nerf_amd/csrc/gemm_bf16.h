@@ -69,4 +69,19 @@ extern int g_tn16_min_points;  // fewest points per split (option "tn_bf16_min_p
 int tn_splits_bf16(int P, int N, int K, int variant = -1, int few = -1);
 int32_t gemm_tn_bf16(const TN16Args& a, int splits, hipStream_t s);
 
+// Up to kTnGroup weight-gradient GEMMs (each its own operands, shape and slabs) in ONE launch
+// of the DMA kernel, splits[i] point splits for GEMM i (option tn_group in mlp.hip): a 512 x 512
+// GEMM has 4 tiles, so alone it fills the CUs with 64 splits and writes 64 MB of partial slabs;
+// n of them together need 1/n of the splits each (n x fewer slab bytes, one launch, one tail).
+constexpr int kTnGroup = 10;
+constexpr int kTnGroupRounds = 2;  // most blocks per CU a group launch may take (option tn_group_rounds)
+struct TN16Group {
+    TN16Args g[kTnGroup];
+    int start[kTnGroup + 1];  // GEMM i's blocks: [start[i], start[i + 1])
+    int n = 1;
+};
+bool tn_group_ok(int P, int N, int K);  // the shape runs on the DMA kernel
+int tn_tiles_bf16(int N, int K);        // its 256 x 256 tiles
+int32_t gemm_tn_bf16_group(const TN16Args* a, int n, const int* splits, hipStream_t s);
+
 }  // namespace spn

@@ -1252,15 +1252,22 @@ constexpr int TD_STEP = 32, TD_STAGES = 4, TD_STG = 4 * TD_STEP * 256;  // bytes
 // IP: where a step issues the next DMA step: 0 = before its MFMAs, 1 = after them, 2 = between
 // its two k-halves (default, option tn_bf16_ip: a wave stalled on the DMA issue then has MFMAs
 // in flight; 393 -> 365 us on 524 288 x 512 x 512, C4 TN 7.18 -> 6.81 ms/step)
+// A group launch (gemm_tn_bf16_group) runs G.n GEMMs in one grid, blocks [start[gi],
+// start[gi + 1]) on GEMM gi — consecutive after the XCD remap, so a split keeps its tiles
+// (which share operand rows) on one XCD as in a single launch.
 template <int IP>
-__global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Args g) {
+__global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     __shared__ __attribute__((aligned(16))) char smem[TD_STAGES * TD_STG];  // [stage][A0|A1|B0|B1]
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     typedef __attribute__((address_space(1))) void* gbl_ptr_t;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    int gi = 0;
+    while (gi + 1 < G.n && wg >= G.start[gi + 1]) ++gi;
+    const int w = wg - G.start[gi];
+    const TN16Args& g = G.g[gi];
     const int nK = (g.K + TW - 1) / TW;
     const int ntiles = cdiv(g.N, TW) * nK;
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
     const int split = w / ntiles, t = w % ntiles;
     const int n0 = (t / nK) * TW, k0 = (t % nK) * TW;
     const int p_beg = split * g.p_per_split;
@@ -1597,6 +1604,53 @@ int tn_splits_bf16(int P, int N, int K, int variant, int few) {
     return splits < 1 ? 1 : splits;
 }
 
+static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip, hipStream_t s) {
+    TN16Group G;
+    G.n = n;
+    G.start[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        G.g[i] = a[i];
+        G.start[i + 1] = G.start[i] + blocks[i];
+    }
+    const dim3 grid(G.start[n]), block(512);
+    if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, grid, block, 0, s, G);
+    else if (ip == 1) hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, grid, block, 0, s, G);
+    else hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, grid, block, 0, s, G);
+}
+
+bool tn_group_ok(int P, int N, int K) { return g_tn16_variant == 3 && !tn_k64(N, K) && tn_wide(N, K, -1) && P % TD_STEP == 0; }
+int tn_tiles_bf16(int N, int K) { return cdiv(N, TW) * cdiv(K, TW); }
+
+int32_t gemm_tn_bf16_group(const TN16Args* a0, int n, const int* splits, hipStream_t s) {
+    SPN_ARG(n >= 1 && n <= kTnGroup, "gemm_tn_bf16_group: %d GEMMs (at most %d)", n, kTnGroup);
+    TN16Args a[kTnGroup];
+    int blocks[kTnGroup];
+    double flop = 0.0, bytes = 0.0;
+    for (int i = 0; i < n; ++i) {
+        a[i] = a0[i];
+        const TN16Args& q = a[i];
+        SPN_ARG(splits[i] >= 1 && q.K1 >= q.K && !q.b_sin, "gemm_tn_bf16_group: GEMM %d: one B segment, >= 1 split", i);
+        SPN_ARG(q.lda % 8 == 0 && q.ldb % 8 == 0 && q.A && q.B && q.slab && q.slab_b, "gemm_tn_bf16_group: operands");
+        const bool two = q.P1 < q.P;
+        SPN_ARG(!two || (q.A_s2 && q.B_s2 && q.P1 % TD_STEP == 0), "gemm_tn_bf16_group: second segment");
+        SPN_ARG(tn_group_ok(q.P, q.N, q.K), "gemm_tn_bf16_group: shape N=%d K=%d P=%d not on the DMA tiles", q.N, q.K, q.P);
+        int pps = cdiv(q.P, splits[i]);
+        pps = (pps + 63) / 64 * 64;
+        a[i].p_per_split = pps < 64 ? 64 : pps;
+        a[i].bias_split = g_tn16_bias_split;
+        blocks[i] = q.P > 0 ? tn_tiles_bf16(q.N, q.K) * splits[i] : 0;
+        flop += 2.0 * q.P * q.N * q.K;
+        bytes += 2.0 * (double)q.P * (q.N + q.K) + 4.0 * splits[i] * (double)q.N * q.K;
+    }
+    int total = 0;
+    for (int i = 0; i < n; ++i) total += blocks[i];
+    if (total == 0) return SPNERF_OK;
+    ProfScope prof("gemm_tn_bf16d", s, flop, bytes);
+    launch_tn_bf16d(a, n, blocks, g_tn16_ip, s);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
 int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     TN16Args a = a0;
     SPN_ARG(a.N > 0 && a.K > 0 && a.P >= 0 && splits >= 1, "gemm_tn_bf16: bad shape");
@@ -1625,10 +1679,8 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
         if (dma)  // B staged as is
         {
             a.bias_split = g_tn16_bias_split;
-            const int ip = (a.dbg & 4) ? 2 : (a.dbg & 2) ? 1 : g_tn16_ip;
-            if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, dim3(nb * splits), dim3(512), 0, s, a);
-            else if (ip == 1) hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, dim3(nb * splits), dim3(512), 0, s, a);
-            else hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, dim3(nb * splits), dim3(512), 0, s, a);
+            const int blocks = nb * splits;
+            launch_tn_bf16d(&a, 1, &blocks, (a.dbg & 4) ? 2 : (a.dbg & 2) ? 1 : g_tn16_ip, s);
         }
         else
             hipLaunchKernelGGL(k_gemm_tn_bf16w, dim3(nb * splits), dim3(512), 0, s, a);

@@ -1104,6 +1104,15 @@ struct Gemms<bf16> {
 };
 
 int g_tn_split_tail = 1;  // option "tn_split_tail": see tn_grad
+// option "tn_group": deferred weight-gradient GEMMs per launch (trunk_wgrad; 1 = one launch each).
+// All 9 of a W = 512 model (sun_v_net.4 / .2, trunk layers 7 .. 1) in one launch: C4 at 512 rays
+// 4.252 / 4.288 -> 4.033 / 4.036 ms, at 4 096 rays 26.57 / 26.49 -> 26.50 / 26.45 (same call; the
+// slab reductions 0.35 -> 0.22 ms per step)
+int g_tn_group = 9;
+// option "tn_group_rounds": a group launch's blocks per CU (≤ kTnGroupRounds); 0 = 2 when a block
+// would otherwise take ≥ 64 K points (C4 at 4 096 rays: 26.29 / 26.32 -> 26.25 / 26.26 ms), else 1
+// (at 512 rays 2 rounds measured 3.976 / 3.977 against 3.963 / 3.964 ms)
+int g_tn_group_rounds = 0;
 
 #ifndef SPN_DEFER_SUNV
 #define SPN_DEFER_SUNV 1  // sun_v_net.2 / .4's weight gradients deferred with the trunk's (0: A/B builds)
@@ -1837,9 +1846,100 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
         Ctx c2 = two ? ctx(j + 1) : c;
         if (two) SPN_ARG(wss[j + 1] && (flags[j + 1] & SPNERF_MLP_SAVE), "spnerf_mlp_trunk_wgrad: bad segment");
         if (c.w.P + (two ? c2.w.P : 0) == 0) continue;
+        auto dzl = [&](const Ctx& q, int i) { return q.hb(i == d.L - 1 ? q.w.dZa : q.w.Db[i]); };
+        const int64_t Pt = c.w.P + (two ? c2.w.P : 0);
+        const int H = d.H;
+        // option tn_group (> 1): sun_v_net.4 / .2 and the trunk layers L-1 .. 1 (the skip layer's
+        // H part; its PE tail on the narrow kernel) run g_tn_group GEMMs per launch of the DMA
+        // kernel, one split count for all (equal points per block), the slab shared out among them
+        struct Item {
+            TN16Args t;
+            ReduceArgs r;
+            int mark, layer;
+        };
+        std::vector<Item> items;
+        bool sunv_grouped = false, grouped[16] = {};
+        if (g_tn_group > 1 && (!two || c.w.P % 32 == 0)) {
+            auto add = [&](const bf16* A, const bf16* A2, int N, const bf16* B, const bf16* B2, int ldb, int K, float* dW,
+                           int ldW, float* db, int mark, int layer) {
+                if (!tn_group_ok((int)Pt, N, K)) return false;
+                Item it;
+                it.t.A = A; it.t.lda = N; it.t.B = B; it.t.ldb = ldb; it.t.K1 = K;
+                it.t.P = (int)Pt; it.t.N = N; it.t.K = K;
+                it.t.ld_slab = K; it.t.slab_stride = (int64_t)N * K;
+                if (two) {
+                    it.t.P1 = c.w.P;
+                    it.t.A_s2 = A2 - c.w.P * N;
+                    it.t.B_s2 = B2 - c.w.P * ldb;
+                }
+                it.r = red(0, N, K, dW, ldW, db);
+                it.mark = mark;
+                it.layer = layer;
+                items.push_back(it);
+                return true;
+            };
+            if (SPN_DEFER_SUNV && tn_group_ok((int)Pt, H, H)) {
+                add(c.hb(c.w.dS3), c2.hb(c2.w.dS3), H, c.hb(c.w.S2), c2.hb(c2.w.S2), H, H, gp(x.s3W), H, gp(x.s3b), 0, -1);
+                add(c.hb(c.w.dS2), c2.hb(c2.w.dS2), H, c.hb(c.w.Q), c2.hb(c2.w.Q), d.NQ, H, gp(x.s2W), H, gp(x.s2b), 0, -1);
+                sunv_grouped = true;
+            }
+            for (int i = d.L - 1; i >= 1; --i)
+                if ((c.k.Kp[i] == W || i == d.skip) && i < 16)
+                    grouped[i] = add(dzl(c, i), dzl(c2, i), W, c.hb(c.w.Hb[i - 1]), c2.hb(c2.w.Hb[i - 1]), W, W,
+                                     gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]), 1 + (d.L - 1 - i), i);
+        }
+        for (size_t g0 = 0; g0 < items.size();) {
+            const size_t g1 = std::min(items.size(), g0 + (size_t)std::min(g_tn_group, kTnGroup));
+            int64_t tiles = 0, nk = 0, nn = 0;
+            for (size_t q = g0; q < g1; ++q) {
+                tiles += tn_tiles_bf16(items[q].t.N, items[q].t.K);
+                nk += (int64_t)items[q].t.N * items[q].t.K;
+                nn += items[q].t.N;
+            }
+            // one split count for the group (equal points per block): rounds x the CUs' worth of
+            // blocks, within the workspace's slab capacity
+            const int64_t sp1 = std::max<int64_t>(1, num_cus() / tiles);
+            const int rounds = g_tn_group_rounds > 0 ? std::min(g_tn_group_rounds, kTnGroupRounds)
+                                                     : (Pt / sp1 >= 65536 ? 2 : 1);
+            const int64_t sp = std::max<int64_t>(1, std::min({(int64_t)rounds * num_cus() / tiles, (int64_t)cdiv(Pt, g_tn16_min_points),
+                                                             c.w.slab_n / nk, c.w.slab_b_n / nn}));
+            SPN_ARG(sp * nk <= c.w.slab_n && sp * nn <= c.w.slab_b_n, "trunk_wgrad: slab capacity for a group of %d GEMMs",
+                    (int)(g1 - g0));
+            TN16Args t[kTnGroup];
+            int spl[kTnGroup];
+            ReduceArgs r[kTnGroup];
+            int64_t off = 0, off_b = 0;
+            bool skip_in = false, sunv_in = false;
+            for (size_t q = g0; q < g1; ++q) {
+                Item& it = items[q];
+                it.t.slab = c.at(c.w.slab) + off;
+                it.t.slab_b = c.at(c.w.slab_b) + off_b;
+                off += sp * it.t.slab_stride;
+                off_b += sp * it.t.N;
+                it.r.slab = it.t.slab; it.r.ld_slab = it.t.K; it.r.slab_stride = it.t.slab_stride; it.r.splits = (int)sp;
+                it.r.N = it.t.N; it.r.slab_b = it.t.slab_b; it.r.accumulate = c.acc;
+                t[q - g0] = it.t;
+                spl[q - g0] = (int)sp;
+                r[q - g0] = it.r;
+                skip_in = skip_in || it.layer == d.skip;
+                sunv_in = sunv_in || it.layer < 0;
+            }
+            const int n = (int)(g1 - g0);
+            SPN_TRY(gemm_tn_bf16_group(t, n, spl, s));
+            for (int q = 0; q < n; q += kReduceMulti) SPN_TRY(reduce_slabs_multi(r + q, std::min(kReduceMulti, n - q), s));
+            if (skip_in) {  // the skip layer's PE columns: N = W, K = K0p (the narrow kernel)
+                const int l = d.skip;
+                const TnSeg st{dzl(c2, l), c2.hb(c2.w.X0b), nullptr, c2.w.P};
+                SPN_TRY(tn_grad<bf16>(c, dzl(c, l), W, W, c.hb(c.w.X0b), d.K0p, nullptr, 0, d.K0p, d.K0p, s,
+                                      {red(0, W, d.K0, gp(x.fcW[l]) + W, ld(x.fcW[l]), nullptr)}, false, two ? &st : nullptr));
+            }
+            if (sunv_in) SPN_TRY(grad_mark(0, s));
+            for (size_t q = g0; q < g1; ++q)
+                if (items[q].layer >= 0) SPN_TRY(grad_mark(items[q].mark, s));
+            g0 = g1;
+        }
         // sun_v_net.4 and .2 (sun-visibility head, in every pass): dW = dZᵀ · input over all points
-        if (SPN_DEFER_SUNV) {
-            const int H = d.H;
+        if (SPN_DEFER_SUNV && !sunv_grouped) {
             const TnSeg s3{c2.hb(c2.w.dS3), c2.hb(c2.w.S2), nullptr, c2.w.P};
             SPN_TRY(tn_grad<bf16>(c, c.hb(c.w.dS3), H, H, c.hb(c.w.S2), H, nullptr, 0, H, H, s,
                                   {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}, false, two ? &s3 : nullptr));
@@ -1849,7 +1949,8 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
             SPN_TRY(grad_mark(0, s));   // the heads' gradients are final again
         }
         for (int i = d.L - 1; i >= 0; --i) {
-            auto dz = [&](const Ctx& q) { return q.hb(i == d.L - 1 ? q.w.dZa : q.w.Db[i]); };
+            if (i < 16 && grouped[i]) continue;
+            auto dz = [&](const Ctx& q) { return dzl(q, i); };
             auto in = [&](const Ctx& q) { return q.hb(i == 0 ? q.w.X0b : q.w.Hb[i - 1]); };
             const int ldin = i == 0 ? d.K0p : W;
             const int kreal = i == 0 ? d.K0 : (i == d.skip ? W + d.K0 : W);
@@ -1979,6 +2080,8 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_ip") return &g_tn16_ip;
     if (n == "tn_bf16_bias_split") return &g_tn16_bias_split;
     if (n == "tn_bf16_few_tiles") return &g_tn16_few_tiles;
+    if (n == "tn_group") return &g_tn_group;
+    if (n == "tn_group_rounds") return &g_tn_group_rounds;
     if (n == "tn_bf16_k64") return &g_tn16_k64;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;

@@ -241,6 +241,17 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         need(d.NG, W);
         need(d.NQ, W);
         need(H, H);
+        if (d.bf && d.W % 256 == 0) {
+            // grouped weight gradients (mlp.hip trunk_wgrad, option tn_group): up to
+            // kTnGroupRounds x num_cus() 256 x 256 blocks of the DMA kernel, each its own slab tile,
+            // over both passes' points (at most 2P here; trunk_wgrad clamps to this capacity)
+            const int64_t blocks = std::min<int64_t>((int64_t)kTnGroupRounds * num_cus(),
+                                                     (int64_t)kTnGroup * 4 * ((2 * P + 1023) / 1024));
+            slab = std::max(slab, blocks * 256 * 256);
+            slab_b = std::max(slab_b, blocks * 256);
+        }
+        w.slab_n = slab;
+        w.slab_b_n = slab_b;
         w.slab = take(slab);
         w.slab_b = take(slab_b);
         w.RQ = take(B * d.NQ);

@@ -89,6 +89,7 @@ struct WS {
     // backward
     int64_t dZG, dZQ, dS3, dS2, dZa, dZb, dZc, hpre, slab, slab_b, RQ, R0, R4, Rp0, Rp4, dsky, skyd, skydh, gemb, embr, sk_slab, sk_slab_b;
     int64_t sk_slab_n = 0, sk_slab_b_n = 0;  // their capacities (floats)
+    int64_t slab_n = 0, slab_b_n = 0;        // the TN slabs' capacities (floats)
     int64_t total;
 };
 WS ws_layout(const Dims& d, int64_t n_rays, int32_t n_samples, int32_t flags);

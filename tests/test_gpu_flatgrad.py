@@ -80,3 +80,64 @@ def test_deferred_trunk_weight_gradients_match_per_pass(sem):
             assert float((a - b).norm() / a.norm()) <= 1e-3, n
     assert (num / den) ** 0.5 <= 1e-5
     assert float(grads[True]["fc_net.2.weight"].norm()) > 0
+
+
+def _deferred_grads(tn_group, n_rays=96, rounds=1):
+    """Flat bf16 gradients of a main + solar render with the deferred trunk weight gradients, and
+    the number of DMA weight-gradient launches they took."""
+    import types
+    from spnerf_amd import _lib
+    args = types.SimpleNamespace(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+                                 sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)
+    rays = torch.tensor(gu_rays(n_rays, 4), device=DEV)
+    g = torch.Generator().manual_seed(3)
+    depths = torch.rand(n_rays, 2, generator=g).to(DEV) * 0.5 + 0.2
+    valid = (torch.rand(n_rays, generator=g) > 0.3).long().to(DEV)
+    sems = torch.randint(0, 3, (n_rays,), generator=g).to(DEV)
+    old = _lib.get_option("tn_group"), _lib.get_option("tn_group_rounds")
+    _lib.set_option("tn_group", tn_group)
+    _lib.set_option("tn_group_rounds", rounds)
+    try:
+        torch.manual_seed(0)
+        m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True,
+                              precision="bf16").to(DEV).use_flat_grads()
+        m.defer_trunk_wgrad = True
+        with spnerf_amd.random_source(spnerf_amd.PhiloxRandom(seed=5)):
+            res = spnerf_amd.render_rays({"coarse": m}, args, rays, None, semantics=sems, mode="train",
+                                         valid_depth=valid, target_depths=depths, target_std=depths[:, 1] * 0 + 0.01)
+        loss = (res["rgb_coarse"] ** 2).mean() + res["sun_sc_coarse"].mean() + res["depth_coarse"].mean()
+        torch.cuda.synchronize()
+        _lib.prof_reset()
+        _lib.prof_enable(True)
+        loss.backward()
+        torch.cuda.synchronize()
+        _lib.prof_enable(False)
+        launches = _lib.prof_read("gemm_tn_bf16d")["launches"] if "gemm_tn_bf16d" in _lib.prof_classes() else 0
+        return {n: p.grad.detach().clone() for n, p in m.named_parameters()}, launches
+    finally:
+        _lib.set_option("tn_group", old[0])
+        _lib.set_option("tn_group_rounds", old[1])
+
+
+@pytest.mark.parametrize("group,rounds", [(4, 1), (9, 1), (9, 2)])
+def test_grouped_trunk_weight_gradients_match(group, rounds):
+    """Option tn_group: the deferred sun_v and trunk-layer weight-gradient GEMMs (the skip layer's
+    H part; its PE tail on the narrow kernel) run `group` per launch of the DMA kernel, each with
+    1/group of the splits (`rounds` blocks per CU).  Fewer launches, the same gradients up to fp32
+    summation order."""
+    g1, n1 = _deferred_grads(1)
+    g2, n2 = _deferred_grads(group, rounds=rounds)
+    assert n2 < n1, (n1, n2)
+    num = den = 0.0
+    for n, a in g1.items():
+        b = g2[n]
+        assert torch.isfinite(b).all(), n
+        num += float(((a - b).double() ** 2).sum())
+        den += float((a.double() ** 2).sum())
+        if a.numel() >= 64 and float(a.norm()) > 0:
+            assert float((a - b).norm() / a.norm()) <= 1e-4, n
+    assert (num / den) ** 0.5 <= 1e-5
+    # deterministic: the same grouping twice is bit for bit the same
+    g3, _ = _deferred_grads(group, rounds=rounds)
+    for n in g2:
+        assert torch.equal(g2[n], g3[n]), n
