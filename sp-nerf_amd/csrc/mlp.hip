@@ -1113,6 +1113,13 @@ int g_tn_group = 9;
 // would otherwise take ≥ 64 K points (C4 at 4 096 rays: 26.29 / 26.32 -> 26.25 / 26.26 ms), else 1
 // (at 512 rays 2 rounds measured 3.976 / 3.977 against 3.963 / 3.964 ms)
 int g_tn_group_rounds = 0;
+// option "defer_heads": under deferred trunk weight gradients the output heads' G / Q weight
+// gradients run in trunk_wgrad too (one GEMM over every pass's points, inside the group launch)
+// — 1 always, 0 never, 2 (default) for passes of at most 2^18 points: C4 at 512 rays 3.970 / 3.973
+// -> 3.926 / 3.917 ms, while at 4 096 rays the per-pass GEMMs overlapping the dX chain on the side
+// stream are worth more (26.04 / 26.14 against 26.16 / 26.19 ms deferred; same call)
+int g_defer_heads = 2;
+static bool defer_heads_for(int64_t P) { return g_defer_heads == 1 || (g_defer_heads == 2 && P <= (1 << 18)); }
 
 #ifndef SPN_DEFER_SUNV
 #define SPN_DEFER_SUNV 1  // sun_v_net.2 / .4's weight gradients deferred with the trunk's (0: A/B builds)
@@ -1679,8 +1686,12 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     }
     // 4. feat: dF = dZ_Q · WQ → dZG[:, :W];  dWQ = dZ_Q^T · feat
     const int NQ = mode == 0 ? d.NQ : H;
+    // deferred (SPNERF_MLP_DEFER_TRUNK_WGRAD, option defer_heads): the G / Q weight gradients run in
+    // spnerf_mlp_trunk_wgrad, over every pass's points in one GEMM each
+    const bool heads_def = c.defer && defer_heads_for(P);
     {
-        if (mode == 0) {
+        if (heads_def) {
+        } else if (mode == 0) {
             if (d.beta)
                 SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, NQ, Gb, d.NG, nullptr, 0, W, W, s2,
                                    {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b)),
@@ -1708,14 +1719,15 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
     int cur = 0;
     T* dZ = dzb[cur];
     {
-        if (mode == 0 && d.sem)
+        if (heads_def) {
+        } else if (mode == 0 && d.sem)
             SPN_TRY(tn_grad<T>(c, dZG, d.NG, d.NG, HL, W, nullptr, 0, W, W, s2,
                                {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
         else
             SPN_TRY(tn_grad<T>(c, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s2, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
         // every output head's gradient is final (spnerf_grad_marks) — unless sun_v_net.2 / .4's
         // are deferred: then spnerf_mlp_trunk_wgrad records the mark once they are
-        if (!c.defer || !SPN_DEFER_SUNV) SPN_TRY(grad_mark(0, s2));
+        if (!c.defer || (!SPN_DEFER_SUNV && !heads_def)) SPN_TRY(grad_mark(0, s2));
         NT g;
         g.A = dZG; g.lda = d.NG; g.K1 = NG; g.B = G::w(c, c.k.WGT, c.k.WGT16); g.ldb = d.NG; g.C = dZ; g.ldc = W;
         g.M = (int)P; g.N = W; g.K = NG;
@@ -1849,94 +1861,180 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
         auto dzl = [&](const Ctx& q, int i) { return q.hb(i == d.L - 1 ? q.w.dZa : q.w.Db[i]); };
         const int64_t Pt = c.w.P + (two ? c2.w.P : 0);
         const int H = d.H;
-        // option tn_group (> 1): sun_v_net.4 / .2 and the trunk layers L-1 .. 1 (the skip layer's
-        // H part; its PE tail on the narrow kernel) run g_tn_group GEMMs per launch of the DMA
-        // kernel, one split count for all (equal points per block), the slab shared out among them
+        // option tn_group (> 1): the output heads' G / Q weight gradients (defer_heads), sun_v_net.4
+        // / .2 and the trunk layers L-1 .. 1 (the skip layer's H part; its PE tail on the narrow
+        // kernel) run g_tn_group GEMMs per launch of the DMA kernel, splits in proportion to each
+        // GEMM's points (equal points per block), the slab shared out among them
         struct Item {
             TN16Args t;
-            ReduceArgs r;
-            int mark, layer;
+            ReduceArgs r[3];
+            int nr, mark, layer;
         };
         std::vector<Item> items;
-        bool sunv_grouped = false, grouped[16] = {};
-        if (g_tn_group > 1 && (!two || c.w.P % 32 == 0)) {
-            auto add = [&](const bf16* A, const bf16* A2, int N, const bf16* B, const bf16* B2, int ldb, int K, float* dW,
-                           int ldW, float* db, int mark, int layer) {
-                if (!tn_group_ok((int)Pt, N, K)) return false;
-                Item it;
-                it.t.A = A; it.t.lda = N; it.t.B = B; it.t.ldb = ldb; it.t.K1 = K;
-                it.t.P = (int)Pt; it.t.N = N; it.t.K = K;
-                it.t.ld_slab = K; it.t.slab_stride = (int64_t)N * K;
-                if (two) {
-                    it.t.P1 = c.w.P;
-                    it.t.A_s2 = A2 - c.w.P * N;
-                    it.t.B_s2 = B2 - c.w.P * ldb;
+        bool sunv_grouped = false, heads_grouped = false, grouped[16] = {};
+        const int mode_a = (flags[j] & SPNERF_MLP_SUN_ONLY) ? 2 : 0;
+        const int mode_b = two ? ((flags[j + 1] & SPNERF_MLP_SUN_ONLY) ? 2 : 0) : -1;
+        // segment a (c) and / or b (c2) of one GEMM: A / B pointers of each, nullptr = not in it
+        struct Seg2 {
+            const bf16 *A1, *B1;
+            int64_t P1;
+            const bf16 *A2, *B2;
+            int64_t P2;
+        };
+        auto seg2 = [&](const bf16* Aa, const bf16* Ba, bool in_a, const bf16* Ab, const bf16* Bb, bool in_b) {
+            Seg2 g{nullptr, nullptr, 0, nullptr, nullptr, 0};
+            if (in_a) g = {Aa, Ba, c.w.P, nullptr, nullptr, 0};
+            if (in_b) {
+                if (in_a) g.A2 = Ab, g.B2 = Bb, g.P2 = c2.w.P;
+                else g = {Ab, Bb, c2.w.P, nullptr, nullptr, 0};
+            }
+            return g;
+        };
+        auto item_ok = [&](const Seg2& g, int N, int K) {
+            return g.P1 + g.P2 > 0 && tn_group_ok((int)(g.P1 + g.P2), N, K) && (g.P2 == 0 || g.P1 % 32 == 0);
+        };
+        auto add = [&](const Seg2& g, int lda, int N, int ldb, int K, std::initializer_list<ReduceArgs> reds, int mark,
+                       int layer) {
+            Item it;
+            it.t.A = g.A1; it.t.lda = lda; it.t.B = g.B1; it.t.ldb = ldb; it.t.K1 = K;
+            it.t.P = (int)(g.P1 + g.P2); it.t.N = N; it.t.K = K;
+            it.t.ld_slab = K; it.t.slab_stride = (int64_t)N * K;
+            if (g.P2) {
+                it.t.P1 = g.P1;
+                it.t.A_s2 = g.A2 - g.P1 * lda;
+                it.t.B_s2 = g.B2 - g.P1 * ldb;
+            }
+            it.nr = 0;
+            for (const ReduceArgs& r : reds) it.r[it.nr++] = r;
+            it.mark = mark;
+            it.layer = layer;
+            items.push_back(it);
+        };
+        const bool grp = g_tn_group > 1;
+        const bool hda = defer_heads_for(c.w.P), hdb = two && defer_heads_for(c2.w.P), hd = hda || hdb;
+        if (grp && hda && (!two || hdb)) {
+            // feat (+ the semantic hidden rows) = dZ_Gᵀ · H_L; sun_v_net.0 (+ rgb / beta rows) = dZ_Qᵀ · G[:, :W]
+            const bool m0a = mode_a == 0, m0b = mode_b == 0;
+            const Seg2 gf = seg2(c.hb(c.w.dZG), c.hb(c.w.Hb[d.L - 1]), true, c2.hb(c2.w.dZG), c2.hb(c2.w.Hb[d.L - 1]), two);
+            const Seg2 gm = seg2(c.hb(c.w.dZG) + W, c.hb(c.w.Hb[d.L - 1]), m0a, c2.hb(c2.w.dZG) + W, c2.hb(c2.w.Hb[d.L - 1]),
+                                 m0b);
+            const Seg2 qs = seg2(c.hb(c.w.dZQ), c.hb(c.w.G), true, c2.hb(c2.w.dZQ), c2.hb(c2.w.G), two);
+            const Seg2 qr = seg2(c.hb(c.w.dZQ) + H, c.hb(c.w.G), m0a, c2.hb(c2.w.dZQ) + H, c2.hb(c2.w.G), m0b);
+            const int nqr = d.beta ? 2 * H : H;
+            const bool any0 = m0a || m0b;
+            if (item_ok(gf, W, W) && item_ok(qs, H, W) && (!any0 || ((!d.sem || item_ok(gm, H, W)) && item_ok(qr, nqr, W)))) {
+                add(gf, d.NG, W, W, W, {red(0, W, W, gp(x.featW), W, gp(x.featb))}, 0, -1);
+                add(qs, d.NQ, H, d.NG, W, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}, 0, -1);
+                if (any0) {
+                    if (d.sem) add(gm, d.NG, H, W, W, {red(0, H, W, gp(x.m1W), W, gp(x.m1b))}, 0, -1);
+                    if (d.beta)
+                        add(qr, d.NQ, nqr, d.NG, W,
+                            {red(0, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b)), red(H, H, W, gp(x.b1W), ld(x.b1W), gp(x.b1b))}, 0, -1);
+                    else
+                        add(qr, d.NQ, nqr, d.NG, W, {red(0, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b))}, 0, -1);
                 }
-                it.r = red(0, N, K, dW, ldW, db);
-                it.mark = mark;
-                it.layer = layer;
-                items.push_back(it);
-                return true;
-            };
-            if (SPN_DEFER_SUNV && tn_group_ok((int)Pt, H, H)) {
-                add(c.hb(c.w.dS3), c2.hb(c2.w.dS3), H, c.hb(c.w.S2), c2.hb(c2.w.S2), H, H, gp(x.s3W), H, gp(x.s3b), 0, -1);
-                add(c.hb(c.w.dS2), c2.hb(c2.w.dS2), H, c.hb(c.w.Q), c2.hb(c2.w.Q), d.NQ, H, gp(x.s2W), H, gp(x.s2b), 0, -1);
+                heads_grouped = true;
+            }
+        }
+        if (grp && SPN_DEFER_SUNV) {
+            const Seg2 g3 = seg2(c.hb(c.w.dS3), c.hb(c.w.S2), true, c2.hb(c2.w.dS3), c2.hb(c2.w.S2), two);
+            const Seg2 g2 = seg2(c.hb(c.w.dS2), c.hb(c.w.Q), true, c2.hb(c2.w.dS2), c2.hb(c2.w.Q), two);
+            if (item_ok(g3, H, H) && item_ok(g2, H, H)) {
+                add(g3, H, H, H, H, {red(0, H, H, gp(x.s3W), H, gp(x.s3b))}, 0, -1);
+                add(g2, H, H, d.NQ, H, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}, 0, -1);
                 sunv_grouped = true;
             }
-            for (int i = d.L - 1; i >= 1; --i)
-                if ((c.k.Kp[i] == W || i == d.skip) && i < 16)
-                    grouped[i] = add(dzl(c, i), dzl(c2, i), W, c.hb(c.w.Hb[i - 1]), c2.hb(c2.w.Hb[i - 1]), W, W,
-                                     gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]), 1 + (d.L - 1 - i), i);
         }
+        if (grp)
+            for (int i = d.L - 1; i >= 1; --i) {
+                const Seg2 g = seg2(dzl(c, i), c.hb(c.w.Hb[i - 1]), true, dzl(c2, i), c2.hb(c2.w.Hb[i - 1]), two);
+                if ((c.k.Kp[i] == W || i == d.skip) && i < 16 && item_ok(g, W, W)) {
+                    add(g, W, W, W, W, {red(0, W, W, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, 1 + (d.L - 1 - i), i);
+                    grouped[i] = true;
+                }
+            }
         for (size_t g0 = 0; g0 < items.size();) {
             const size_t g1 = std::min(items.size(), g0 + (size_t)std::min(g_tn_group, kTnGroup));
-            int64_t tiles = 0, nk = 0, nn = 0;
+            // one split count per point: GEMM q takes sp · P_q / Pt splits, rounds x the CUs' worth
+            // of blocks, within the workspace's slab capacity
+            double tiles = 0, nk = 0, nn = 0;
             for (size_t q = g0; q < g1; ++q) {
-                tiles += tn_tiles_bf16(items[q].t.N, items[q].t.K);
-                nk += (int64_t)items[q].t.N * items[q].t.K;
-                nn += items[q].t.N;
+                const double w = (double)items[q].t.P / (double)Pt;
+                tiles += w * tn_tiles_bf16(items[q].t.N, items[q].t.K);
+                nk += w * items[q].t.N * items[q].t.K;
+                nn += w * items[q].t.N;
             }
-            // one split count for the group (equal points per block): rounds x the CUs' worth of
-            // blocks, within the workspace's slab capacity
-            const int64_t sp1 = std::max<int64_t>(1, num_cus() / tiles);
+            const int64_t sp1 = std::max<int64_t>(1, (int64_t)(num_cus() / tiles));
             const int rounds = g_tn_group_rounds > 0 ? std::min(g_tn_group_rounds, kTnGroupRounds)
                                                      : (Pt / sp1 >= 65536 ? 2 : 1);
-            const int64_t sp = std::max<int64_t>(1, std::min({(int64_t)rounds * num_cus() / tiles, (int64_t)cdiv(Pt, g_tn16_min_points),
-                                                             c.w.slab_n / nk, c.w.slab_b_n / nn}));
-            SPN_ARG(sp * nk <= c.w.slab_n && sp * nn <= c.w.slab_b_n, "trunk_wgrad: slab capacity for a group of %d GEMMs",
-                    (int)(g1 - g0));
+            const int64_t sp = std::max<int64_t>(1, std::min({(int64_t)(rounds * num_cus() / tiles), (int64_t)cdiv(Pt, g_tn16_min_points),
+                                                             (int64_t)(c.w.slab_n / nk), (int64_t)(c.w.slab_b_n / nn)}));
             TN16Args t[kTnGroup];
             int spl[kTnGroup];
-            ReduceArgs r[kTnGroup];
+            std::vector<ReduceArgs> r;
             int64_t off = 0, off_b = 0;
-            bool skip_in = false, sunv_in = false;
+            bool skip_in = false, mark0 = false;
             for (size_t q = g0; q < g1; ++q) {
                 Item& it = items[q];
+                const int sq = (int)std::max<int64_t>(1, sp * it.t.P / Pt);
                 it.t.slab = c.at(c.w.slab) + off;
                 it.t.slab_b = c.at(c.w.slab_b) + off_b;
-                off += sp * it.t.slab_stride;
-                off_b += sp * it.t.N;
-                it.r.slab = it.t.slab; it.r.ld_slab = it.t.K; it.r.slab_stride = it.t.slab_stride; it.r.splits = (int)sp;
-                it.r.N = it.t.N; it.r.slab_b = it.t.slab_b; it.r.accumulate = c.acc;
+                off += sq * it.t.slab_stride;
+                off_b += (int64_t)sq * it.t.N;
+                for (int k = 0; k < it.nr; ++k) {
+                    ReduceArgs& rr = it.r[k];
+                    rr.slab = it.t.slab; rr.ld_slab = it.t.K; rr.slab_stride = it.t.slab_stride; rr.splits = sq;
+                    rr.N = it.t.N; rr.slab_b = it.t.slab_b; rr.accumulate = c.acc;
+                    r.push_back(rr);
+                }
                 t[q - g0] = it.t;
-                spl[q - g0] = (int)sp;
-                r[q - g0] = it.r;
+                spl[q - g0] = sq;
                 skip_in = skip_in || it.layer == d.skip;
-                sunv_in = sunv_in || it.layer < 0;
+                mark0 = mark0 || it.layer < 0;
             }
-            const int n = (int)(g1 - g0);
-            SPN_TRY(gemm_tn_bf16_group(t, n, spl, s));
-            for (int q = 0; q < n; q += kReduceMulti) SPN_TRY(reduce_slabs_multi(r + q, std::min(kReduceMulti, n - q), s));
+            SPN_ARG(off <= c.w.slab_n && off_b <= c.w.slab_b_n, "trunk_wgrad: slab capacity for a group of %d GEMMs",
+                    (int)(g1 - g0));
+            SPN_TRY(gemm_tn_bf16_group(t, (int)(g1 - g0), spl, s));
+            for (size_t q = 0; q < r.size(); q += kReduceMulti)
+                SPN_TRY(reduce_slabs_multi(r.data() + q, (int)std::min<size_t>(kReduceMulti, r.size() - q), s));
             if (skip_in) {  // the skip layer's PE columns: N = W, K = K0p (the narrow kernel)
                 const int l = d.skip;
                 const TnSeg st{dzl(c2, l), c2.hb(c2.w.X0b), nullptr, c2.w.P};
                 SPN_TRY(tn_grad<bf16>(c, dzl(c, l), W, W, c.hb(c.w.X0b), d.K0p, nullptr, 0, d.K0p, d.K0p, s,
                                       {red(0, W, d.K0, gp(x.fcW[l]) + W, ld(x.fcW[l]), nullptr)}, false, two ? &st : nullptr));
             }
-            if (sunv_in) SPN_TRY(grad_mark(0, s));
+            // mark 0 (the output heads) once the last group holding one of them is done
+            bool later0 = false;
+            for (size_t q = g1; q < items.size(); ++q) later0 = later0 || items[q].layer < 0;
+            if (mark0 && !later0 && (sunv_grouped || !SPN_DEFER_SUNV) && (heads_grouped || !hd))
+                SPN_TRY(grad_mark(0, s));
             for (size_t q = g0; q < g1; ++q)
                 if (items[q].layer >= 0) SPN_TRY(grad_mark(items[q].mark, s));
             g0 = g1;
+        }
+        // the heads' G / Q weight gradients not grouped: per segment, as the backward computes them
+        if (hd && !heads_grouped) {
+            for (int k = 0; k < (two ? 2 : 1); ++k) {
+                const Ctx& q = k ? c2 : c;
+                if (!(k ? hdb : hda)) continue;
+                const int mode = k ? mode_b : mode_a;
+                const bf16 *dZQ = q.hb(q.w.dZQ), *dZG = q.hb(q.w.dZG), *Gb = q.hb(q.w.G), *HL = q.hb(q.w.Hb[d.L - 1]);
+                if (mode == 0 && d.beta)
+                    SPN_TRY(tn_grad<bf16>(q, dZQ, d.NQ, d.NQ, Gb, d.NG, nullptr, 0, W, W, s,
+                                          {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b)),
+                                           red(2 * H, H, W, gp(x.b1W), ld(x.b1W), gp(x.b1b))}));
+                else if (mode == 0)
+                    SPN_TRY(tn_grad<bf16>(q, dZQ, d.NQ, d.NQ, Gb, d.NG, nullptr, 0, W, W, s,
+                                          {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b)), red(H, H, W, gp(x.r1W), ld(x.r1W), gp(x.r1b))}));
+                else
+                    SPN_TRY(tn_grad<bf16>(q, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
+                if (mode == 0 && d.sem)
+                    SPN_TRY(tn_grad<bf16>(q, dZG, d.NG, d.NG, HL, W, nullptr, 0, W, W, s,
+                                          {red(0, W, W, gp(x.featW), W, gp(x.featb)), red(W, H, W, gp(x.m1W), W, gp(x.m1b))}));
+                else
+                    SPN_TRY(tn_grad<bf16>(q, dZG, d.NG, W, HL, W, nullptr, 0, W, W, s, {red(0, W, W, gp(x.featW), W, gp(x.featb))}));
+            }
+            if (sunv_grouped || !SPN_DEFER_SUNV) SPN_TRY(grad_mark(0, s));
         }
         // sun_v_net.4 and .2 (sun-visibility head, in every pass): dW = dZᵀ · input over all points
         if (SPN_DEFER_SUNV && !sunv_grouped) {
@@ -2082,6 +2180,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_few_tiles") return &g_tn16_few_tiles;
     if (n == "tn_group") return &g_tn_group;
     if (n == "tn_group_rounds") return &g_tn_group_rounds;
+    if (n == "defer_heads") return &g_defer_heads;
     if (n == "tn_bf16_k64") return &g_tn16_k64;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;

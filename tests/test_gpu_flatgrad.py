@@ -82,30 +82,36 @@ def test_deferred_trunk_weight_gradients_match_per_pass(sem):
     assert float(grads[True]["fc_net.2.weight"].norm()) > 0
 
 
-def _deferred_grads(tn_group, n_rays=96, rounds=1):
+def _deferred_grads(tn_group, n_rays=96, rounds=1, beta=False, defer_heads=1):
     """Flat bf16 gradients of a main + solar render with the deferred trunk weight gradients, and
     the number of DMA weight-gradient launches they took."""
     import types
     from spnerf_amd import _lib
-    args = types.SimpleNamespace(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+    args = types.SimpleNamespace(n_samples=64, n_importance=0, model="sp-nerf", beta=beta, guidedsample=True,
                                  sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)
     rays = torch.tensor(gu_rays(n_rays, 4), device=DEV)
     g = torch.Generator().manual_seed(3)
     depths = torch.rand(n_rays, 2, generator=g).to(DEV) * 0.5 + 0.2
     valid = (torch.rand(n_rays, generator=g) > 0.3).long().to(DEV)
     sems = torch.randint(0, 3, (n_rays,), generator=g).to(DEV)
-    old = _lib.get_option("tn_group"), _lib.get_option("tn_group_rounds")
-    _lib.set_option("tn_group", tn_group)
-    _lib.set_option("tn_group_rounds", rounds)
+    ts = torch.randint(0, 4, (n_rays,), generator=g).to(DEV)
+    names = ("tn_group", "tn_group_rounds", "defer_heads")
+    old = [_lib.get_option(k) for k in names]
+    for k, v in zip(names, (tn_group, rounds, defer_heads)):
+        _lib.set_option(k, v)
     try:
         torch.manual_seed(0)
-        m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True,
-                              precision="bf16").to(DEV).use_flat_grads()
+        m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=512, mapping=True, sem=True, beta=beta,
+                              t_embedding_dims=4 if beta else 16, precision="bf16").to(DEV).use_flat_grads()
         m.defer_trunk_wgrad = True
+        models = {"coarse": m}
+        if beta:
+            torch.manual_seed(1)
+            models["t"] = torch.nn.Embedding(4, 4).to(DEV)
         with spnerf_amd.random_source(spnerf_amd.PhiloxRandom(seed=5)):
-            res = spnerf_amd.render_rays({"coarse": m}, args, rays, None, semantics=sems, mode="train",
+            res = spnerf_amd.render_rays(models, args, rays, ts if beta else None, semantics=sems, mode="train",
                                          valid_depth=valid, target_depths=depths, target_std=depths[:, 1] * 0 + 0.01)
-        loss = (res["rgb_coarse"] ** 2).mean() + res["sun_sc_coarse"].mean() + res["depth_coarse"].mean()
+        loss = sum((v.float() ** 2).mean() for k, v in sorted(res.items()) if v.requires_grad)
         torch.cuda.synchronize()
         _lib.prof_reset()
         _lib.prof_enable(True)
@@ -115,18 +121,22 @@ def _deferred_grads(tn_group, n_rays=96, rounds=1):
         launches = _lib.prof_read("gemm_tn_bf16d")["launches"] if "gemm_tn_bf16d" in _lib.prof_classes() else 0
         return {n: p.grad.detach().clone() for n, p in m.named_parameters()}, launches
     finally:
-        _lib.set_option("tn_group", old[0])
-        _lib.set_option("tn_group_rounds", old[1])
+        for k, v in zip(names, old):
+            _lib.set_option(k, v)
 
 
-@pytest.mark.parametrize("group,rounds", [(4, 1), (9, 1), (9, 2)])
-def test_grouped_trunk_weight_gradients_match(group, rounds):
-    """Option tn_group: the deferred sun_v and trunk-layer weight-gradient GEMMs (the skip layer's
-    H part; its PE tail on the narrow kernel) run `group` per launch of the DMA kernel, each with
-    1/group of the splits (`rounds` blocks per CU).  Fewer launches, the same gradients up to fp32
+@pytest.mark.parametrize("group,rounds,beta", [(4, 1, False), (9, 1, False), (9, 2, False), (10, 1, True), (6, 2, True)])
+def test_grouped_trunk_weight_gradients_match(group, rounds, beta):
+    """Option tn_group: the deferred output-head (G / Q, defer_heads), sun_v and trunk-layer
+    weight-gradient GEMMs (the skip layer's H part; its PE tail on the narrow kernel) run `group`
+    per launch of the DMA kernel, splits in proportion to their points (`rounds` blocks per CU).  Fewer launches, the same gradients up to fp32
     summation order."""
-    g1, n1 = _deferred_grads(1)
-    g2, n2 = _deferred_grads(group, rounds=rounds)
+    g0, _ = _deferred_grads(1, beta=beta, defer_heads=0)   # the heads' weight gradients per pass
+    g1, n1 = _deferred_grads(1, beta=beta)
+    g2, n2 = _deferred_grads(group, rounds=rounds, beta=beta)
+    for n, a in g0.items():   # deferred heads (per segment, ungrouped) = per pass up to summation order
+        if a.numel() >= 64 and float(a.norm()) > 0:
+            assert float((a - g1[n]).norm() / a.norm()) <= 1e-4, n
     assert n2 < n1, (n1, n2)
     num = den = 0.0
     for n, a in g1.items():
@@ -138,6 +148,6 @@ def test_grouped_trunk_weight_gradients_match(group, rounds):
             assert float((a - b).norm() / a.norm()) <= 1e-4, n
     assert (num / den) ** 0.5 <= 1e-5
     # deterministic: the same grouping twice is bit for bit the same
-    g3, _ = _deferred_grads(group, rounds=rounds)
+    g3, _ = _deferred_grads(group, rounds=rounds, beta=beta)
     for n in g2:
         assert torch.equal(g2[n], g3[n]), n
