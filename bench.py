@@ -820,8 +820,9 @@ class TrainStep:
         self.src = PhiloxRandom(seed=0, ray_offset=rank * B)
         set_random_source(self.src)
         # Batch indices live in static buffers so that the captured step reads each new batch.
-        self.idx_s = torch.empty(B, dtype=torch.int64, device=dev)
+        # (this rank's rows are a view of the global batch: one copy per step)
         self.gidx_s = torch.empty(B * world, dtype=torch.int64, device=dev)
+        self.idx_s = self.gidx_s[rank * B:(rank + 1) * B]
         # The gradient all-reduce (N > 1): by default in buckets (dp.GradBuckets), each issued on a
         # communication stream behind the backward mark after which its gradients are final, so the
         # collectives overlap the rest of the backward; --flat-allreduce = one all-reduce after it.
@@ -843,11 +844,8 @@ class TrainStep:
     def load_batch(self, gidx=None):
         """The next shared-seed global batch (or the given global indices) into the static buffers."""
         if gidx is None:
-            gidx, idx = self.sampler.next()
-        else:
-            idx = gidx[self.rank * self.B:(self.rank + 1) * self.B]
+            gidx, _ = self.sampler.next()
         self.gidx_s.copy_(gidx)
-        self.idx_s.copy_(idx)
 
     def fwd_bwd(self):
         """render + losses + backward for the batch in idx_s / gidx_s (grads are written, not

@@ -83,5 +83,8 @@ struct TN16Group {
 bool tn_group_ok(int P, int N, int K);  // the shape runs on the DMA kernel
 int tn_tiles_bf16(int N, int K);        // its 256 x 256 tiles
 int32_t gemm_tn_bf16_group(const TN16Args* a, int n, const int* splits, hipStream_t s);
+// the same for the narrow N = 512, K = 64 kernel (fc_net.0 and the skip layer's PE tail together)
+bool tn_k64_ok(int N, int K);
+int32_t gemm_tn_bf16_k64_group(const TN16Args* a, int n, const int* splits, hipStream_t s);
 
 }  // namespace spn

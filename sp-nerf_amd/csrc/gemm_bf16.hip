@@ -963,10 +963,14 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16(TN16Args g) {
 // kernel is HBM-bound (1.1 KB per point, 64 K MAC per point).  Steps past the split read
 // clamped rows that are stored as zeros (an even step count, so the loop has no branch).
 constexpr int T64_STEP = 32, T64_IMG = T64_STEP * 256, T64_STG = 5 * T64_IMG;
-__global__ __launch_bounds__(512) void k_gemm_tn_bf16_k64(TN16Args g) {
+// (a group launch: blocks [start[gi], start[gi + 1]) are the splits of GEMM gi)
+__global__ __launch_bounds__(512) void k_gemm_tn_bf16_k64(TN16Group G) {
     __shared__ __attribute__((aligned(16))) char smem[2 * T64_STG];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int split = blockIdx.x;
+    int gi = 0;
+    while (gi + 1 < G.n && (int)blockIdx.x >= G.start[gi + 1]) ++gi;
+    const TN16Args& g = G.g[gi];
+    const int split = blockIdx.x - G.start[gi];
     const int p_beg = split * g.p_per_split;
     const int p_end = min(g.P, p_beg + g.p_per_split);
     const int ach = tid & 63, arow = tid >> 6;         // A: features 8·ach.., rows arow + 8i
@@ -1618,6 +1622,34 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
     else hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, grid, block, 0, s, G);
 }
 
+bool tn_k64_ok(int N, int K) { return tn_k64(N, K); }
+
+int32_t gemm_tn_bf16_k64_group(const TN16Args* a0, int n, const int* splits, hipStream_t s) {
+    SPN_ARG(n >= 1 && n <= kTnGroup, "gemm_tn_bf16_k64_group: %d GEMMs (at most %d)", n, kTnGroup);
+    TN16Group G;
+    G.n = n;
+    G.start[0] = 0;
+    double flop = 0.0, bytes = 0.0;
+    for (int i = 0; i < n; ++i) {
+        TN16Args& q = G.g[i];
+        q = a0[i];
+        SPN_ARG(tn_k64(q.N, q.K) && q.K1 >= q.K && !q.b_sin && q.ld_slab == q.K && splits[i] >= 1 && q.A && q.B && q.slab,
+                "gemm_tn_bf16_k64_group: GEMM %d is not a narrow N = 512, K = 64 one", i);
+        SPN_ARG(q.P1 >= q.P || (q.A_s2 && q.B_s2), "gemm_tn_bf16_k64_group: second segment");
+        int pps = cdiv(q.P, splits[i]);
+        pps = (pps + 63) / 64 * 64;
+        q.p_per_split = pps < 64 ? 64 : pps;
+        G.start[i + 1] = G.start[i] + (q.P > 0 ? splits[i] : 0);
+        flop += 2.0 * q.P * q.N * q.K;
+        bytes += 2.0 * (double)q.P * (q.N + q.K) + 4.0 * splits[i] * ((double)q.N * q.K + (q.slab_b ? q.N : 0));
+    }
+    if (G.start[n] == 0) return SPNERF_OK;
+    ProfScope prof("gemm_tn_bf16k", s, flop, bytes);
+    hipLaunchKernelGGL(k_gemm_tn_bf16_k64, dim3(G.start[n]), dim3(512), 0, s, G);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
 bool tn_group_ok(int P, int N, int K) { return g_tn16_variant == 3 && !tn_k64(N, K) && tn_wide(N, K, -1) && P % TD_STEP == 0; }
 int tn_tiles_bf16(int N, int K) { return cdiv(N, TW) * cdiv(K, TW); }
 
@@ -1666,7 +1698,12 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
     if (tn_k64(a.N, a.K) && a.K1 >= a.K && !a.b_sin && a.ld_slab == a.K) {
         ProfScope prof("gemm_tn_bf16k", s, 2.0 * a.P * a.N * a.K,
                        2.0 * (double)a.P * (a.N + a.K) + 4.0 * splits * ((double)a.N * a.K + a.N));
-        hipLaunchKernelGGL(k_gemm_tn_bf16_k64, dim3(splits), dim3(512), 0, s, a);
+        TN16Group G;
+        G.g[0] = a;
+        G.n = 1;
+        G.start[0] = 0;
+        G.start[1] = splits;
+        hipLaunchKernelGGL(k_gemm_tn_bf16_k64, dim3(splits), dim3(512), 0, s, G);
         SPN_HIP(hipGetLastError());
         return SPNERF_OK;
     }

@@ -1119,6 +1119,7 @@ int g_tn_group_rounds = 0;
 // -> 3.926 / 3.917 ms, while at 4 096 rays the per-pass GEMMs overlapping the dX chain on the side
 // stream are worth more (26.04 / 26.14 against 26.16 / 26.19 ms deferred; same call)
 int g_defer_heads = 2;
+int g_tn_k64_pair = 1;  // option "tn_k64_pair": the skip layer's PE tail and fc_net.0 in one narrow launch
 static bool defer_heads_for(int64_t P) { return g_defer_heads == 1 || (g_defer_heads == 2 && P <= (1 << 18)); }
 
 #ifndef SPN_DEFER_SUNV
@@ -1953,6 +1954,11 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
                     grouped[i] = true;
                 }
             }
+        // the skip layer's PE tail and fc_net.0 (both N = W, K = K0p over the PE rows X0b) share one
+        // launch of the narrow kernel at the end, with half the splits each
+        const bool pair_tail = g_tn_k64_pair && tn_k64_ok(W, d.K0p) && d.skip >= 1 && d.skip < 16 && grouped[d.skip] &&
+                               c.k.Kp[0] == d.K0p;
+        bool tail_pending = false;
         for (size_t g0 = 0; g0 < items.size();) {
             const size_t g1 = std::min(items.size(), g0 + (size_t)std::min(g_tn_group, kTnGroup));
             // one split count per point: GEMM q takes sp · P_q / Pt splits, rounds x the CUs' worth
@@ -1997,7 +2003,9 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
             SPN_TRY(gemm_tn_bf16_group(t, (int)(g1 - g0), spl, s));
             for (size_t q = 0; q < r.size(); q += kReduceMulti)
                 SPN_TRY(reduce_slabs_multi(r.data() + q, (int)std::min<size_t>(kReduceMulti, r.size() - q), s));
-            if (skip_in) {  // the skip layer's PE columns: N = W, K = K0p (the narrow kernel)
+            if (skip_in && pair_tail) {
+                tail_pending = true;   // with fc_net.0's, one launch of the narrow kernel (below)
+            } else if (skip_in) {  // the skip layer's PE columns: N = W, K = K0p (the narrow kernel)
                 const int l = d.skip;
                 const TnSeg st{dzl(c2, l), c2.hb(c2.w.X0b), nullptr, c2.w.P};
                 SPN_TRY(tn_grad<bf16>(c, dzl(c, l), W, W, c.hb(c.w.X0b), d.K0p, nullptr, 0, d.K0p, d.K0p, s,
@@ -2009,7 +2017,7 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
             if (mark0 && !later0 && (sunv_grouped || !SPN_DEFER_SUNV) && (heads_grouped || !hd))
                 SPN_TRY(grad_mark(0, s));
             for (size_t q = g0; q < g1; ++q)
-                if (items[q].layer >= 0) SPN_TRY(grad_mark(items[q].mark, s));
+                if (items[q].layer >= 0 && !(tail_pending && items[q].layer == d.skip)) SPN_TRY(grad_mark(items[q].mark, s));
             g0 = g1;
         }
         // the heads' G / Q weight gradients not grouped: per segment, as the backward computes them
@@ -2048,6 +2056,37 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
         }
         for (int i = d.L - 1; i >= 0; --i) {
             if (i < 16 && grouped[i]) continue;
+            if (i == 0 && tail_pending) {
+                const int l = d.skip;
+                TN16Args t[2];
+                int spl[2];
+                ReduceArgs r[2];
+                const int sp = std::max(1, tn_splits_bf16((int)Pt, W, d.K0p) / 2);
+                for (int q = 0; q < 2; ++q) {
+                    TN16Args& a = t[q];
+                    const int li = q ? l : 0;
+                    a.A = dzl(c, li); a.lda = W; a.B = c.hb(c.w.X0b); a.ldb = d.K0p; a.K1 = d.K0p;
+                    a.P = (int)Pt; a.N = W; a.K = d.K0p;
+                    a.slab = c.at(c.w.slab) + (int64_t)q * sp * W * d.K0p; a.ld_slab = d.K0p; a.slab_stride = (int64_t)W * d.K0p;
+                    a.slab_b = q ? nullptr : c.at(c.w.slab_b);
+                    if (two) {
+                        a.P1 = c.w.P;
+                        a.A_s2 = dzl(c2, li) - c.w.P * W;
+                        a.B_s2 = c2.hb(c2.w.X0b) - c.w.P * d.K0p;
+                    }
+                    spl[q] = sp;
+                    r[q] = q ? red(0, W, d.K0, gp(x.fcW[l]) + W, ld(x.fcW[l]), nullptr)
+                             : red(0, W, d.K0, gp(x.fcW[0]), ld(x.fcW[0]), gp(x.fcb[0]));
+                    r[q].slab = a.slab; r[q].ld_slab = d.K0p; r[q].slab_stride = a.slab_stride; r[q].splits = sp; r[q].N = W;
+                    r[q].slab_b = a.slab_b; r[q].accumulate = c.acc;
+                }
+                SPN_ARG(2 * sp * (int64_t)W * d.K0p <= c.w.slab_n && sp * (int64_t)W <= c.w.slab_b_n, "trunk_wgrad: slab capacity");
+                SPN_TRY(gemm_tn_bf16_k64_group(t, 2, spl, s));
+                SPN_TRY(reduce_slabs_multi(r, 2, s));
+                SPN_TRY(grad_mark(1 + (d.L - 1 - l), s));
+                SPN_TRY(grad_mark(d.L, s));
+                continue;
+            }
             auto dz = [&](const Ctx& q) { return dzl(q, i); };
             auto in = [&](const Ctx& q) { return q.hb(i == 0 ? q.w.X0b : q.w.Hb[i - 1]); };
             const int ldin = i == 0 ? d.K0p : W;
@@ -2181,6 +2220,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_group") return &g_tn_group;
     if (n == "tn_group_rounds") return &g_tn_group_rounds;
     if (n == "defer_heads") return &g_defer_heads;
+    if (n == "tn_k64_pair") return &g_tn_k64_pair;
     if (n == "tn_bf16_k64") return &g_tn16_k64;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;
