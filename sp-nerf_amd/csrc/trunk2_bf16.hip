@@ -454,12 +454,23 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(
     }
 }
 
-int g_trunk2_tile = 128;  // option "trunk2_tile": 64 (two workgroups per CU) or 128
+// option "trunk2_tile": 64 (two workgroups per CU) or 128 points per tile (the default); 0 = 128, or
+// 64 when per-ray rows are staged per tile and a ray's samples (e.g. 64) do not fill 128 points —
+// which puts C4's guided pass 1 on the two-workgroup kernel: measured slower than the one-workgroup
+// k_trunk_bf16<128> it otherwise falls back to (0.161 vs 0.145 ms per 512-ray step, 1.17 vs 1.05 at
+// 4 096 rays; same call)
+int g_trunk2_tile = 128;
+
+static int trunk2_tm(const TrunkArgs& a) {
+    if (g_trunk2_tile == 64 || g_trunk2_tile == 128) return g_trunk2_tile;
+    const bool rows = ((a.X0 || a.rays) && a.rb0) || a.rb_skip;
+    return rows && a.S % 128 != 0 && a.S % 64 == 0 ? 64 : 128;
+}
 
 bool trunk2_supported(const TrunkArgs& a, bool save) {
     const bool on = g_trunk2 == 2 || (g_trunk2 == 1 && save) || (g_trunk2 == 3 && !save);
     if (!on || a.zround) return false;
-    const int TM = g_trunk2_tile == 64 ? 64 : 128;
+    const int TM = trunk2_tm(a);
     const bool l0 = a.X0 || a.rays;
     if (l0 && !(a.K0p % 4 == 0 && (a.K0p / 4) % TPD == 0)) return false;
     if (a.skip > 0 && a.K0p != 16 * TPD) return false;  // the skip layer's PE tail is one ring round
@@ -483,7 +494,7 @@ static void launch_trunk2(const TrunkArgs& ad, hipStream_t s, bool l0, bool save
 }
 
 int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, double bytes) {
-    const int TM = g_trunk2_tile == 64 ? 64 : 128;
+    const int TM = trunk2_tm(a);
     const int ntiles = cdiv(a.P, TM);
     TrunkArgs ad = a;
     ad.dbg = g_trunk_dbg;
@@ -502,7 +513,7 @@ int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, d
 int g_trunk_heads = 1;
 
 bool trunk2_heads_ok(const TrunkArgs& a) {
-    return g_trunk_heads && g_trunk2_tile != 64 && trunk2_supported(a, false);
+    return g_trunk_heads && trunk2_tm(a) == 128 && trunk2_supported(a, false);
 }
 
 int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const PackedOffs& k, hipStream_t s, double flop,
