@@ -58,12 +58,14 @@ extern int g_nt16_epi;  // option nt_bf16_epi
 extern int g_nt16_ip, g_tn16_ip, g_nt16_ip_gen;
 extern int g_tn16_bias_split;  // option tn_bf16_bias_split
 extern int g_tn16_k64;         // option tn_bf16_k64: the narrow kernel for N = 512, K = 64 weight gradients
+extern int g_tn16_pf;          // option tn_bf16_pf: prefetched LDS fragments in the DMA weight-gradient GEMM
 extern int g_tn16_few_tiles;   // option tn_bf16_few_tiles  // DMA kernels: issue placement of the next K-step (options nt_bf16_ip, tn_bf16_ip)
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);
 // variant: 1 = 128x128 tiles, 2 = 256x256 tiles where N, K are multiples of 256, 3 = the same
 // tiles fed by LDS-DMA (when P % 32 == 0 as well);
 // <= 0 = library default (g_tn16_variant)
 extern int g_tn16_variant;
+extern int g_tn16_rounds;      // option tn_bf16_rounds: wide weight-gradient blocks per CU (1 or 2)
 extern int g_tn16_min_points;  // fewest points per split (option "tn_bf16_min_points")
 // few: the tn_bf16_few_tiles choice (-1: the option; the workspace layout takes the larger, 1)
 int tn_splits_bf16(int P, int N, int K, int variant = -1, int few = -1);

@@ -1259,7 +1259,11 @@ constexpr int TD_STEP = 32, TD_STAGES = 4, TD_STG = 4 * TD_STEP * 256;  // bytes
 // A group launch (gemm_tn_bf16_group) runs G.n GEMMs in one grid, blocks [start[gi],
 // start[gi + 1]) on GEMM gi — consecutive after the XCD remap, so a split keeps its tiles
 // (which share operand rows) on one XCD as in a single launch.
-template <int IP>
+// PF (option tn_bf16_pf): the next k-step's fragments are read from LDS while the current
+// k-step's MFMAs run (two register sets), and a step's barrier sits between its two k-halves —
+// the same MFMAs in the same order (bit-identical); without it every k-step waits out its own
+// LDS reads (on-chip ceiling of the kernel with one-row operands: 0.44 of the MFMA peak).
+template <int IP, bool PF = false>
 __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     __shared__ __attribute__((aligned(16))) char smem[TD_STAGES * TD_STG];  // [stage][A0|A1|B0|B1]
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -1288,8 +1292,10 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     // this lane's 4 DMA sources (instructions q = wid + 8 i: i < 2 → A, else B), advanced by
     // TD_STEP rows per step
     // second point segment (g.P1 a multiple of TD_STEP, host-checked): a step lies in one segment
+    // src: this lane's source in the first segment (VGPRs); dl: the wave-uniform byte offset to the
+    // second segment's (readfirstlane: a B column range never straddles K1, host-checked K1 % 128)
     const bf16* src[4];
-    const bf16* src2[4];
+    int64_t dl[4];
     int ld[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1299,24 +1305,25 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
         const int f = (X ? k0 : n0) + hf * 128 + 8 * chl;
         if (X == 0) {
             src[i] = g.A + (int64_t)row * g.lda + min(f, g.N - 8);
-            src2[i] = g.A_s2 + (int64_t)row * g.lda + min(f, g.N - 8);
+            dl[i] = (int64_t)((intptr_t)g.A_s2 - (intptr_t)g.A);
             ld[i] = g.lda;
         } else {
             const int kc = min(f, g.K - 8);
-            const bool s2 = kc >= g.K1;
+            const bool s2 = __builtin_amdgcn_readfirstlane(kc >= g.K1 ? 1 : 0) != 0;
             ld[i] = s2 ? g.ldb2 : g.ldb;
             src[i] = (s2 ? g.B2 + (kc - g.K1) : g.B + kc) + (int64_t)row * ld[i];
-            src2[i] = (s2 ? g.B2_s2 + (kc - g.K1) : g.B_s2 + kc) + (int64_t)row * ld[i];
+            dl[i] = s2 ? (int64_t)((intptr_t)g.B2_s2 - (intptr_t)g.B2) : (int64_t)((intptr_t)g.B_s2 - (intptr_t)g.B);
         }
     }
+    const int64_t P1 = g.P1;  // (a local: no scalar loads from the argument inside the loops)
     auto issue = [&](int st, int stg) {
         const int64_t p0 = p_beg + (int64_t)TD_STEP * st;
-        const bool sg2 = p0 >= g.P1;
+        const bool sg2 = p0 >= P1;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int q = wid + 8 * i;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)((sg2 ? src2[i] : src[i]) + p0 * ld[i]),
-                                             (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
+            const char* a = reinterpret_cast<const char*>(src[i] + p0 * ld[i]) + (sg2 ? dl[i] : 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)a, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
         }
     };
 
@@ -1405,7 +1412,83 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
         }
     };
 
-    if (ns > 0) {  // block-uniform
+    // PF: fragments of one k-step (16 points) of stage stg into a register set; MFMAs from one
+    struct Frag {
+        s16x4 al[4], ah[4], bl[2], bh[2];
+    };
+    auto fread = [&](Frag& f, int stg, int ks) {
+        const char* sA = smem + stg * TD_STG + wa * HALF;
+        const char* sB = smem + stg * TD_STG + (2 + (wb >> 1)) * HALF;
+        const int cb = (wb & 1) * 64;
+        const int r0 = 16 * ks + 8 * h;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            f.bl[j] = trd(sB, r0, cb + 32 * j + 16 * grp);
+            f.bh[j] = trd(sB, r0 + 4, cb + 32 * j + 16 * grp);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f.al[i] = trd(sA, r0, 32 * i + 16 * grp);
+            f.ah[i] = trd(sA, r0 + 4, 32 * i + 16 * grp);
+        }
+    };
+    // wait until at most `later` LDS reads (the other set's, issued after f's) are outstanding
+    auto fwait12 = [](Frag& f) {
+        asm volatile("s_waitcnt lgkmcnt(12)"
+                     : "+v"(f.al[0]), "+v"(f.al[1]), "+v"(f.al[2]), "+v"(f.al[3]), "+v"(f.ah[0]), "+v"(f.ah[1]),
+                       "+v"(f.ah[2]), "+v"(f.ah[3]), "+v"(f.bl[0]), "+v"(f.bl[1]), "+v"(f.bh[0]), "+v"(f.bh[1])
+                     :
+                     : "memory");
+    };
+    auto fwait0 = [](Frag& f) {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(f.al[0]), "+v"(f.al[1]), "+v"(f.al[2]), "+v"(f.al[3]), "+v"(f.ah[0]), "+v"(f.ah[1]),
+                       "+v"(f.ah[2]), "+v"(f.ah[3]), "+v"(f.bl[0]), "+v"(f.bl[1]), "+v"(f.bh[0]), "+v"(f.bh[1])
+                     :
+                     : "memory");
+    };
+    auto fmma = [&](const Frag& f) {
+        bf16x8 a[4], b[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = join(f.bl[j], f.bh[j]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = join(f.al[i], f.ah[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    };
+
+    if (PF && ns > 0) {  // block-uniform
+        issue(0, 0);
+        issue(min(1, ns - 1), 1);
+        issue(min(2, ns - 1), 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // step 0 landed (own DMAs)
+        __builtin_amdgcn_s_barrier();
+        Frag f0, f1;
+        fread(f0, 0, 0);
+        for (int st = 0; st < ns; ++st) {
+            const int stg = st % TD_STAGES;
+            fread(f1, stg, 1);
+            fwait12(f0);
+            fmma(f0);
+            // (the bias rows' plain LDS reads: the compiler's own waits for them are conservative
+            // under in-order LDS counting, and the fragment waits count them as later reads)
+            if (do_bias) bias_rows(stg);
+            // step st+1 landed (own DMAs: st+1, st+2 outstanding, st+3 not yet issued); the barrier
+            // publishes it and retires every wave's reads of stage (st+3) % 4 = (st-1) % 4
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES);
+            if (st + 1 < ns) fread(f0, (st + 1) % TD_STAGES, 0);
+            if (st + 1 < ns) fwait12(f1);
+            else fwait0(f1);
+            fmma(f1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
+        __builtin_amdgcn_s_barrier();
+    } else if (ns > 0) {  // block-uniform
         issue(0, 0);
         issue(min(1, ns - 1), 1);  // past the end: re-reads of the last step, never consumed
         issue(min(2, ns - 1), 2);
@@ -1591,6 +1674,7 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
 }
 
 int g_tn16_min_points = 1024;  // fewest points per split of a bf16 weight-gradient GEMM
+int g_tn16_rounds = 1;         // option tn_bf16_rounds (tn_splits_bf16): 2 measured level in the bench (C4 6.24 vs 6.19 ms TN)
 
 int tn_splits_bf16(int P, int N, int K, int variant, int few) {
     // the narrow kernel: one block per CU, at least half the usual points per split
@@ -1600,13 +1684,23 @@ int tn_splits_bf16(int P, int N, int K, int variant, int few) {
     const int tiles = wide ? cdiv(N, TW) * cdiv(K, TW) : cdiv(N, HB) * cdiv(K, HB);
     // one wide block per CU, two 128x128 ones: as many splits as fill the CUs (256 on MI355X)
     // WITHOUT a second round (N = 768, K = 512 rounded up to 258 wide blocks: 221 us, two rounds)
-    int splits = (wide ? cus : 2 * cus) / tiles;
-    if (splits > (wide && tiles < 4 ? cus : 64)) splits = wide && tiles < 4 ? cus : 64;
+    // (option tn_bf16_rounds: wide blocks per CU — 2 lets the blocks' ring fills and slab writes
+    // fall at different times; 1 M x 512 x 512 in isolation: 750 -> 646 us)
+    const int rounds = wide && tiles >= 4 && g_tn16_rounds > 1 ? 2 : 1;
+    int splits = (wide ? rounds * cus : 2 * cus) / tiles;
+    if (splits > (wide && tiles < 4 ? cus : 64 * rounds)) splits = wide && tiles < 4 ? cus : 64 * rounds;
     // (few wide tiles: half the points per split, so small batches still spread over the chip)
     const int max_splits = cdiv(P, wide && tiles < 4 ? g_tn16_min_points / 2 : g_tn16_min_points);
     if (splits > max_splits) splits = max_splits;
     return splits < 1 ? 1 : splits;
 }
+
+// option tn_bf16_pf: the prefetched-fragment main loop of k_gemm_tn_bf16d (1; 2 = only for launches
+// of at most one block per CU). Bit-identical; in isolation (tools/tn_lab, 1 M x 512 x 512, 64
+// splits) 762 -> 672 us, but in the bench slower: C4 TN class 6.17 / 6.21 -> 6.47 / 6.46 ms (1) and
+// 6.20 / 6.17 -> 6.25 / 6.24 (2), C4@512 3.744 -> 3.766 (2) / 3.799 (1) — the grouped launch already
+// runs two blocks per CU (as 128 splits does in isolation: 669 us) and the two do not stack. Off.
+int g_tn16_pf = 0;
 
 static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip, hipStream_t s) {
     TN16Group G;
@@ -1617,6 +1711,10 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
         G.start[i + 1] = G.start[i] + blocks[i];
     }
     const dim3 grid(G.start[n]), block(512);
+    if (g_tn16_pf == 1 || (g_tn16_pf == 2 && G.start[n] <= num_cus())) {
+        hipLaunchKernelGGL((k_gemm_tn_bf16d<1, true>), grid, block, 0, s, G);
+        return;
+    }
     if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, grid, block, 0, s, G);
     else if (ip == 1) hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, grid, block, 0, s, G);
     else hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, grid, block, 0, s, G);
@@ -1708,7 +1806,8 @@ int32_t gemm_tn_bf16(const TN16Args& a0, int splits, hipStream_t s) {
         return SPNERF_OK;
     }
     // DMA: whole 32-point steps (and a segment boundary on a step)
-    const bool dma = wide && g_tn16_variant == 3 && a.P % TD_STEP == 0 && !a.b_sin && (!two || a.P1 % TD_STEP == 0);
+    const bool dma = wide && g_tn16_variant == 3 && a.P % TD_STEP == 0 && !a.b_sin && (!two || a.P1 % TD_STEP == 0) &&
+                     (a.K1 >= a.K || a.K1 % 128 == 0);
     ProfScope prof(dma ? "gemm_tn_bf16d" : wide ? "gemm_tn_bf16w" : "gemm_tn_bf16", s, 2.0 * a.P * a.N * a.K,
                    2.0 * (double)a.P * (a.N + a.K) + 4.0 * splits * (double)a.N * a.K);
     if (wide) {

@@ -237,3 +237,32 @@ def test_bf16_fused_backward_register_dz_bitwise_equal(n, ns):
         assert torch.isfinite(g1[k]).all(), k
         assert torch.equal(g0[k], g1[k]), k
 
+
+
+@pytest.mark.parametrize("n,ns", [(300, 64), (2048, 64)])
+def test_bf16_tn_prefetched_fragments_bitwise_equal(n, ns):
+    """Option tn_bf16_pf: the DMA weight-gradient GEMM reading the next k-step's LDS fragments
+    during the current k-step's MFMAs (same MFMAs, same order) gives the same gradients bit for bit
+    — per-pass launches here, the deferred group launches below."""
+    r0, g0 = _render_bf16({"tn_bf16_pf": 0}, n=n, ns=ns)
+    r1, g1 = _render_bf16({"tn_bf16_pf": 1}, n=n, ns=ns)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    assert sorted(g0) == sorted(g1)
+    for k in g0:
+        assert torch.isfinite(g0[k]).all(), k
+        assert torch.equal(g0[k], g1[k]), k
+
+
+def test_bf16_tn_prefetched_fragments_grouped_bitwise_equal():
+    from test_gpu_flatgrad import _deferred_grads
+    old = _lib.get_option("tn_bf16_pf")
+    out = []
+    try:
+        for pf in (0, 1):
+            _lib.set_option("tn_bf16_pf", pf)
+            out.append(_deferred_grads(9, n_rays=256)[0])
+    finally:
+        _lib.set_option("tn_bf16_pf", old)
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k

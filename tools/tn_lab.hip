@@ -128,8 +128,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dBi, bi.data(), bi.size() * 2, hipMemcpyHostToDevice));
     const int splits = tn_splits_bf16(P, N, K);
     float *slab, *slab_b, *ref, *got;
-    CK(hipMalloc(&slab, (size_t)splits * N * K * 4));
-    CK(hipMalloc(&slab_b, (size_t)splits * N * 4));
+    CK(hipMalloc(&slab, (size_t)2 * splits * N * K * 4));   // (room for the 2x-splits run)
+    CK(hipMalloc(&slab_b, (size_t)2 * splits * N * 4));
     CK(hipMalloc(&ref, (size_t)N * K * 4));
     CK(hipMalloc(&got, (size_t)N * K * 4));
     hipEvent_t e0, e1;
@@ -156,6 +156,37 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, ref);
     printf("P=%d splits=%d  library DMA TN: %8.1f us  %7.1f TF/s  %6.2f TB/s (operands)\n", P, splits, ul, flop / ul * 1e-6,
            bytes / ul * 1e-6);
+    {   // option tn_bf16_pf: prefetched LDS fragments, bit-identical
+        g_tn16_pf = 1;
+        const double up = timeit([&] { gemm_tn_bf16(t, splits, 0); });
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, got);
+        std::vector<float> hr((size_t)N * K), hg(hr.size());
+        CK(hipMemcpy(hr.data(), ref, hr.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hg.data(), got, hg.size() * 4, hipMemcpyDeviceToHost));
+        printf("library DMA TN, prefetched fragments: %8.1f us  %7.1f TF/s  %6.2f TB/s  bitwise %s\n", up, flop / up * 1e-6,
+               bytes / up * 1e-6, memcmp(hr.data(), hg.data(), hr.size() * 4) == 0 ? "equal" : "DIFFERENT");
+        TN16Args t0 = t;
+        t0.lda = 0;
+        t0.ldb = 0;
+        const double u0 = timeit([&] { gemm_tn_bf16(t0, splits, 0); });
+        printf("  ... one row (on-chip): %8.1f us  %7.1f TF/s\n", u0, flop / u0 * 1e-6);
+        const double u2 = timeit([&] { gemm_tn_bf16(t, 2 * splits, 0); });
+        printf("  ... %3d splits: %8.1f us  %7.1f TF/s\n", 2 * splits, u2, flop / u2 * 1e-6);
+        g_tn16_pf = 0;
+    }
+    {   // the same kernel with every point row the same row (lda = ldb = 0): operands from L2 / L1,
+        // the on-chip ceiling of the DMA pipeline
+        TN16Args t0 = t;
+        t0.lda = 0;
+        t0.ldb = 0;
+        const double u0 = timeit([&] { gemm_tn_bf16(t0, splits, 0); });
+        printf("library DMA TN, one row (on-chip): %8.1f us  %7.1f TF/s\n", u0, flop / u0 * 1e-6);
+        for (int sp : {splits / 2, splits * 2}) {
+            const double u1 = timeit([&] { gemm_tn_bf16(t, sp, 0); });
+            printf("library DMA TN, %3d splits: %8.1f us  %7.1f TF/s  %6.2f TB/s\n", sp, u1, flop / u1 * 1e-6, bytes / u1 * 1e-6);
+        }
+    }
     const int pps = (P + splits - 1) / splits;
     auto run = [&](auto kern, const char* name, int resident = 0) {
         const double us = timeit([&] { hipLaunchKernelGGL(kern, dim3(4 * splits), dim3(512), 0, 0, dAi, dBi, P, N, K, pps, slab, resident); });
