@@ -58,6 +58,7 @@ extern int g_nt16_epi;  // option nt_bf16_epi
 extern int g_nt16_ip, g_tn16_ip, g_nt16_ip_gen;
 extern int g_tn16_bias_split;  // option tn_bf16_bias_split
 extern int g_tn16_k64;         // option tn_bf16_k64: the narrow kernel for N = 512, K = 64 weight gradients
+extern int g_tn16_quad;        // option tn_bf16_quad: the quad-wave 128x128-per-wave DMA weight-gradient kernel
 extern int g_tn16_pf;          // option tn_bf16_pf: prefetched LDS fragments in the DMA weight-gradient GEMM
 extern int g_tn16_few_tiles;   // option tn_bf16_few_tiles  // DMA kernels: issue placement of the next K-step (options nt_bf16_ip, tn_bf16_ip)
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);

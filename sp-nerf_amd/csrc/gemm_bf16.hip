@@ -1554,6 +1554,239 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     }
 }
 
+// Quad-wave DMA weight-gradient GEMM (option tn_bf16_quad): the 256x256 tile and LDS-DMA ring
+// of k_gemm_tn_bf16d, but 4 waves (one per SIMD) of 128x128 each (4 x 4 32x32 accumulators, 256
+// registers): 16 MFMAs per 16 fragment reads instead of 8 per 12, and the next k-step's fragments
+// read while the current k-step's MFMAs run (two register sets) — a single wave per SIMD has no
+// partner to hide its LDS latency. Same per-element k-order as k_gemm_tn_bf16d (bit-identical).
+__global__ __launch_bounds__(256) void k_gemm_tn_bf16q(TN16Group G) {
+    __shared__ __attribute__((aligned(16))) char smem[TD_STAGES * TD_STG];  // [stage][A0|A1|B0|B1]
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    int gi = 0;
+    while (gi + 1 < G.n && wg >= G.start[gi + 1]) ++gi;
+    const int w = wg - G.start[gi];
+    const TN16Args& g = G.g[gi];
+    const int nK = (g.K + TW - 1) / TW;
+    const int ntiles = cdiv(g.N, TW) * nK;
+    const int split = w / ntiles, t = w % ntiles;
+    const int n0 = (t / nK) * TW, k0 = (t % nK) * TW;
+    const int p_beg = split * g.p_per_split;
+    const int p_end = min(g.P, p_beg + g.p_per_split);
+    const bool bsplit = g.bias_split && nK == 2;
+    const int kt = t % nK;
+    const bool do_bias = g.slab_b != nullptr && (bsplit || k0 == 0);
+    const int ns = p_end > p_beg ? (p_end - p_beg) / TD_STEP : 0;
+
+    // this lane's 8 DMA sources (wave-instructions q = wid + 4 i of the stage's 32)
+    const bf16* src[8];
+    int64_t dl[8];
+    int ld[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int q = wid + 4 * i, X = q >> 4, hf = (q >> 3) & 1, rg = q & 7;
+        const int row = rg * 4 + (lane >> 4);
+        const int chl = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const int f = (X ? k0 : n0) + hf * 128 + 8 * chl;
+        if (X == 0) {
+            src[i] = g.A + (int64_t)row * g.lda + min(f, g.N - 8);
+            dl[i] = (int64_t)((intptr_t)g.A_s2 - (intptr_t)g.A);
+            ld[i] = g.lda;
+        } else {
+            const int kc = min(f, g.K - 8);
+            const bool s2 = __builtin_amdgcn_readfirstlane(kc >= g.K1 ? 1 : 0) != 0;
+            ld[i] = s2 ? g.ldb2 : g.ldb;
+            src[i] = (s2 ? g.B2 + (kc - g.K1) : g.B + kc) + (int64_t)row * ld[i];
+            dl[i] = s2 ? (int64_t)((intptr_t)g.B2_s2 - (intptr_t)g.B2) : (int64_t)((intptr_t)g.B_s2 - (intptr_t)g.B);
+        }
+    }
+    const int64_t P1 = g.P1;
+    auto issue = [&](int st, int stg) {
+        const int64_t p0 = p_beg + (int64_t)TD_STEP * st;
+        const bool sg2 = p0 >= P1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int q = wid + 4 * i;
+            const char* a = reinterpret_cast<const char*>(src[i] + p0 * ld[i]) + (sg2 ? dl[i] : 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)a, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int wa = wid >> 1, wb = wid & 1, h = lane >> 5, grp = (lane >> 4) & 1;
+    const int q4 = (lane & 15) >> 2, pp = lane & 3;
+    auto trd = [&](const char* base, int r0, int col) -> s16x4 {
+        const int o = tn_off(r0 + q4, (col >> 3) + (pp >> 1)) + 8 * (pp & 1);
+        const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(base + o);
+        s16x4 v;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+        return v;
+    };
+    auto join = [](s16x4 lo, s16x4 hi) -> bf16x8 {
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    constexpr int HALF = TD_STEP * 256;
+    struct Frag {
+        s16x4 al[4], ah[4], bl[4], bh[4];
+    };
+    auto fread = [&](Frag& f, int stg, int ks) {
+        const char* sA = smem + stg * TD_STG + wa * HALF;
+        const char* sB = smem + stg * TD_STG + (2 + wb) * HALF;
+        const int r0 = 16 * ks + 8 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f.bl[j] = trd(sB, r0, 32 * j + 16 * grp);
+            f.bh[j] = trd(sB, r0 + 4, 32 * j + 16 * grp);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f.al[i] = trd(sA, r0, 32 * i + 16 * grp);
+            f.ah[i] = trd(sA, r0 + 4, 32 * i + 16 * grp);
+        }
+    };
+    // at most 15 LDS operations (the other set's reads, issued after f's) left in flight
+    auto fwait = [](Frag& f, auto cnt) {
+        if constexpr (decltype(cnt)::value == 15)
+            asm volatile("s_waitcnt lgkmcnt(15)"
+                         : "+v"(f.al[0]), "+v"(f.al[1]), "+v"(f.al[2]), "+v"(f.al[3]), "+v"(f.ah[0]), "+v"(f.ah[1]),
+                           "+v"(f.ah[2]), "+v"(f.ah[3]), "+v"(f.bl[0]), "+v"(f.bl[1]), "+v"(f.bl[2]), "+v"(f.bl[3]),
+                           "+v"(f.bh[0]), "+v"(f.bh[1]), "+v"(f.bh[2]), "+v"(f.bh[3])
+                         :
+                         : "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(f.al[0]), "+v"(f.al[1]), "+v"(f.al[2]), "+v"(f.al[3]), "+v"(f.ah[0]), "+v"(f.ah[1]),
+                           "+v"(f.ah[2]), "+v"(f.ah[3]), "+v"(f.bl[0]), "+v"(f.bl[1]), "+v"(f.bl[2]), "+v"(f.bl[3]),
+                           "+v"(f.bh[0]), "+v"(f.bh[1]), "+v"(f.bh[2]), "+v"(f.bh[3])
+                         :
+                         : "memory");
+    };
+    auto fmma = [&](const Frag& f) {
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = join(f.bl[j], f.bh[j]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = join(f.al[i], f.ah[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    };
+    // bias: the per-phase sums of k_gemm_tn_bf16d in the same order (bit-identical), two phases per
+    // thread: bsplit: chunk ch of the tile's 16, phases lrow and lrow + 16 (row = phase);
+    // else chunk ch of 32, phases lrow and lrow + 8 (rows phase and phase + 16)
+    const int ch = bsplit ? 16 * kt + (tid & 15) : tid & 31, lrow = bsplit ? tid >> 4 : tid >> 5;
+    float bs[2][8] = {{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}};
+    auto bias_rows = [&](int stg) {
+        const char* sA = smem + stg * TD_STG + (ch >> 4) * HALF;
+        if (bsplit) {  // block-uniform
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                float f[8];
+                unpack8(*reinterpret_cast<const u32x4*>(sA + tn_off(lrow + 16 * i, ch & 15)), f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bs[i][e] += f[e];
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                float f[8];
+                unpack8(*reinterpret_cast<const u32x4*>(sA + tn_off(lrow + 8 * i + 16 * r, ch & 15)), f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bs[i][e] += f[e];
+            }
+    };
+    using I0 = std::integral_constant<int, 0>;
+
+    if (ns > 0) {  // block-uniform
+        issue(0, 0);
+        issue(min(1, ns - 1), 1);  // past the end: re-reads of the last step, never consumed
+        issue(min(2, ns - 1), 2);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 landed (own DMAs)
+        __builtin_amdgcn_s_barrier();
+        Frag f0, f1;
+        fread(f0, 0, 0);
+        // each set is waited for (lgkmcnt(0): issued a whole MFMA burst earlier) just before the
+        // other set's reads are issued, so they run under this set's MFMAs
+        for (int st = 0; st < ns; ++st) {
+            const int stg = st % TD_STAGES;
+            fwait(f0, I0{});
+            fread(f1, stg, 1);
+            fmma(f0);
+            if (do_bias) bias_rows(stg);
+            // step st+1 landed (own DMAs of st+1, st+2 outstanding); the barrier publishes it and
+            // retires every wave's reads of stage (st+3) % 4 = (st-1) % 4 before it is refilled
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES);
+            fwait(f1, I0{});
+            if (st + 1 < ns) fread(f0, (st + 1) % TD_STAGES, 0);
+            fmma(f1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
+        __builtin_amdgcn_s_barrier();
+    }
+
+    float* slab = g.slab + (int64_t)split * g.slab_stride;
+    const int r32 = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = k0 + wb * 128 + j * 32 + r32;
+        if (k >= g.K) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n0 + wa * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (n < g.N) slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
+            }
+    }
+    if (do_bias && bsplit) {
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);  // [32 phases][128 features]
+        const int cl = ch & 15;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red[(lrow + 16 * i) * 128 + 8 * cl + e] = bs[i][e];
+        __syncthreads();
+        const int n = n0 + 128 * kt + tid;
+        if (tid < 128 && n < g.N) {
+            float s = 0.f;
+            for (int ph = 0; ph < 32; ++ph) s += red[ph * 128 + tid];
+            g.slab_b[(int64_t)split * g.N + n] = s;
+        }
+    } else if (do_bias) {
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(smem);  // [16 phases][256 features]
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red[(lrow + 8 * i) * 256 + 8 * ch + e] = bs[i][e];
+        __syncthreads();
+        if (n0 + tid < g.N) {
+            float s = 0.f;
+            for (int ph = 0; ph < 16; ++ph) s += red[ph * 256 + tid];
+            g.slab_b[(int64_t)split * g.N + n0 + tid] = s;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
@@ -1701,6 +1934,11 @@ int tn_splits_bf16(int P, int N, int K, int variant, int few) {
 // 6.20 / 6.17 -> 6.25 / 6.24 (2), C4@512 3.744 -> 3.766 (2) / 3.799 (1) — the grouped launch already
 // runs two blocks per CU (as 128 splits does in isolation: 669 us) and the two do not stack. Off.
 int g_tn16_pf = 0;
+// option tn_bf16_quad: k_gemm_tn_bf16q (4 waves of 128x128) for the DMA weight gradients —
+// bit-identical, but slower: 1 M x 512 x 512 in isolation 778 vs 792 us, with one-row (on-chip)
+// operands 710 vs 498 us (MFMA busy 34% against 50%: one wave per SIMD leaves its waits and
+// issue stalls uncovered; tools/pmc_tn_lab.sh); C4 TN 6.30 -> 7.9 ms per step, C4@512 3.956 -> 4.22
+int g_tn16_quad = 0;
 
 static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip, hipStream_t s) {
     TN16Group G;
@@ -1711,6 +1949,10 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
         G.start[i + 1] = G.start[i] + blocks[i];
     }
     const dim3 grid(G.start[n]), block(512);
+    if (g_tn16_quad) {
+        hipLaunchKernelGGL(k_gemm_tn_bf16q, grid, dim3(256), 0, s, G);
+        return;
+    }
     if (g_tn16_pf == 1 || (g_tn16_pf == 2 && G.start[n] <= num_cus())) {
         hipLaunchKernelGGL((k_gemm_tn_bf16d<1, true>), grid, block, 0, s, G);
         return;

@@ -2219,6 +2219,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_few_tiles") return &g_tn16_few_tiles;
     if (n == "tn_group") return &g_tn_group;
     if (n == "tn_bf16_pf") return &g_tn16_pf;
+    if (n == "tn_bf16_quad") return &g_tn16_quad;
     if (n == "tn_bf16_rounds") return &g_tn16_rounds;
     if (n == "tn_group_rounds") return &g_tn_group_rounds;
     if (n == "defer_heads") return &g_defer_heads;

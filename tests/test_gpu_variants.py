@@ -266,3 +266,30 @@ def test_bf16_tn_prefetched_fragments_grouped_bitwise_equal():
         _lib.set_option("tn_bf16_pf", old)
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
+
+
+@pytest.mark.parametrize("n,ns", [(300, 64), (2048, 64)])
+def test_bf16_tn_quad_wave_bitwise_equal(n, ns):
+    """Option tn_bf16_quad: the 4-wave (128x128 per wave) DMA weight-gradient kernel keeps every
+    output's k-order and the bias sums' phase order: gradients bit for bit equal."""
+    r0, g0 = _render_bf16({"tn_bf16_quad": 0}, n=n, ns=ns)
+    r1, g1 = _render_bf16({"tn_bf16_quad": 1}, n=n, ns=ns)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    for k in g0:
+        assert torch.isfinite(g0[k]).all(), k
+        assert torch.equal(g0[k], g1[k]), k
+
+
+def test_bf16_tn_quad_wave_grouped_bitwise_equal():
+    from test_gpu_flatgrad import _deferred_grads
+    old = _lib.get_option("tn_bf16_quad")
+    out = []
+    try:
+        for q in (0, 1):
+            _lib.set_option("tn_bf16_quad", q)
+            out.append(_deferred_grads(9, n_rays=256)[0])
+    finally:
+        _lib.set_option("tn_bf16_quad", old)
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k

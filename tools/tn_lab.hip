@@ -146,6 +146,20 @@ int main(int argc, char** argv) {
         return 1e3 * ms / iters;
     };
     const double flop = 2.0 * P * N * K, bytes = 2.0 * P * (N + K);
+    // profiling mode (argv[3]): one configuration only, for PMC passes — 1 DMA one-row, 2 quad
+    // one-row, 3 DMA, 4 quad, 5 prefetched one-row
+    const int mode = argc > 3 ? atoi(argv[3]) : 0;
+    if (mode) {
+        TN16Args t;
+        t.A = dA; t.lda = (mode == 1 || mode == 2 || mode == 5) ? 0 : N; t.B = dB; t.ldb = t.lda ? K : 0; t.K1 = K;
+        t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K; t.slab_b = slab_b;
+        t.P = P; t.N = N; t.K = K;
+        g_tn16_quad = mode == 2 || mode == 4;
+        g_tn16_pf = mode == 5;
+        const double u = timeit([&] { gemm_tn_bf16(t, splits, 0); });
+        printf("mode %d: %8.1f us  %7.1f TF/s\n", mode, u, flop / u * 1e-6);
+        return 0;
+    }
     // library kernel (row layout), its slab reduction on the side
     TN16Args t;
     t.A = dA; t.lda = N; t.B = dB; t.ldb = K; t.K1 = K;
@@ -156,15 +170,17 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, ref);
     printf("P=%d splits=%d  library DMA TN: %8.1f us  %7.1f TF/s  %6.2f TB/s (operands)\n", P, splits, ul, flop / ul * 1e-6,
            bytes / ul * 1e-6);
-    {   // option tn_bf16_pf: prefetched LDS fragments, bit-identical
-        g_tn16_pf = 1;
+    for (int variant : {2, 1}) {   // 2: option tn_bf16_quad (4 waves of 128x128); 1: tn_bf16_pf
+        g_tn16_quad = variant == 2;
+        g_tn16_pf = variant == 1;
+        const char* name = variant == 2 ? "quad-wave" : "prefetched fragments";
         const double up = timeit([&] { gemm_tn_bf16(t, splits, 0); });
         CK(hipDeviceSynchronize());
         hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, got);
         std::vector<float> hr((size_t)N * K), hg(hr.size());
         CK(hipMemcpy(hr.data(), ref, hr.size() * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hg.data(), got, hg.size() * 4, hipMemcpyDeviceToHost));
-        printf("library DMA TN, prefetched fragments: %8.1f us  %7.1f TF/s  %6.2f TB/s  bitwise %s\n", up, flop / up * 1e-6,
+        printf("library DMA TN, %s: %8.1f us  %7.1f TF/s  %6.2f TB/s  bitwise %s\n", name, up, flop / up * 1e-6,
                bytes / up * 1e-6, memcmp(hr.data(), hg.data(), hr.size() * 4) == 0 ? "equal" : "DIFFERENT");
         TN16Args t0 = t;
         t0.lda = 0;
@@ -174,6 +190,18 @@ int main(int argc, char** argv) {
         const double u2 = timeit([&] { gemm_tn_bf16(t, 2 * splits, 0); });
         printf("  ... %3d splits: %8.1f us  %7.1f TF/s\n", 2 * splits, u2, flop / u2 * 1e-6);
         g_tn16_pf = 0;
+        g_tn16_quad = 0;
+    }
+    {   // the register-staged 256x256 kernel (tn_bf16_variant 2), normal and one-row operands
+        g_tn16_variant = 2;
+        const double u = timeit([&] { gemm_tn_bf16(t, splits, 0); });
+        TN16Args t0 = t;
+        t0.lda = 0;
+        t0.ldb = 0;
+        const double u0 = timeit([&] { gemm_tn_bf16(t0, splits, 0); });
+        printf("register-staged TN (variant 2): %8.1f us  %7.1f TF/s; one row (on-chip): %8.1f us  %7.1f TF/s\n", u,
+               flop / u * 1e-6, u0, flop / u0 * 1e-6);
+        g_tn16_variant = 3;
     }
     {   // the same kernel with every point row the same row (lda = ldb = 0): operands from L2 / L1,
         // the on-chip ceiling of the DMA pipeline
