@@ -13,6 +13,8 @@
 //  * N ≤ C-wide output heads (σ, rgb, sun, β, semantic logits) are per-point dot products.
 #include <algorithm>
 #include <type_traits>
+#include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -52,13 +54,9 @@ struct PackArgs {
 // One launch for up to kMaxPieces pieces: block b re-lays tile (b - tile0[piece]) of its piece,
 // 8 elements per thread.  Transposed pieces (fp32 or bf16) go through an LDS tile so both the
 // read (rows of the source) and the write (rows of the transpose) are coalesced.
-__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+// block b re-lays tile t of piece pc into packed
+__device__ __forceinline__ void pack_block(const PackPiece pc, int t, float* packed) {
     __shared__ float tileT[kPackTC][kPackTR + 1];
-    const int b = blockIdx.x;
-    int pi = 0;
-    while (pi + 1 < a.n && a.tile0[pi + 1] <= b) ++pi;  // block-uniform
-    const PackPiece pc = a.p[pi];
-    const int t = b - a.tile0[pi];
     const int tcols = (pc.cols + kPackTC - 1) / kPackTC;
     const int r0 = (t / tcols) * kPackTR, c0 = (t % tcols) * kPackTC;
     const int tid = threadIdx.x;
@@ -76,8 +74,8 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
             const int r = r0 + rr, c = c0 + cc;
             if (r < pc.rows && c < pc.cols) {
                 const int64_t o = pc.dst + (pc.bf == 2 ? trunk_frag_off(c, r, pc.dst_ld) : (int64_t)c * pc.dst_ld + r);
-                if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)tileT[cc][rr];
-                else a.packed[o] = pc.rnd ? (float)(bf16)tileT[cc][rr] : tileT[cc][rr];
+                if (pc.bf) reinterpret_cast<bf16*>(packed)[o] = (bf16)tileT[cc][rr];
+                else packed[o] = pc.rnd ? (float)(bf16)tileT[cc][rr] : tileT[cc][rr];
             }
         }
         return;
@@ -94,12 +92,12 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
                 const bf16 hi = (bf16)v;
                 o = (r & 1) ? (bf16)(v - (float)hi) : hi;
             }
-            reinterpret_cast<bf16*>(a.packed)[pc.dst + frag_off(r, c, pc.dst_ld, 1)] = o;
+            reinterpret_cast<bf16*>(packed)[pc.dst + frag_off(r, c, pc.dst_ld, 1)] = o;
             continue;
         }
         const float v = pc.src[(int64_t)r * pc.src_ld + pc.src_c0 + c];
         if (pc.bf == 3 || pc.bf == 4) {
-            bf16* dst = reinterpret_cast<bf16*>(a.packed) + pc.dst;
+            bf16* dst = reinterpret_cast<bf16*>(packed) + pc.dst;
             const int kp = pc.dst_ld / 4;
             const bf16 hi = (bf16)v, lo = (bf16)(v - (float)hi);
             const bf16 pl[4] = {hi, hi, lo, lo};
@@ -111,9 +109,30 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
                                     : pc.bf == 5   ? frag_off(r, c, pc.dst_ld, 1)
                                     : pc.transpose ? (int64_t)c * pc.dst_ld + r
                                                    : (int64_t)r * pc.dst_ld + c);
-        if (pc.bf) reinterpret_cast<bf16*>(a.packed)[o] = (bf16)v;
-        else a.packed[o] = pc.rnd ? (float)(bf16)v : v;
+        if (pc.bf) reinterpret_cast<bf16*>(packed)[o] = (bf16)v;
+        else packed[o] = pc.rnd ? (float)(bf16)v : v;
     }
+}
+
+__global__ __launch_bounds__(256) void k_pack(PackArgs a) {
+    const int b = blockIdx.x;
+    int pi = 0;
+    while (pi + 1 < a.n && a.tile0[pi + 1] <= b) ++pi;  // block-uniform
+    pack_block(a.p[pi], b - a.tile0[pi], a.packed);
+}
+
+// The same for a piece table resident in device memory (pack_table: one launch for any number
+// of pieces — the bf16 MLP's ~90 pieces took two kernarg-table launches per re-pack)
+__global__ __launch_bounds__(256) void k_pack_dev(const PackPiece* __restrict__ pcs, const int* __restrict__ tile0, int n,
+                                                  float* packed) {
+    const int b = blockIdx.x;
+    int lo = 0, hi = n - 1;  // the piece whose tile range holds b: tile0[pi] <= b < tile0[pi + 1]
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tile0[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    pack_block(pcs[lo], b - tile0[lo], packed);
 }
 
 // X0[p][c]: positional encoding of xyz = o + dir*z (rendering.py:147; spnerf.py:32-37), one
@@ -908,7 +927,56 @@ __global__ __launch_bounds__(256) void k_class_sum(int64_t B, const float* __res
 // host orchestration
 // ------------------------------------------------------------------------------------------
 
+// Device-resident piece tables, one per distinct table (the pieces hold the parameters' and
+// offsets' addresses: a model has one or two), built on first use outside a stream capture and
+// never freed (a captured graph may hold one); option pack_table 0 = the kernarg tables only
+int g_pack_table = 1;
+struct PackTable {
+    int dev;
+    std::vector<PackPiece> key;
+    PackPiece* d_pcs;
+    int* d_tile0;
+    int tiles;
+};
+static std::mutex g_pack_mu;
+static std::vector<PackTable> g_pack_tables;
+
+static const PackTable* pack_table(const std::vector<PackPiece>& pieces, hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pack_mu);
+    for (const PackTable& t : g_pack_tables)
+        if (t.dev == dev && t.key.size() == pieces.size() &&
+            std::memcmp(t.key.data(), pieces.data(), pieces.size() * sizeof(PackPiece)) == 0)
+            return &t;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if (g_pack_tables.size() >= 64) return nullptr;
+    std::vector<int> tile0(pieces.size() + 1, 0);
+    for (size_t i = 0; i < pieces.size(); ++i)
+        tile0[i + 1] = tile0[i] + cdiv(pieces[i].rows, kPackTR) * cdiv(pieces[i].cols, kPackTC);
+    PackTable t{dev, pieces, nullptr, nullptr, tile0.back()};
+    if (hipMalloc(&t.d_pcs, pieces.size() * sizeof(PackPiece)) != hipSuccess) return nullptr;
+    if (hipMalloc(&t.d_tile0, tile0.size() * sizeof(int)) != hipSuccess ||
+        hipMemcpy(t.d_pcs, pieces.data(), pieces.size() * sizeof(PackPiece), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(t.d_tile0, tile0.data(), tile0.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(t.d_pcs);
+        if (t.d_tile0) (void)hipFree(t.d_tile0);
+        return nullptr;
+    }
+    g_pack_tables.push_back(t);
+    return &g_pack_tables.back();
+}
+
 static int32_t launch_pack(const std::vector<PackPiece>& pieces, float* packed, hipStream_t s) {
+    if (g_pack_table && pieces.size() > (size_t)kMaxPieces) {
+        if (const PackTable* t = pack_table(pieces, s)) {
+            ProfScope prof("pack", s, 0.0, 0.0);
+            hipLaunchKernelGGL(k_pack_dev, dim3(t->tiles), dim3(256), 0, s, t->d_pcs, t->d_tile0, (int)pieces.size(), packed);
+            SPN_HIP(hipGetLastError());
+            return SPNERF_OK;
+        }
+    }
     for (size_t b = 0; b < pieces.size(); b += kMaxPieces) {
         PackArgs a{};
         a.packed = packed;
@@ -2218,6 +2286,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_bf16_bias_split") return &g_tn16_bias_split;
     if (n == "tn_bf16_few_tiles") return &g_tn16_few_tiles;
     if (n == "tn_group") return &g_tn_group;
+    if (n == "pack_table") return &g_pack_table;
     if (n == "tn_bf16_pf") return &g_tn16_pf;
     if (n == "tn_bf16_quad") return &g_tn16_quad;
     if (n == "tn_bf16_rounds") return &g_tn16_rounds;

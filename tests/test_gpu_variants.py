@@ -293,3 +293,26 @@ def test_bf16_tn_quad_wave_grouped_bitwise_equal():
         _lib.set_option("tn_bf16_quad", old)
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
+
+
+def test_pack_table_bitwise_equal():
+    """Option pack_table: the weight re-pack from a device-resident piece table (one launch)
+    writes the same packed buffer as the kernarg-table launches (two for the bf16 MLP)."""
+    model = make_model(ModelDims(width=512, sem=True, beta=True), 3, "bf16")
+    old = _lib.get_option("pack_table")
+    bufs, launches = [], []
+    try:
+        for t in (0, 1):
+            _lib.set_option("pack_table", t)
+            model.packed_weights()          # (first use builds the table)
+            torch.cuda.synchronize()
+            _lib.prof_reset()
+            _lib.prof_enable(True)
+            bufs.append(model.packed_weights().clone())
+            torch.cuda.synchronize()
+            _lib.prof_enable(False)
+            launches.append(_lib.prof_read("pack")["launches"])
+    finally:
+        _lib.set_option("pack_table", old)
+    assert torch.equal(bufs[0], bufs[1])
+    assert launches == [2, 1], launches
