@@ -125,15 +125,18 @@ def _deferred_grads(tn_group, n_rays=96, rounds=1, beta=False, defer_heads=1):
             _lib.set_option(k, v)
 
 
-@pytest.mark.parametrize("group,rounds,beta", [(4, 1, False), (9, 1, False), (9, 2, False), (10, 1, True), (6, 2, True)])
-def test_grouped_trunk_weight_gradients_match(group, rounds, beta):
+@pytest.mark.parametrize("group,rounds,beta,n_rays", [(4, 1, False, 96), (9, 1, False, 96), (9, 2, False, 96), (10, 1, True, 96),
+                                                    (6, 2, True, 96), (9, 0, False, 2048)])
+def test_grouped_trunk_weight_gradients_match(group, rounds, beta, n_rays):
     """Option tn_group: the deferred output-head (G / Q, defer_heads), sun_v and trunk-layer
     weight-gradient GEMMs (the skip layer's H part; its PE tail on the narrow kernel) run `group`
     per launch of the DMA kernel, splits in proportion to their points (`rounds` blocks per CU).  Fewer launches, the same gradients up to fp32
     summation order."""
-    g0, _ = _deferred_grads(1, beta=beta, defer_heads=0)   # the heads' weight gradients per pass
-    g1, n1 = _deferred_grads(1, beta=beta)
-    g2, n2 = _deferred_grads(group, rounds=rounds, beta=beta)
+    # (2 048 rays: 2^18 points per pass, the bench's sizes — the ungrouped skip layer takes the
+    # split-tail path, the grouped one the paired narrow launch, 2 blocks per CU with rounds 0)
+    g0, _ = _deferred_grads(1, n_rays, beta=beta, defer_heads=0)   # the heads' weight gradients per pass
+    g1, n1 = _deferred_grads(1, n_rays, beta=beta)
+    g2, n2 = _deferred_grads(group, n_rays, rounds=rounds, beta=beta)
     for n, a in g0.items():   # deferred heads (per segment, ungrouped) = per pass up to summation order
         if a.numel() >= 64 and float(a.norm()) > 0:
             assert float((a - g1[n]).norm() / a.norm()) <= 1e-4, n
@@ -148,6 +151,6 @@ def test_grouped_trunk_weight_gradients_match(group, rounds, beta):
             assert float((a - b).norm() / a.norm()) <= 1e-4, n
     assert (num / den) ** 0.5 <= 1e-5
     # deterministic: the same grouping twice is bit for bit the same
-    g3, _ = _deferred_grads(group, rounds=rounds, beta=beta)
+    g3, _ = _deferred_grads(group, n_rays, rounds=rounds, beta=beta)
     for n in g2:
         assert torch.equal(g2[n], g3[n]), n
