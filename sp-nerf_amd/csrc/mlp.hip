@@ -38,9 +38,15 @@ struct PackPiece {
     // same planes in the fused trunk's fragment order (dst_ld = 4·K0p); 6 = a narrow head's
     // [32][cols] hi/lo-row A operand (PackedOffs::Fnar16; rows = 32, nsrc source rows)
     int src_ld, src_c0, rows, cols, dst_ld, transpose, bf;
+    int src_idx;   // the parameter's index (device-resident tables: src comes from PackSrcs)
     int64_t dst;
     int nsrc = 0;  // bf = 6: source rows
     int rnd = 0;   // fp32 destination rounded to bf16 (precision study, option emu_bf16 & 4)
+};
+static_assert(sizeof(PackPiece) == 56, "PackArgs must stay within the 4 KB kernel-argument segment");
+constexpr int kPackParams = 64;
+struct PackSrcs {
+    const float* p[kPackParams];
 };
 constexpr int kMaxPieces = 64;
 constexpr int kPackTR = 32, kPackTC = 64;  // a block re-lays one 32 x 64 tile of a piece
@@ -124,7 +130,7 @@ __global__ __launch_bounds__(256) void k_pack(PackArgs a) {
 // The same for a piece table resident in device memory (pack_table: one launch for any number
 // of pieces — the bf16 MLP's ~90 pieces took two kernarg-table launches per re-pack)
 __global__ __launch_bounds__(256) void k_pack_dev(const PackPiece* __restrict__ pcs, const int* __restrict__ tile0, int n,
-                                                  float* packed) {
+                                                  float* packed, PackSrcs srcs) {
     const int b = blockIdx.x;
     int lo = 0, hi = n - 1;  // the piece whose tile range holds b: tile0[pi] <= b < tile0[pi + 1]
     while (lo < hi) {
@@ -132,7 +138,9 @@ __global__ __launch_bounds__(256) void k_pack_dev(const PackPiece* __restrict__ 
         if (tile0[mid] <= b) lo = mid;
         else hi = mid - 1;
     }
-    pack_block(pcs[lo], b - tile0[lo], packed);
+    PackPiece pc = pcs[lo];
+    pc.src = srcs.p[pc.src_idx];
+    pack_block(pc, b - tile0[lo], packed);
 }
 
 // X0[p][c]: positional encoding of xyz = o + dir*z (rendering.py:147; spnerf.py:32-37), one
@@ -927,9 +935,10 @@ __global__ __launch_bounds__(256) void k_class_sum(int64_t B, const float* __res
 // host orchestration
 // ------------------------------------------------------------------------------------------
 
-// Device-resident piece tables, one per distinct table (the pieces hold the parameters' and
-// offsets' addresses: a model has one or two), built on first use outside a stream capture and
-// never freed (a captured graph may hold one); option pack_table 0 = the kernarg tables only
+// Device-resident piece tables, one per distinct model layout (the parameters' addresses go in
+// the launch's kernarg PackSrcs, so every model of one configuration shares a table), built on
+// first use outside a stream capture and never freed (a captured graph may hold one); option
+// pack_table 0 = the kernarg tables only
 int g_pack_table = 1;
 struct PackTable {
     int dev;
@@ -941,9 +950,14 @@ struct PackTable {
 static std::mutex g_pack_mu;
 static std::vector<PackTable> g_pack_tables;
 
-static const PackTable* pack_table(const std::vector<PackPiece>& pieces, hipStream_t s) {
+static const PackTable* pack_table(const std::vector<PackPiece>& pieces0, hipStream_t s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::vector<PackPiece> pieces = pieces0;   // the key: layout only
+    for (PackPiece& p : pieces) {
+        if (p.src_idx < 0 || p.src_idx >= kPackParams) return nullptr;
+        p.src = nullptr;
+    }
     std::lock_guard<std::mutex> lk(g_pack_mu);
     for (const PackTable& t : g_pack_tables)
         if (t.dev == dev && t.key.size() == pieces.size() &&
@@ -971,8 +985,11 @@ static const PackTable* pack_table(const std::vector<PackPiece>& pieces, hipStre
 static int32_t launch_pack(const std::vector<PackPiece>& pieces, float* packed, hipStream_t s) {
     if (g_pack_table && pieces.size() > (size_t)kMaxPieces) {
         if (const PackTable* t = pack_table(pieces, s)) {
+            PackSrcs srcs{};
+            for (const PackPiece& p : pieces) srcs.p[p.src_idx] = p.src;
             ProfScope prof("pack", s, 0.0, 0.0);
-            hipLaunchKernelGGL(k_pack_dev, dim3(t->tiles), dim3(256), 0, s, t->d_pcs, t->d_tile0, (int)pieces.size(), packed);
+            hipLaunchKernelGGL(k_pack_dev, dim3(t->tiles), dim3(256), 0, s, t->d_pcs, t->d_tile0, (int)pieces.size(), packed,
+                               srcs);
             SPN_HIP(hipGetLastError());
             return SPNERF_OK;
         }
@@ -1002,7 +1019,7 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
     std::vector<PackPiece> v;
     auto piece = [&](int pi, int c0, int rows, int cols, int64_t dst, int dst_ld, int tr, int bf = 0) {
         SPN_ARG(prm[pi] != nullptr, "parameter %s is NULL", specs[pi].name.c_str());
-        v.push_back(PackPiece{prm[pi], (int)specs[pi].ld(), c0, rows, cols, dst_ld, tr, bf, dst});
+        v.push_back(PackPiece{prm[pi], (int)specs[pi].ld(), c0, rows, cols, dst_ld, tr, bf, pi, dst});
         return SPNERF_OK;
     };
     const int W = d.W, H = d.H;
