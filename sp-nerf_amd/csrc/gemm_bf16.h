@@ -83,6 +83,7 @@ struct TN16Group {
     int start[kTnGroup + 1];  // GEMM i's blocks: [start[i], start[i + 1])
     int n = 1;
 };
+static_assert(sizeof(TN16Group) <= 4096, "a kernel argument: within the 4 KB kernarg segment");
 bool tn_group_ok(int P, int N, int K);  // the shape runs on the DMA kernel
 int tn_tiles_bf16(int N, int K);        // its 256 x 256 tiles
 int32_t gemm_tn_bf16_group(const TN16Args* a, int n, const int* splits, hipStream_t s);
