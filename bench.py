@@ -58,7 +58,8 @@ GEMM_CLASSES = {
     "gemm_nt_bf16w": ("k_gemm_nt_bf16w (bf16 MFMA NT GEMM, register-staged)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_nt_bf16": ("k_gemm_nt_bf16 (bf16 MFMA NT GEMM, 128x128 tiles)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16d": ("k_gemm_tn_bf16d<IP> (bf16 MFMA weight-gradient GEMM, 256x256 tiles, LDS-DMA; IP = option "
-                      "tn_bf16_ip)", BF16_MFMA_PEAK_TFLOPS),
+                      "tn_bf16_ip; the deferred GEMMs of a render in one group launch, option tn_group)",
+                      BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16w": ("k_gemm_tn_bf16w (bf16 MFMA weight-gradient GEMM, 256x256 register-staged)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16": ("k_gemm_tn_bf16 (bf16 MFMA weight-gradient GEMM, 128x128 tiles)", BF16_MFMA_PEAK_TFLOPS),
     "gemm_tn_bf16k": ("k_gemm_tn_bf16_k64 (bf16 MFMA weight gradient N = 512, K = 64: fc_net.0 and the skip "
@@ -492,7 +493,8 @@ def roofline_of(dom, nt, traffic=None, traffic_src=None):
     if dom in GEMM_CLASSES:
         dom_name, peak = GEMM_CLASSES[dom]
         if "<IP>" in dom_name:   # the template instance the library launches under the current option
-            dom_name = dom_name.replace("<IP>", f"<{_lib.get_option('tn_bf16_ip')}>")
+            dom_name = dom_name.replace("<IP>", f"<{_lib.get_option('tn_bf16_ip')}, "
+                                                f"{'true' if _lib.get_option('tn_bf16_pf') == 1 else 'false'}>")
     else:
         dom_name, peak = HBM_CLASSES.get(dom, dom), None
     secs = nt["ms"] * 1e-3
