@@ -7,6 +7,25 @@ namespace spn {
 
 typedef __bf16 bf16;
 
+// Narrow output heads computed in the epilogue of the GEMM producing their input (the training
+// forward's G, Q and sun_v.3 layers; models/spnerf.py:345-367): a tile whose 256 columns start at
+// col0[i] is head group i's whole input; out[p] = f(Σ_c y[p][c]·w[o][c] + b[o]) over the tile's
+// bf16-rounded outputs y, o < nout[i].  kind: 0 = rgb (sigmoid, out cols 0..2 as x·1.002 - 0.001,
+// hsave 1..3), 1 = sun (sigmoid, out col 4 / hsave 4; the tile also writes σ = softplus(hsave 0)
+// to col 3 and, full, the ray's sky to cols 5..7 — not full: zeros elsewhere), 2 = beta
+// (softplus, out col 8, hsave 5 = pre-activation), 3 = semantic logits (out sem_col + o).
+constexpr int kNTHeads = 3;
+struct NTHeads {
+    int n = 0;
+    int col0[kNTHeads] = {}, nout[kNTHeads] = {}, kind[kNTHeads] = {};
+    const float* w[kNTHeads] = {};   // [nout][256] fp32 (row stride ldw)
+    int ldw[kNTHeads] = {};
+    const float* b[kNTHeads] = {};
+    float* out = nullptr; int NO = 0; int sem_col = 0;
+    float* hsave = nullptr;          // [M][8]
+    const float* sky = nullptr; int S = 1; int full = 0;
+};
+
 // C[M,N] = epi(A[M,K] · B[N,K]^T), bf16 operands, fp32 accumulation, bf16 C.  A may be split
 // along K (columns [K1,K) from A2: the skip-layer input [h | x0]).  Epilogue (as NTArgs):
 // + bias[col] + rowbias[row/rows_per_ray][col] + r1_a[row]*r1_v[col]; act==1 and col>=n_lin:
@@ -30,6 +49,7 @@ struct NT16Args {
     int zround = 0, dout_z = 0, dmul_z = 0;
     int dbg = 0;    // ablations (tools only; variant 8): 1 = no MFMAs, 2 = no epilogue, 4 = no DMA wait
     unsigned long long* stamps = nullptr;  // diagnostic builds (-DND_STAMPS, tools only)
+    NTHeads hd;     // narrow output heads folded into the epilogue (k_gemm_nt_bf16d, option heads_epi)
 };
 
 // slab[s][n][k] = Σ_{p in split s} A[p][n] · B[p][k] (B split along k at K1),

@@ -506,7 +506,11 @@ __device__ const float kZeroRow[2048 + 8] = {};
 // argument and kZeroRow otherwise compiles to
 typedef const __attribute__((address_space(1))) float* gfloat_ptr;
 __device__ __forceinline__ float ldgf(const float* p) { return *(gfloat_ptr)p; }
-template <bool DM, int IP = 0, int EV = 0>
+// HD: the narrow output heads of NT16Args::hd in the epilogue (EV 1 / 2 only): a head tile's
+// lanes dot their 8 bf16-rounded outputs per row with the head weights, the 8 lanes of a row
+// reduce by xor butterfly, the 4 column waves' partials meet in the staging LDS after a barrier
+// and are summed in wave order (deterministic).
+template <bool DM, int IP = 0, int EV = 0, bool HD = false>
 __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
     __shared__ __attribute__((aligned(16))) char smem[ND_STAGES * ND_STG + 8 * 4096];
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -589,6 +593,36 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
         // variants 1-3: the tile's bias (and rank-1 / per-ray row) values load before its K-loop,
         // so no epilogue wait covers the next tile's DMAs
         float bias8[8], r1v8[8], rbl[4];
+        // HD: this tile's head group (block-uniform) and this lane's 8 columns' head weights
+        // (the group's fields picked by unrolled compares: a dynamic index into the kernel
+        // argument would copy it to scratch)
+        int hg = -1, hno = 0, hkind = 0;
+        const float* hwp = nullptr;
+        const float* hbp = nullptr;
+        int hldw = 0;
+        float hw[3][8];
+        if constexpr (HD) {
+#pragma unroll
+            for (int i = 0; i < kNTHeads; ++i)
+                if (i < g.hd.n && g.hd.col0[i] == bn) {
+                    hg = i;
+                    hno = g.hd.nout[i];
+                    hkind = g.hd.kind[i];
+                    hwp = g.hd.w[i];
+                    hbp = g.hd.b[i];
+                    hldw = g.hd.ldw[i];
+                }
+            if (hg >= 0) {
+                const int cq0 = (opaque(lane) & 7) * 8;
+                const int cl = wc * 64 + cq0;  // column within the head's 256
+                const bool ok = bn + cl < g.N;
+#pragma unroll
+                for (int o = 0; o < 3; ++o)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) hw[o][e] = (o < hno && ok) ? ldgf(hwp + (int64_t)o * hldw + cl + e) : 0.f;
+            }
+        }
+        float hpart[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // this lane's two kept rows
         {
             const int cq0 = (opaque(lane) & 7) * 8;
             const int colc0 = min(bn + wc * 64 + cq0, g.N - 8);
@@ -768,6 +802,23 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                 }
                 oc[q4] = pack8(v);
                 od[q4] = (GEN && g.dout_z) ? pack8_f16(d) : pack8(d);
+                if constexpr (HD) {
+                    if (hg >= 0) {  // block-uniform
+                        float y[8];
+                        unpack8(oc[q4], y);
+                        const int combo = i * 4 + q4;   // lane (combo % 8) of the row keeps the row's sums
+#pragma unroll
+                        for (int o = 0; o < 3; ++o) {
+                            float t = 0.f;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) t += y[e] * hw[o][e];
+                            t += __shfl_xor(t, 1, 64);
+                            t += __shfl_xor(t, 2, 64);
+                            t += __shfl_xor(t, 4, 64);
+                            if ((el & 7) == (combo & 7)) hpart[combo >> 3][o] = t;
+                        }
+                    }
+                }
                 // materialise the piece's results here: hipcc otherwise sinks the arithmetic
                 // (and the Dmul waits, as vmcnt(0)) into the guarded stores below
                 asm volatile("" : "+v"(oc[q4]));
@@ -789,6 +840,64 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             ND_STAMP(8);
         }
         ND_STAMP(7);
+        if constexpr (HD) {
+            if (hg >= 0) {  // block-uniform: the 4 column waves' row partials, summed in wave order
+                __syncthreads();  // every wave is done with its staging
+                float* part = reinterpret_cast<float*>(smem + ND_STAGES * ND_STG);  // [4 wc][256 rows][4]
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int combo = 8 * k + (el & 7), pi = combo >> 2, pq = combo & 3;
+                    const int row = wr * 128 + pi * 32 + erow + 8 * pq;
+#pragma unroll
+                    for (int o = 0; o < 3; ++o) part[(wc * 256 + row) * 4 + o] = hpart[k][o];
+                }
+                __syncthreads();
+                const int row = tid;
+                const int64_t p = (int64_t)bm + row;
+                if (row < 256 && p < g.M) {
+                    const NTHeads& H = g.hd;
+                    const int kind = hkind;
+                    float x[3];
+#pragma unroll
+                    for (int o = 0; o < 3; ++o)
+                        x[o] = ((part[(0 * 256 + row) * 4 + o] + part[(1 * 256 + row) * 4 + o]) + part[(2 * 256 + row) * 4 + o]) +
+                               part[(3 * 256 + row) * 4 + o];
+                    // explicitly global accesses: a flat one would wait for the next tile's DMAs
+                    typedef __attribute__((address_space(1))) float* gfloat_w;
+                    const gfloat_w out = (gfloat_w)(H.out + p * H.NO);
+                    const gfloat_w hs = (gfloat_w)(H.hsave + p * 8);
+                    const float* bb = hbp;
+                    if (kind == 0) {          // rgb
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) {
+                            const float gv = sigmoidf_(x[c] + ldgf(bb + c));
+                            out[c] = __fsub_rn(__fmul_rn(gv, 1.002f), 0.001f);
+                            hs[1 + c] = gv;
+                        }
+                    } else if (kind == 1) {   // sun, and σ / sky
+                        const float sun = sigmoidf_(x[0] + ldgf(bb));
+                        out[4] = sun;
+                        hs[4] = sun;
+                        out[3] = softplusf_(hs[0]);
+                        if (H.full) {
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) out[5 + c] = ldgf(H.sky + (p / H.S) * 4 + c);
+                        } else {
+                            for (int c = 0; c < H.NO; ++c)
+                                if (c != 3 && c != 4) out[c] = 0.f;
+                        }
+                    } else if (kind == 2) {   // beta
+                        const float bpre = x[0] + ldgf(bb);
+                        out[8] = softplusf_(bpre);
+                        hs[5] = bpre;
+                    } else {                  // semantic logits
+#pragma unroll
+                        for (int o = 0; o < 3; ++o)
+                            if (o < hno) out[H.sem_col + o] = x[o] + ldgf(bb + o);
+                    }
+                }
+            }
+        }
         if (!more) break;  // block-uniform
         t = tn;
     }
@@ -1867,7 +1976,15 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
                 else if (a.Dmul && a.r1_a && !a.rowbias && a.act == 0 && !a.Dout) ev = 3;
             }
             const bool ip2 = g_nt16_ip_gen == 2;
-            if (ev == 1) {
+            if (a.hd.n > 0) {
+                SPN_ARG((ev == 1 || ev == 2) && ip2 && a.hd.n <= kNTHeads && a.hd.out && a.hd.hsave && a.N % 256 == 0,
+                        "gemm_nt_bf16: output heads need the bias / per-ray-row DMA epilogue");
+                for (int i = 0; i < a.hd.n; ++i)
+                    SPN_ARG(a.hd.col0[i] % 256 == 0 && a.hd.col0[i] + 256 <= a.N && a.hd.nout[i] >= 1 && a.hd.nout[i] <= 3,
+                            "gemm_nt_bf16: head group %d", i);
+                if (ev == 1) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 1, true>), grid, block, 0, s, a, nt);
+                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 2, true>), grid, block, 0, s, a, nt);
+            } else if (ev == 1) {
                 if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 1>), grid, block, 0, s, a, nt);
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 1>), grid, block, 0, s, a, nt);
             } else if (ev == 2) {

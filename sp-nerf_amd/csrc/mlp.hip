@@ -1156,6 +1156,7 @@ struct Ctx {
     int rs = 0, dir_off = 0;
     float* out = nullptr;           // the forward's output rows (the fused trunk + heads write them)
     bool* heads_done = nullptr;     // set when the trunk launch ran the fused heads too
+    bool* heads_epi_done = nullptr;  // set when the head GEMMs' epilogues wrote the narrow heads
     float* at(int64_t off) const { return ws + off; }
     const float* pk(int64_t off) const { return P + off; }
     bf16* hb(int64_t off) const { return reinterpret_cast<bf16*>(ws + off); }          // bf16 workspace buffer
@@ -1205,6 +1206,11 @@ int g_tn_group_rounds = 0;
 // stream are worth more (26.04 / 26.14 against 26.16 / 26.19 ms deferred; same call)
 int g_defer_heads = 2;
 int g_tn_k64_pair = 1;  // option "tn_k64_pair": the skip layer's PE tail and fc_net.0 in one narrow launch
+// option "heads_epi": the training forward's narrow heads (rgb, sun, beta, semantic logits; σ and the
+// sky columns with the sun) in the epilogues of the G / Q / sun_v.3 GEMMs instead of k_heads_fwd_v:
+// C4 26.39 / 26.35 -> 26.13 / 26.08 ms (heads_fwd's 0.58 ms for +0.31 ms of epilogue), C4@512
+// 3.950 / 3.945 -> 3.919 / 3.921 ms (same call)
+int g_heads_epi = 1;
 static bool defer_heads_for(int64_t P) { return g_defer_heads == 1 || (g_defer_heads == 2 && P <= (1 << 18)); }
 
 #ifndef SPN_DEFER_SUNV
@@ -1540,6 +1546,21 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
     if (BF && heads_fused_on(c, save, mode)) return SPNERF_OK;  // G, Q, sun_v 2/3 inside the fused heads
     T* S2buf = save ? G::buf(c, c.w.S2) : G::buf(c, c.w.Hb[((d.L - 1) & 1) ^ 1]);
     T* S3buf = save ? G::buf(c, c.w.S3) : G::buf(c, c.w.Hb[2]);
+    // option heads_epi: the narrow heads in the G / Q / sun_v.3 epilogues (bf16 DMA NT with the
+    // bias / per-ray-row epilogue; σ from the trunk's hsave column)
+    const bool hepi = BF && g_heads_epi && g_nt16_epi && save && sig_done && *sig_done && c.out && c.heads_epi_done &&
+                      W == 512 && H == 256 && (!d.sem || d.C <= 3) && S % 32 == 0 && mode != 1 &&
+                      d.NG % 256 == 0 && d.NQ % 256 == 0;
+    NTHeads hbase;
+    if (hepi) {
+        hbase.out = c.out; hbase.NO = d.NO; hbase.sem_col = d.sem_col;
+        hbase.hsave = c.at(c.w.hsave); hbase.sky = c.at(c.w.sky); hbase.S = S; hbase.full = mode == 0 ? 1 : 0;
+    }
+    auto head = [&](NTHeads& hd, int col0, int nout, int kind, int64_t w, int ldw, int64_t b) {
+        hd.col0[hd.n] = col0; hd.nout[hd.n] = nout; hd.kind[hd.n] = kind;
+        hd.w[hd.n] = c.pk(w); hd.ldw[hd.n] = ldw; hd.b[hd.n] = c.pk(b);
+        ++hd.n;
+    };
     // G = H_L · [feat ; sem hidden]^T   (feat linear, sem hidden sin)
     NT g;
     g.A = HL; g.lda = W; g.K1 = W;
@@ -1549,6 +1570,11 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
     g.bias = c.pk(c.k.bG);
     g.act = 1; g.w0 = 1.f; g.n_lin = W;
     if (save) { g.Dout = G::buf(c, c.w.DG); g.ld_dout = d.NG; }
+    if constexpr (BF)
+        if (hepi && mode == 0 && d.sem) {
+            g.hd = hbase;
+            head(g.hd, W, d.C, 3, c.k.Wm2, H, c.k.bm2);
+        }
     SPN_TRY(G::nt(g, s));
     // Q = feat · [sun1 ; rgb1 ; beta1]^T + per-ray (sun_d / t) rows, all sin
     NT q;
@@ -1560,6 +1586,12 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
     q.rowbias = c.at(c.w.rbQ); q.ld_rb = d.NQ; q.rows_per_ray = S;
     q.act = 1; q.w0 = 1.f;
     if (save) { q.Dout = G::buf(c, c.w.DQ); q.ld_dout = d.NQ; }
+    if constexpr (BF)
+        if (hepi && mode == 0) {
+            q.hd = hbase;
+            head(q.hd, H, 3, 0, c.k.Wr2, H, c.k.br2);
+            if (d.beta) head(q.hd, 2 * H, 1, 2, c.k.wb2, H, c.k.bb2);
+        }
     SPN_TRY(G::nt(q, s));
     // sun_v_net layers 2 and 3
     NT s2;
@@ -1576,7 +1608,14 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
     s3.C = S3buf;
     s3.bias = c.pk(c.k.bs3);
     s3.Dout = save ? G::buf(c, c.w.DS3) : nullptr;
-    return G::nt(s3, s);
+    if constexpr (BF)
+        if (hepi) {
+            s3.hd = hbase;
+            head(s3.hd, 0, 1, 1, c.k.ws4, H, c.k.bs4);
+        }
+    SPN_TRY(G::nt(s3, s));
+    if (hepi) *c.heads_epi_done = true;
+    return SPNERF_OK;
 }
 
 static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays, int rs, int dir_off,
@@ -1624,11 +1663,13 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
     }
     bool sig_done = false;  // hsave[p·8] (σ pre-activation) written by the fused trunk
     bool heads_done = false;  // the trunk launch ran the fused heads
+    bool heads_epi_done = false;  // the head GEMMs' epilogues wrote the narrow heads
     c.out = out;
     c.heads_done = &heads_done;
+    c.heads_epi_done = &heads_epi_done;
     if (d.bf) SPN_TRY(forward_gemms<bf16>(c, save, mode, s, &sig_done));
     else SPN_TRY(forward_gemms<float>(c, save, mode, s, nullptr));
-    if (heads_done) return SPNERF_OK;
+    if (heads_done || heads_epi_done) return SPNERF_OK;
     if (heads_fused_on(c, save, mode)) {
         double flop = 0.0, bytes = 0.0;
         const HeadsFusedArgs a = heads_args(c, mode, c.w.Hb[(d.L - 1) & 1], &flop, &bytes);
@@ -2310,6 +2351,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_group_rounds") return &g_tn_group_rounds;
     if (n == "defer_heads") return &g_defer_heads;
     if (n == "tn_k64_pair") return &g_tn_k64_pair;
+    if (n == "heads_epi") return &g_heads_epi;
     if (n == "tn_bf16_k64") return &g_tn16_k64;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;

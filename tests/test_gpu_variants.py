@@ -316,3 +316,56 @@ def test_pack_table_bitwise_equal():
         _lib.set_option("pack_table", old)
     assert torch.equal(bufs[0], bufs[1])
     assert launches == [2, 1], launches
+
+
+def _render_heads(opts, beta, n=300):
+    """A C3-flag bf16 training render (guided 64 + 64 samples, solar pass, semantic head; beta
+    with a t embedding) and its gradients under library options."""
+    old = {k: _lib.get_option(k) for k in opts}
+    for k, v in opts.items():
+        _lib.set_option(k, v)
+    try:
+        args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=beta, guidedsample=True,
+                                        sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+        rays = torch.tensor(gu_rays(n, 23), device=DEV)
+        g = torch.Generator(device="cpu").manual_seed(6)
+        kw = dict(valid_depth=(torch.rand(n, generator=g) < 0.7).long().to(DEV),
+                  target_depths=torch.stack([rays[:, 7] * 0.5, torch.ones(n, device=DEV)], 1),
+                  target_std=torch.full((n,), 0.01, device=DEV))
+        sem = torch.randint(0, 3, (n,), generator=g).to(DEV)
+        model = make_model(ModelDims(width=512, sem=True, beta=beta), 6, "bf16")
+        models = {"coarse": model}
+        ts = None
+        if beta:
+            torch.manual_seed(1)
+            models["t"] = torch.nn.Embedding(4, model.t_embedding_dims).to(DEV)
+            ts = torch.randint(0, 4, (n,), generator=g).to(DEV)
+        torch.manual_seed(7)
+        res = spnerf_amd.render_rays(models, args, rays, ts, semantics=sem, mode="train", **kw)
+        loss = sum((v.float() ** 2).mean() for k, v in sorted(res.items()) if v.requires_grad)
+        loss.backward()
+        torch.cuda.synchronize()
+        return ({k: v.detach().cpu() for k, v in res.items()},
+                {k: p.grad.detach().cpu() for k, p in model.named_parameters() if p.grad is not None})
+    finally:
+        for k, v in old.items():
+            _lib.set_option(k, v)
+
+
+@pytest.mark.parametrize("beta", [False, True])
+def test_heads_in_gemm_epilogue_agree(beta):
+    """Option heads_epi: the narrow heads (rgb, sun, beta, semantic logits; σ and sky with the sun)
+    computed in the epilogues of the G / Q / sun_v.3 GEMMs instead of k_heads_fwd_v: the same
+    dot products over the same bf16 inputs in another fp32 summation order — renders and gradients
+    agree to fp32 rounding."""
+    r0, g0 = _render_heads({"heads_epi": 0}, beta)
+    r1, g1 = _render_heads({"heads_epi": 1}, beta)
+    assert sorted(r0) == sorted(r1) and sorted(g0) == sorted(g1)
+    for k in r0:
+        assert torch.isfinite(r1[k]).all(), k
+        scale = r0[k].abs().max().item()
+        assert (r0[k] - r1[k]).abs().max().item() <= 1e-5 * scale + 1e-7, k
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        scale = g0[k].abs().max().item()
+        assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
