@@ -26,7 +26,9 @@ TOL = 1e-5  # norm-relative
 
 def _render(fused: bool, dims: ModelDims, n_rays: int, guided: bool, sc: float, seed: int = 0, n_samples: int = 64,
             options: dict | None = None):
-    opts = {"fused_trunk": int(fused), **(options or {})}
+    # (heads_epi 0: the narrow heads on k_heads_fwd_v for every variant compared here — the epilogue
+    # heads need the trunk's σ column, which not every trunk variant writes)
+    opts = {"fused_trunk": int(fused), "heads_epi": 0, **(options or {})}
     saved = {k: _lib.get_option(k) for k in opts}
     for k, v in opts.items():
         _lib.set_option(k, v)

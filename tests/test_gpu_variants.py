@@ -59,6 +59,7 @@ def test_fp32_gemm_variants_bitwise_equal(opts):
 
 
 def _render_bf16(opts, n=300, ns=64):
+    opts = {"heads_epi": 0, **opts}   # (k_heads_fwd_v for every GEMM variant compared: see test_gpu_trunk._render)
     old = {k: _lib.get_option(k) for k in opts}
     for k, v in opts.items():
         _lib.set_option(k, v)
