@@ -1942,6 +1942,7 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     // two blocks per CU (the LDS limit), depth 1 / 2
     int v = variant > 0 ? variant : g_nt16_variant;
     if (v == 8 && (a.K % ND_K != 0 || (a.K1 != a.K && a.K1 % ND_K != 0))) v = 5;  // DMA needs whole 32-wide K-steps
+    SPN_ARG(a.hd.n == 0 || v == 8, "gemm_nt_bf16: output heads need the DMA kernel (variant 8)");
     const bool dm = a.Dmul && !a.bias && !a.rowbias && !a.r1_a && a.act == 0 && !a.Dout;
     // one profiling class per kernel function: the DMA kernel's two epilogue instances apart
     ProfScope prof(v == 8 ? (dm ? "gemm_nt_bf16d_dmul" : "gemm_nt_bf16d") : v >= 5 ? "gemm_nt_bf16w" : "gemm_nt_bf16", s,
