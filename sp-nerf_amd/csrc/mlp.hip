@@ -833,8 +833,12 @@ __global__ __launch_bounds__(512) void k_tile_rowsum16(const bf16* __restrict__ 
 }
 
 // ... and the T tiles of a ray added in tile order: out[ray][c] = Σ_t part[ray·T + t][c]
-__global__ __launch_bounds__(256) void k_ray_tiles_sum(const float* __restrict__ part, int T, int64_t n_rays,
-                                                       float* __restrict__ out) {
+// (blockIdx.y = 1: the second part / output pair — layer 0 and the skip layer in one launch)
+__global__ __launch_bounds__(256) void k_ray_tiles_sum(const float* __restrict__ part0, int T, int64_t n_rays,
+                                                       float* __restrict__ out0, const float* __restrict__ part1,
+                                                       float* __restrict__ out1) {
+    const float* part = blockIdx.y ? part1 : part0;
+    float* out = blockIdx.y ? out1 : out0;
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n_rays * 512) return;
     const int64_t ray = i >> 9;
@@ -1211,6 +1215,7 @@ int g_tn_k64_pair = 1;  // option "tn_k64_pair": the skip layer's PE tail and fc
 // C4 26.39 / 26.35 -> 26.13 / 26.08 ms (heads_fwd's 0.58 ms for +0.31 ms of epilogue), C4@512
 // 3.950 / 3.945 -> 3.919 / 3.921 ms (same call)
 int g_heads_epi = 1;
+int g_ray_tiles_pair = 1;  // option "ray_tiles_pair": the per-ray dZ sums of layer 0 and the skip layer in one launch
 static bool defer_heads_for(int64_t P) { return g_defer_heads == 1 || (g_defer_heads == 2 && P <= (1 << 18)); }
 
 #ifndef SPN_DEFER_SUNV
@@ -1880,7 +1885,16 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
             SPN_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(k_ray_tiles_sum, dim3((unsigned)cdiv(n_rays * 512, 256)), dim3(256), 0, s2, part, S / 64,
-                           n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4));
+                           n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), nullptr, nullptr);
+        SPN_HIP(hipGetLastError());
+        return SPNERF_OK;
+    };
+    // both layers' tile sums written by the fused chain: one launch adds both, after the chain
+    bool pair_tiles = false;
+    auto ray_tiles_pair = [&]() -> int32_t {
+        ProfScope prof("ray_rowsum", s2, 0.0, 2.0 * 4.0 * (P / 64 + n_rays) * W);
+        hipLaunchKernelGGL(k_ray_tiles_sum, dim3((unsigned)cdiv(n_rays * 512, 256), 2), dim3(256), 0, s2, c.at(c.w.Rp0),
+                           S / 64, n_rays, c.at(c.w.R0), c.at(c.w.Rp4), c.at(c.w.R4));
         SPN_HIP(hipGetLastError());
         return SPNERF_OK;
     };
@@ -1901,7 +1915,8 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
             SPN_TRY(tn_grad<T>(c, dZi, W, W, In, ldin, nullptr, 0, c.k.Kp[i], c.k.Kp[i], s2,
                                {red(0, W, kreal, gp(x.fcW[i]), ld(x.fcW[i]), gp(x.fcb[i]))}, zin));
         if (d.sem && (i == 0 || i == d.skip)) {
-            if (tsum) SPN_TRY(ray_tiles(i, dZi, parts_in_bwd));
+            if (pair_tiles) {
+            } else if (tsum) SPN_TRY(ray_tiles(i, dZi, parts_in_bwd));
             else SPN_TRY(ray_rowsum<T>(dZi, W, 0, W, S, n_rays, c.at(i == 0 ? c.w.R0 : c.w.R4), W, s2));
         }
         // a mark is recorded only once its gradients are final: deferred layers get theirs from
@@ -1928,6 +1943,8 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         // algorithmic HBM bytes: dZ_{L-1} in, per layer D_{i-1} in and dZ_{i-1} out
         SPN_TRY(trunk_bwd_bf16(a, s, 2.0 * P * W * W * (d.L - 1), 2.0 * P * W * (1.0 + 2.0 * (d.L - 1))));
         SPN_TRY(stream_dep(sd, s, s2));
+        pair_tiles = parts_in_bwd && g_ray_tiles_pair;
+        if (pair_tiles) SPN_TRY(ray_tiles_pair());
         for (int i = d.L - 1; i >= 0; --i) SPN_TRY(layer_grads(i, i == d.L - 1 ? dZ : buf(c.w.Db[i])));
         return SPNERF_OK;
     }
@@ -2353,6 +2370,7 @@ static int* option_slot(const char* name) {
     if (n == "defer_heads") return &g_defer_heads;
     if (n == "tn_k64_pair") return &g_tn_k64_pair;
     if (n == "heads_epi") return &g_heads_epi;
+    if (n == "ray_tiles_pair") return &g_ray_tiles_pair;
     if (n == "tn_bf16_k64") return &g_tn16_k64;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;

@@ -122,7 +122,7 @@ def test_seeded_init_matches_reference():
 def test_kernel_options_roundtrip_and_reject_unknown_names():
     L = _lib.lib()
     for name in ("fused_trunk", "trunk_tile", "nt_f32_variant", "tn_f32_variant", "nt_bf16_variant", "tn_bf16_variant", "heads_variant",
-                 "l0_split", "trunk_l0", "fused_heads", "zsave", "pe_inline", "tn_split_tail", "tn_bf16_k64", "trunk_dreg", "trunk_bwd_dreg", "trunk_bwd_nt", "trunk_sigma", "nt_bf16_ip", "tn_bf16_ip", "nt_bf16_epi", "tn_group", "tn_group_rounds", "defer_heads", "tn_k64_pair", "tn_bf16_pf", "tn_bf16_rounds", "tn_bf16_quad", "pack_table", "heads_epi",
+                 "l0_split", "trunk_l0", "fused_heads", "zsave", "pe_inline", "tn_split_tail", "tn_bf16_k64", "trunk_dreg", "trunk_bwd_dreg", "trunk_bwd_nt", "trunk_sigma", "nt_bf16_ip", "tn_bf16_ip", "nt_bf16_epi", "tn_group", "tn_group_rounds", "defer_heads", "tn_k64_pair", "tn_bf16_pf", "tn_bf16_rounds", "tn_bf16_quad", "pack_table", "heads_epi", "ray_tiles_pair",
                  "bwd_streams"):
         old = _lib.get_option(name)
         _lib.set_option(name, old)
