@@ -66,7 +66,7 @@ GEMM_CLASSES = {
                       "layer's PE tail, whole 512x64 output per split)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bf16": ("k_trunk2_bf16<128> (fused bf16 trunk, inference: 128-point LDS-resident tiles, option trunk2 3; "
                    "k_trunk_bf16<128> with trunk2 0)", BF16_MFMA_PEAK_TFLOPS),
-    "trunk_bf16_train": ("k_trunk_bf16<64> (fused bf16 trunk, training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
+    "trunk_bf16_train": ("k_trunk_bf16<128, 2048> (fused bf16 trunk, 128-point training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bwd_bf16": ("k_trunk_bwd_bf16 (fused bf16 backward dX chain, LDS-resident dZ)", BF16_MFMA_PEAK_TFLOPS),
     "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_heads_bf16": ("k_trunk2_bf16<128, L0, false, true> (fused bf16 inference trunk with the heads on its last LDS "

@@ -45,7 +45,7 @@ namespace spn {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 int g_fused_trunk = 1;
-int g_trunk_tile = 0;  // 0 = by mode (64 when saving, else 128); 64 / 128 force a tiling (A/B runs)
+int g_trunk_tile = 0;  // 0 = 128 (64 when saving Z, zsave); 64 / 128 force a tiling (A/B runs)
 // bit 1: the training trunk's H copy-outs non-temporal (glc slc), the default: C4@512 4.41 -> 4.30 and
 // 4.18 / 4.20 -> 4.09 / 4.09 ms, C4 26.63 / 26.64 -> 26.60 / 26.57, C3 7.36 -> 7.26, C5 level (pairs in
 // one call each, tools/gpu_r3u.sh, tools/gpu_r3v.sh); bit 4: the register-D
@@ -91,6 +91,9 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
     constexpr int TPD = Geo::TPD;
     constexpr bool NOMF = VAR & 16, NOSIN = VAR & 32, NOW = VAR & 64, NOB = VAR & 128, NOEPI = VAR & 256;
     constexpr bool DREG = Geo::DIMG && (VAR & 512);  // D from the registers (see epilogue_dreg)
+    // (VAR 2048: the saving launches of the 128-point tiling as their own instance — the same code,
+    // so rocprof tells the training launches from the inference ones by name)
+    static_assert(!(VAR & 2048) || TMt == 128, "the 128-point training instance");
     __shared__ __attribute__((aligned(16))) char smem[Geo::LDS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     float* sbias = reinterpret_cast<float*>(smem + Geo::BIAS_OFF);
@@ -555,6 +558,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 if (last) {
                     __syncthreads();
                     copy_all(smem, Hs, p0);
+                    if (g.sig_hsave) sigma_rows(p0);  // block-uniform
                 }
                 hpend = last ? nullptr : Hs;
             }
@@ -845,7 +849,9 @@ bool trunk_bf16_supported(int W, int L, int skip, int K0p) {
     return W == TW && L >= 2 && L <= kTrunkMaxL && K0p <= 64 && K0p % 16 == 0 && skip < L;
 }
 
-static int trunk_tile(bool save) { return g_trunk_tile ? g_trunk_tile : (save ? 64 : 128); }
+// 128-point tiles for training too: C4 26.16 / 26.07 -> 25.41 / 25.43 ms, C4@512 3.789 -> 3.656 ms
+// (pairs in one call; the 64-point tiling halves the points each weight byte from L2 serves)
+static int trunk_tile(bool save) { return g_trunk_tile ? g_trunk_tile : 128; }
 
 bool trunk_l0_supported(int K0p, bool save) {
     const int tpd = trunk_tile(save) == 64 ? TrunkGeo<64>::TPD : TrunkGeo<128>::TPD;
@@ -857,7 +863,7 @@ bool trunk_l0_supported(int K0p, bool save) {
 int g_trunk_sigma = 1;
 
 bool trunk_sigma_ok(const TrunkArgs& a, bool save) {
-    return g_trunk_sigma && save && !a.zround && !trunk2_supported(a, save) && trunk_tile(save) == 64;
+    return g_trunk_sigma && save && !a.zround && !trunk2_supported(a, save);  // either training tiling
 }
 
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes) {
@@ -879,9 +885,9 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     ad.dbg = g_trunk_dbg;
     ad.nt = (g_trunk_nt & 1) | ((g_trunk_nt & 4) ? 2 : 0);  // H copy-outs / register-D stores non-temporal
     const int ntiles = cdiv(a.P, tm);
-    // the saving 64-point tiling (training) is its own profiling class: its roofline (HBM-heavy,
-    // H and D of every layer out) is not the inference tiling's (MFMA-bound)
-    ProfScope prof(tm == 64 ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
+    // the saving launches (training) are their own profiling class: their roofline (HBM-heavy,
+    // H and D of every layer out) is not the inference launches' (MFMA-bound)
+    ProfScope prof(save ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
     if (tm == 64 && g_trunk_dreg && g_trunk_var == 32)  // ablation: no sin / cos in the epilogue
         hipLaunchKernelGGL((k_trunk_bf16<64, 544>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     else if (tm == 64 && g_trunk_dreg && g_trunk_var == 256)  // ablation: no epilogue at all
@@ -894,6 +900,7 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     else if (g_trunk_var == 128) hipLaunchKernelGGL((k_trunk_bf16<128, 128>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 256) hipLaunchKernelGGL((k_trunk_bf16<128, 256>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     else if (g_trunk_var == 464) hipLaunchKernelGGL((k_trunk_bf16<128, 464>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else if (save) hipLaunchKernelGGL((k_trunk_bf16<128, 2048>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     else hipLaunchKernelGGL((k_trunk_bf16<128, 0>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;

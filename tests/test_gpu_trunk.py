@@ -96,7 +96,7 @@ def test_fused_trunk_matches_layerwise(dims, n_rays, guided, sc):
 
 def test_fused_trunk_with_layer0_when_saving_bitwise_vs_layerwise():
     """trunk_l0=2 (the default): fc_net.0 inside the fused launch also when activations are saved
-    (64-point tiles, D = w0·cos(w0·z) of layer 0 from the trunk's epilogue); trunk_l0=1 keeps it a
+    (the training tiles, D = w0·cos(w0·z) of layer 0 from the trunk's epilogue); trunk_l0=1 keeps it a
     separate GEMM there."""
     old = _lib.get_option("trunk_l0")
     try:
@@ -155,22 +155,39 @@ def test_training_trunk_register_d_bitwise(dims, n_rays, guided, sc, n_samples, 
     """k_trunk_bf16<64> with D = cos stored from the accumulators during the epilogue (option
     trunk_dreg 1, the default; layers with per-ray rows keep the D image) against the D image
     drained behind the next k-loop (0): the same values, so renders and gradients bit for bit."""
-    opts = {"trunk_l0": l0}
+    opts = {"trunk_l0": l0, "trunk_tile": 64}
     base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_dreg=0))
     _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_dreg=1)), base)
 
 
+@pytest.mark.parametrize("dims,n_rays,guided,sc,n_samples,l0", [
+    (ModelDims(width=512, sem=True), 257, True, 0.1, 64, 2),  # C3 flags, layer 0 in the launch
+    (ModelDims(width=512, sem=True), 257, True, 0.1, 64, 1),  # layer 0 as its own GEMM
+    (ModelDims(width=512), 33, False, 0.1, 32, 2),            # 33·32 points: the last 128-point tile a quarter full
+])
+def test_training_trunk_128_point_tiles_bitwise(dims, n_rays, guided, sc, n_samples, l0):
+    """The training trunk on 128-point tiles (option trunk_tile 128: cos through the image
+    between two barriers, then sin; σ pre-activation rows from the last image) against the
+    64-point tiles: the same per-point arithmetic and k order, so renders and gradients bit for
+    bit, with the narrow heads on k_heads_fwd_v and in the head GEMMs' epilogues."""
+    for hepi in (0, 1):
+        opts = {"trunk_l0": l0, "heads_epi": hepi}
+        base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_tile=64))
+        _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options=dict(opts, trunk_tile=128)), base)
+
+
+@pytest.mark.parametrize("tile", [64, 128])
 @pytest.mark.parametrize("dims,n_rays,guided,sc,n_samples", [
     (ModelDims(width=512, sem=True), 257, True, 0.1, 64),   # C3 flags: main (all heads) and solar (σ + sun) passes
-    (ModelDims(width=512), 33, False, 0.1, 32),             # the last 64-point tile half full
+    (ModelDims(width=512), 33, False, 0.1, 32),             # the last tile partly full
 ])
-def test_training_trunk_sigma_rows_bitwise(dims, n_rays, guided, sc, n_samples):
+def test_training_trunk_sigma_rows_bitwise(dims, n_rays, guided, sc, n_samples, tile):
     """The training trunk writing each point's σ pre-activation from its last layer's LDS image
     (option trunk_sigma 1, the default: k_heads_fwd_v's lane layout, dot4 order and wave_total, so
     the wave-per-point heads skip H_L) against the heads computing it from H_L (0): renders and
     gradients bit for bit."""
-    base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 0})
-    _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 1}), base)
+    base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 0, "trunk_tile": tile})
+    _assert_bitwise(_render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk_sigma": 1, "trunk_tile": tile}), base)
 
 
 @pytest.mark.parametrize("dims,n_rays,guided,sc,n_samples", [
