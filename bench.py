@@ -69,9 +69,9 @@ GEMM_CLASSES = {
     "trunk_bf16_train": ("k_trunk_bf16<128, 2048> (fused bf16 trunk, 128-point training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bwd_bf16": ("k_trunk_bwd_bf16 (fused bf16 backward dX chain, LDS-resident dZ)", BF16_MFMA_PEAK_TFLOPS),
     "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
-    "trunk_heads_bf16": ("k_trunk2_bf16<128, L0, false, true> (fused bf16 inference trunk with the heads on its last LDS "
+    "trunk_heads_bf16": ("k_trunk_bf16<128, 4096> (fused bf16 inference trunk with the heads on its last LDS "
                          "image: layers 0..7, sigma, semantic, feat, Q, albedo, sun_v, sun per 128-point tile; option "
-                         "trunk_heads)", BF16_MFMA_PEAK_TFLOPS)}
+                         "trunk_heads 2; k_trunk2_bf16<128, L0, false, true> with trunk_heads 1)", BF16_MFMA_PEAK_TFLOPS)}
 HBM_CLASSES = {"tn_skinny": "k_tn_skinny_multi (narrow-head / per-ray weight gradients, one launch per backward step)",
                "reduce_slabs": "k_reduce_slabs(_multi) (fixed-order weight-gradient split reductions)",
                "encode": "k_encode (positional encoding)", "heads_fwd": "k_heads_fwd_v (narrow heads)",

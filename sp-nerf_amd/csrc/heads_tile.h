@@ -328,4 +328,13 @@ __device__ __forceinline__ void heads_tile(GA& g, KA& k, char* smem, float* ost,
 }
 
 }  // namespace hd
+
+// The argument of a fused trunk launch that runs the heads on its last image: the trunk's (first,
+// so the kernarg-segment reads of TrunkArgs stay valid) and the heads'
+struct TrunkHeadsArgs : TrunkArgs {
+    HeadsFusedArgs hg;
+    PackedOffs hk;
+};
+static_assert(sizeof(TrunkHeadsArgs) <= 4096, "a kernel argument: within the 4 KB kernarg segment");
+
 }  // namespace spn

@@ -1483,11 +1483,14 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
             const double bytes = in + 2.0 * P * W * nout + (a.X0b_out ? 2.0 * P * d.K0p : 0.0);
             if constexpr (BF) {
                 // inference: the fused heads on the trunk's last LDS image (no H_L in HBM)
-                if (c.heads_done && c.out && heads_fused_on(c, save, mode) && trunk2_heads_ok(a)) {
+                if (c.heads_done && c.out && heads_fused_on(c, save, mode) && (trunk1_heads_ok(a) || trunk2_heads_ok(a))) {
                     double hflop = 0.0, hbytes = 0.0;
                     const HeadsFusedArgs h = heads_args(c, mode, -1, &hflop, &hbytes);
                     // algorithmic bytes: the trunk's input, the output rows (H_L never leaves)
-                    SPN_TRY(trunk2_heads_bf16(a, h, c.k, s, 2.0 * P * W * ksum + hflop, in + (hbytes - 2.0 * P * W)));
+                    if (trunk1_heads_ok(a))
+                        SPN_TRY(trunk1_heads_bf16(a, h, c.k, s, 2.0 * P * W * ksum + hflop, in + (hbytes - 2.0 * P * W)));
+                    else
+                        SPN_TRY(trunk2_heads_bf16(a, h, c.k, s, 2.0 * P * W * ksum + hflop, in + (hbytes - 2.0 * P * W)));
                     *c.heads_done = true;
                     return SPNERF_OK;
                 }

@@ -178,6 +178,10 @@ int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, 
 // the inference trunk with the fused heads on its last LDS image (k_trunk2_bf16 HEADS): no H_L in HBM
 extern int g_trunk_heads;
 bool trunk2_heads_ok(const TrunkArgs& a);
+// the same fused heads inside the one-workgroup k_trunk_bf16<128> (option trunk_heads 2)
+bool trunk1_heads_ok(const TrunkArgs& a);
+int32_t trunk1_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const PackedOffs& k, hipStream_t s, double flop,
+                          double bytes);
 int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const PackedOffs& k, hipStream_t s, double flop,
                           double bytes);
 

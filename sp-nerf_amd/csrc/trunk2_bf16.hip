@@ -101,10 +101,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(bf16* t, int64_t p0,
 // The HEADS kernel's argument: the trunk's (first, so the kernarg-segment reads of TrunkArgs stay
 // valid) and the heads' — read per tile through an opaque kernarg pointer, so the compiler does not
 // hoist the heads' ~40 offsets out of the tile loop into registers live through the trunk layers
-struct Trunk2HeadsArgs : TrunkArgs {
-    HeadsFusedArgs hg;
-    PackedOffs hk;
-};
+using Trunk2HeadsArgs = TrunkHeadsArgs;  // (heads_tile.h)
 
 template <int TM, bool L0, bool SAVE, bool HEADS = false>
 __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(
@@ -508,12 +505,13 @@ int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, d
     return SPNERF_OK;
 }
 
-// option trunk_heads: 1 = a bf16 inference forward whose trunk takes the 128-point two-workgroup
-// kernel runs the fused heads inside it (H_L stays in LDS); 0 = the trunk, then k_heads_bf16
-int g_trunk_heads = 1;
+// option trunk_heads: a bf16 inference forward runs the fused heads inside its trunk launch (H_L
+// stays in LDS): 2 = in the one-workgroup k_trunk_bf16<128> (trunk_bf16.hip, the default), 1 = in
+// the two-workgroup kernel here; 0 = the trunk, then k_heads_bf16
+int g_trunk_heads = 2;
 
 bool trunk2_heads_ok(const TrunkArgs& a) {
-    return g_trunk_heads && trunk2_tm(a) == 128 && trunk2_supported(a, false);
+    return g_trunk_heads == 1 && trunk2_tm(a) == 128 && trunk2_supported(a, false);
 }
 
 int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const PackedOffs& k, hipStream_t s, double flop,

@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "heads_tile.h"
 #include "trunk.h"
 
 #ifndef SPN_BIAS_HOIST
@@ -84,17 +85,26 @@ __device__ __forceinline__ int x0_rel(int row, int ch) { return row * 128 + ((ch
 // VAR (TMt = 128 only): 0 = the kernel; profiling ablations (outputs invalid; option trunk_var),
 // bits: 16 = no MFMAs in the main k-loop, 32 = no sine in the epilogue, 64 = no weight refills
 // in the k-loop, 128 = no image (B) reads in the k-loop, 256 = no epilogue (464: all of them)
+// HEADS (VAR 4096; inference, TMt = 128, option trunk_heads 2): the fused heads (heads_tile.h) run
+// on the last layer's LDS image, so H_L never leaves the chip; their output staging is 8 KB beyond
+// the trunk's LDS, their partials overlay the PE tile (restaged by the next tile), and the weight
+// ring is primed per tile instead of running on through the heads.  The heads' arguments are read
+// per tile through an opaque kernarg pointer (not hoisted into registers live through the layers).
 template <int TMt, int VAR = 0>
-__global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
+__global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 4096) != 0, TrunkHeadsArgs, TrunkArgs> g,
+                                                    int ntiles) {
     using Geo = TrunkGeo<TMt>;
     constexpr int NJ = Geo::NJ, IMG = Geo::IMG, CPT = Geo::CPT;
     constexpr int TPD = Geo::TPD;
+    constexpr bool HEADS = (VAR & 4096) != 0;
+    static_assert(!HEADS || (TMt == 128 && Geo::BIAS_OFF - Geo::X0_OFF >= hd::PART_BYTES &&
+                             Geo::LDS + hd::OST_BYTES <= 160 * 1024), "the fused heads: 128-point tiles, LDS");
     constexpr bool NOMF = VAR & 16, NOSIN = VAR & 32, NOW = VAR & 64, NOB = VAR & 128, NOEPI = VAR & 256;
     constexpr bool DREG = Geo::DIMG && (VAR & 512);  // D from the registers (see epilogue_dreg)
     // (VAR 2048: the saving launches of the 128-point tiling as their own instance — the same code,
     // so rocprof tells the training launches from the inference ones by name)
     static_assert(!(VAR & 2048) || TMt == 128, "the 128-point training instance");
-    __shared__ __attribute__((aligned(16))) char smem[Geo::LDS];
+    __shared__ __attribute__((aligned(16))) char smem[Geo::LDS + (HEADS ? hd::OST_BYTES : 0)];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     float* sbias = reinterpret_cast<float*>(smem + Geo::BIAS_OFF);
     char* sx0 = smem + Geo::X0_OFF;
@@ -185,10 +195,12 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
 
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
-    prime(first, std::integral_constant<int, 0>{}, std::integral_constant<int, TPD>{});
+    if constexpr (!HEADS) prime(first, std::integral_constant<int, 0>{}, std::integral_constant<int, TPD>{});
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TMt;
         const int st = opaque(tid);
+        // (HEADS) the first layer's stream, in flight through the tile's staging
+        if constexpr (HEADS) prime(first, std::integral_constant<int, 0>{}, std::integral_constant<int, TPD>{});
         // stage the first layer's input and the PE tile; rows past P read a clamped row (their
         // outputs are never stored)
         if (l0) {
@@ -262,7 +274,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
             // k-loop instead reloaded registers whose refills were still in flight, and hipcc
             // drained vmcnt(0) — every refill and H / D copy-out store — before each epilogue
             const bool last = i == g.L - 1;
-            const int inext = last ? (tile + (int)gridDim.x < ntiles ? first : -1) : i + 1;
+            const int inext = last ? (!HEADS && tile + (int)gridDim.x < ntiles ? first : -1) : i + 1;
             const bf16* wnxt = inext >= 0 ? wstream(inext) : wsrc;
             const int nkm = i == 0 ? nk0 : nmain;  // k-steps over the image
             float* sb = sbias + (i & 1) * TW;  // slot (i-1)&1 may still be read by the previous epilogue
@@ -557,8 +569,16 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(TrunkArgs g, int ntiles) {
                 epi(std::integral_constant<int, 1>{});
                 if (last) {
                     __syncthreads();
-                    copy_all(smem, Hs, p0);
-                    if (g.sig_hsave) sigma_rows(p0);  // block-uniform
+                    if constexpr (HEADS) {  // H_L stays on chip: the heads on this image
+                        typedef const __attribute__((address_space(4))) TrunkHeadsArgs* KH;
+                        KH kh = (KH)__builtin_amdgcn_kernarg_segment_ptr();
+                        asm volatile("" : "+s"(kh));  // opaque per tile: the heads' argument loads stay here
+                        hd::heads_tile<false>(kh->hg, kh->hk, smem, reinterpret_cast<float*>(smem + Geo::LDS),
+                                              reinterpret_cast<float*>(smem + Geo::X0_OFF), nullptr, p0);
+                    } else {
+                        copy_all(smem, Hs, p0);
+                        if (g.sig_hsave) sigma_rows(p0);  // block-uniform
+                    }
                 }
                 hpend = last ? nullptr : Hs;
             }
@@ -864,6 +884,35 @@ int g_trunk_sigma = 1;
 
 bool trunk_sigma_ok(const TrunkArgs& a, bool save) {
     return g_trunk_sigma && save && !a.zround && !trunk2_supported(a, save);  // either training tiling
+}
+
+bool trunk1_heads_ok(const TrunkArgs& a) {
+    bool save = false;
+    for (int i = 1; i < a.L; ++i) save |= a.Ds[i] != nullptr;
+    return g_trunk_heads == 2 && g_fused_trunk && !save && !a.zround && trunk_tile(false) == 128 && !a.X0b_out &&
+           trunk_bf16_supported(TW, a.L, a.skip, a.K0p) && (!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, false)));
+}
+
+int32_t trunk1_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const PackedOffs& k, hipStream_t s, double flop,
+                          double bytes) {
+    SPN_ARG(trunk1_heads_ok(a), "trunk1_heads_bf16: unsupported shape or option");
+    SPN_ARG(h.P == a.P && h.S == a.S && h.NO <= hd::OST_LD && h.C <= 4 && k.Fnar16 >= 0, "trunk1_heads_bf16: bad heads");
+    SPN_ARG(!a.rays || (a.z && a.rs > 0 && !a.X0), "trunk1_heads_bf16: inline encoding needs z and rs");
+    if (a.P == 0) return SPNERF_OK;
+    SPN_ARG(a.P < (1ll << 31) / TW, "trunk1_heads_bf16: too many points (%lld)", (long long)a.P);
+    const int ntiles = cdiv(a.P, 128);
+    TrunkHeadsArgs ad;
+    static_cast<TrunkArgs&>(ad) = a;
+    ad.dbg = 0;
+    ad.nt = 0;
+    ad.hg = h;
+    ad.hg.nt = 0;
+    ad.hg.dbg = 0;
+    ad.hk = k;
+    ProfScope prof("trunk_heads_bf16", s, flop, bytes);
+    hipLaunchKernelGGL((k_trunk_bf16<128, 4096>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
 }
 
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes) {

@@ -171,12 +171,15 @@ def test_inline_encoding_bit_identical():
             assert torch.equal(outs[0][k], outs[1][k]), (sem, k)
 
 
-@pytest.mark.parametrize("sem,B,S", [(True, 3000, 128), (False, 301, 40), (True, 37, 128)])
-def test_trunk_with_fused_heads_bit_identical(sem, B, S):
-    """The inference trunk running the fused heads on its last LDS image (option trunk_heads 1:
-    H_L never goes to HBM; k_trunk2_bf16 HEADS) against the trunk launch followed by the heads
-    kernel (trunk_heads 0, H_L through HBM): the same bf16 H_L bits and the same heads code
-    (heads_tile.h), so every output is bit-identical.  301 x 40 points end in a ragged tile."""
+@pytest.mark.parametrize("th", [2, 1])
+@pytest.mark.parametrize("sem,B,S", [(True, 3000, 128), (False, 301, 40), (True, 37, 128), (True, 300, 64)])
+def test_trunk_with_fused_heads_bit_identical(sem, B, S, th):
+    """The inference trunk running the fused heads on its last LDS image (option trunk_heads 2:
+    the one-workgroup k_trunk_bf16<128> HEADS, the default; 1: k_trunk2_bf16 HEADS; H_L never goes
+    to HBM) against the trunk launch followed by the heads kernel (trunk_heads 0, H_L through
+    HBM): the same bf16 H_L bits and the same heads code (heads_tile.h), so every output is
+    bit-identical.  301 x 40 points end in a ragged tile; 64 samples per ray put two rays' per-ray
+    rows in one 128-point tile (trunk_heads 1 then falls back to the separate heads)."""
     from spnerf_amd import _lib
     from oracle.weights import ModelDims
     g = torch.Generator(device="cpu").manual_seed(11)
@@ -188,13 +191,13 @@ def test_trunk_with_fused_heads_bit_identical(sem, B, S):
     model = make_model(ModelDims(width=512, sem=sem), 9, "bf16")
     outs = []
     try:
-        for th in (1, 0):
-            _lib.set_option("trunk_heads", th)
+        for t in (th, 0):
+            _lib.set_option("trunk_heads", t)
             with torch.no_grad(), random_source(FixedU(u)):
                 outs.append(spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels if sem else None,
                                                    mode="test"))
     finally:
-        _lib.set_option("trunk_heads", 1)
+        _lib.set_option("trunk_heads", 2)
     for k in outs[1]:
         assert torch.isfinite(outs[0][k]).all(), k
         assert torch.equal(outs[0][k], outs[1][k]), (k, float((outs[0][k] - outs[1][k]).abs().max()))
