@@ -49,7 +49,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // s_waitcnt 51–65 % of their cycles (one-workgroup kernel 37 %): vmcnt retires loads and stores
 // in order, so the weight refills issued after an epilogue's D stores wait for those stores'
 // acknowledgements.  Bit-identical (tests/test_gpu_trunk.py).
-int g_trunk2 = 3;
+// Round 4: 0 is the default again — the one-workgroup k_trunk_bf16<128> is now the faster inference
+// trunk (C5 trunk alone, trunk_heads 0: 15.49 against 16.65 ms per step, one call) and carries the
+// fused heads itself (trunk_heads 2).
+int g_trunk2 = 0;
 
 namespace {
 constexpr int TW = 512;

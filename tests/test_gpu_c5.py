@@ -193,11 +193,13 @@ def test_trunk_with_fused_heads_bit_identical(sem, B, S, th):
     try:
         for t in (th, 0):
             _lib.set_option("trunk_heads", t)
+            _lib.set_option("trunk2", 3 if t == 1 else 0)   # trunk_heads 1 rides on the two-workgroup trunk
             with torch.no_grad(), random_source(FixedU(u)):
                 outs.append(spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels if sem else None,
                                                    mode="test"))
     finally:
         _lib.set_option("trunk_heads", 2)
+        _lib.set_option("trunk2", 0)
     for k in outs[1]:
         assert torch.isfinite(outs[0][k]).all(), k
         assert torch.equal(outs[0][k], outs[1][k]), (k, float((outs[0][k] - outs[1][k]).abs().max()))

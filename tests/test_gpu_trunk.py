@@ -138,7 +138,7 @@ def test_two_workgroup_trunk_bitwise(dims, n_rays, guided, sc, n_samples):
     """k_trunk2_bf16 (D stored from the registers, trunk2_bf16.hip; 128-point tiles, or 64-point
     tiles two workgroups per CU) against the one-workgroup kernels with the D image: training
     (trunk2=1), training and inference (trunk2=2, layer 0 and the inline encoding in the launch)
-    and inference only (trunk2=3, the default) equal trunk2=0 bit for bit."""
+    and inference only (trunk2=3) equal trunk2=0 (the default) bit for bit."""
     base = _render(True, dims, n_rays, guided, sc, n_samples=n_samples, options={"trunk2": 0})
     for tile in (128, 64):
         for t2 in (1, 2, 3):
