@@ -710,6 +710,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 line reported beside the default C4 at N=1")
     ap.add_argument("--torch-adam", action="store_true", help="torch.optim.Adam(fused=True) instead of spnerf_amd.optim.Adam")
     ap.add_argument("--torch-loss", action="store_true", help="the losses module (plain torch) instead of the fused loss kernels")
+    ap.add_argument("--torch-gather", action="store_true", help="torch indexing per field instead of the one-launch batch gather")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--psnr-steps", type=int, default=1000,
                     help="steps per seed of the paired bf16-vs-fp32 training PSNR study in the default line (0 = skip)")
@@ -825,6 +826,8 @@ class TrainStep:
         # (this rank's rows are a view of the global batch: one copy per step)
         self.gidx_s = torch.empty(B * world, dtype=torch.int64, device=dev)
         self.idx_s = self.gidx_s[rank * B:(rank + 1) * B]
+        # this rank's rows of every per-ray field in one launch, into static buffers
+        self.gather = None if getattr(a, "torch_gather", False) else dp.BatchGather(self.R, B)
         # The gradient all-reduce (N > 1): by default in buckets (dp.GradBuckets), each issued on a
         # communication stream behind the backward mark after which its gradients are final, so the
         # collectives overlap the rest of the backward; --flat-allreduce = one all-reduce after it.
@@ -854,23 +857,24 @@ class TrainStep:
         accumulated: the caller clears them before an eager call)."""
         R, c, world = self.R, self.c, self.world
         idx, gidx = self.idx_s, self.gidx_s
-        # each per-ray field gathered once, shared by the render and the loss (the guided clamp's
-        # global first ray is this batch's first row on one rank)
-        rays = R["rays"][idx]
-        depths, valid, dstd = R["depths"][idx], R["valid_depth"][idx], R["depth_std"][idx]
+        # each per-ray field gathered once (one launch), shared by the render and the loss (the
+        # guided clamp's global first ray is this batch's first row on one rank)
+        bt = self.gather(idx) if self.gather is not None else {k: v[idx] for k, v in R.items()}
+        rays = bt["rays"]
+        depths, valid, dstd = bt["depths"], bt["valid_depth"], bt["depth_std"]
         kw = {}
         if c["guided"]:
             first = rays[0, 6:8] if world == 1 else R["rays"].index_select(0, gidx[:1])[0, 6:8]
             kw = dict(valid_depth=valid, target_depths=depths, target_std=dstd, clamp_near_far=first)
-        sem = R["sems"][idx] if c["sem"] else None
+        sem = bt["sems"] if c["sem"] else None
         res = spnerf_amd.render_rays({"coarse": self.model}, self.args, rays, None, semantics=sem, mode="train", **kw)
         self.res = res
         if self.floss is not None:   # the trainer's loss sum (main.py:143-174) in two kernels
-            loss, _ = self.floss(res, R["rgbs"][idx], depths, valid, dstd, sem,
+            loss, _ = self.floss(res, bt["rgbs"], depths, valid, dstd, sem,
                                  labels_global=R["sems"][gidx] if (world > 1 and sem is not None) else None, world=world)
             loss.backward()
             return loss.detach()
-        loss, _ = self.sloss(res, R["rgbs"][idx])
+        loss, _ = self.sloss(res, bt["rgbs"])
         if self.dloss is not None:
             loss = loss + self.dloss(res, depths[:, 0], depths[:, 1], valid, dstd)[0]
         if self.semloss is not None:

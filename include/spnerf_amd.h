@@ -234,6 +234,15 @@ int32_t spnerf_adam_step(int32_t n, void* const* params, const void* const* grad
                          void* const* exp_avg_sq, const int64_t* numel, double lr, double beta1, double beta2,
                          double eps, int32_t step, void* stream);
 
+/* ---- batch gather (reference main.py:108-115, satellite_scene.py:577-592: the DataLoader's
+ * per-ray batch; here the dataset's fields stay resident in HBM) ----------------------------------
+ * For nfields <= 8 fields f: dst[f] row i = src[f] row idx[i], i < n, rows of row_bytes[f] bytes
+ * (a positive multiple of 4; 4-byte aligned tensors).  An index outside [0, src_rows[f]) leaves
+ * its destination row untouched (torch indexing would raise; the caller's sampler draws in range).
+ * One launch for all fields. */
+int32_t spnerf_gather_rows(const int64_t* idx, int64_t n, int32_t nfields, const void* const* src,
+                           const int64_t* src_rows, const int32_t* row_bytes, void* const* dst, void* stream);
+
 /* ---- gradient readiness marks for data parallelism (no reference counterpart: the reference
  *      trains on one GPU, main.py:322-337).  A backward passes n_marks = layers + 2 points after
  *      which groups of parameter gradients are final: mark 0 after the output heads', mark

@@ -75,6 +75,43 @@ class SharedSeedSampler:
         return g, g[self.rank * self.local:(self.rank + 1) * self.local]
 
 
+class BatchGather:
+    """The batch's per-ray fields gathered in ONE launch (spnerf_gather_rows) into buffers
+    allocated once: ``out[k][i] = fields[k][idx[i]]`` for every key — the trainer's
+    ``batch[k]`` from the DataLoader (main.py:108-115, satellite_scene.py:577-592), with the
+    dataset resident in HBM.  Bit-exact copies; the static outputs let a captured HIP graph read
+    each new batch.  Every field: contiguous on the GPU, rows a multiple of 4 bytes, at most 8."""
+
+    def __init__(self, fields: dict, n: int):
+        import ctypes
+        from . import _lib
+        self._lib = _lib
+        self.keys = list(fields)
+        assert 0 < len(self.keys) <= 8, "BatchGather: 1..8 fields"
+        self.src = [fields[k].contiguous() for k in self.keys]
+        _lib.require_device(*self.src)
+        self.out = {k: torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+                    for k, t in zip(self.keys, self.src)}
+        self.n = n
+        nf = len(self.keys)
+        row_bytes = [t.element_size() * (t.numel() // max(t.shape[0], 1)) for t in self.src]
+        for k, rb in zip(self.keys, row_bytes):
+            if rb % 4:
+                raise ValueError(f"BatchGather: field {k!r} rows are {rb} bytes (not a multiple of 4)")
+        self._src = (ctypes.c_void_p * nf)(*[t.data_ptr() for t in self.src])
+        self._dst = (ctypes.c_void_p * nf)(*[self.out[k].data_ptr() for k in self.keys])
+        self._rows = (ctypes.c_int64 * nf)(*[t.shape[0] for t in self.src])
+        self._rb = (ctypes.c_int32 * nf)(*row_bytes)
+
+    def __call__(self, idx: torch.Tensor) -> dict:
+        assert idx.dtype == torch.int64 and idx.is_contiguous() and idx.numel() == self.n, "BatchGather: idx"
+        self._lib.require_device(idx)
+        self._lib.check(self._lib.lib().spnerf_gather_rows(self._lib.ptr(idx), self.n, len(self.keys), self._src,
+                                                          self._rows, self._rb, self._dst, self._lib.stream_of(idx)),
+                        "gather_rows")
+        return self.out
+
+
 def allreduce_grads(params, world: int, group=None):
     """One flat all-reduce (SUM then /world) of every gradient.
 
