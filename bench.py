@@ -555,48 +555,73 @@ def kernel_table(steps):
     return dict(sorted(out.items(), key=lambda kv: -kv[1]["ms_per_step"]))
 
 
-def run_inference(a, c, rank, world, dev):
-    """Config 5: ray-sharded whole-image inference.  Rank r generates rows [r·h/N, (r+1)·h/N)
-    of the image with the GPU RPC ray generator, then each step renders the next chunk of its
-    shard (render_rays in test mode: stratified samples, MLP without saved activations,
-    compositing).  No collective: the ranks only meet at the timing barriers."""
+def c5_shard(c, rank, world, dev, img_downscale=None):
+    """Rank ``rank``'s row shard [r0, r1) of the C5 image: its RPC rays (GPU generator), synthetic
+    semantic labels as a fixed function of the GLOBAL ray index (so a shard's labels do not depend
+    on the sharding), and the seeded SPNeRF.  Returns (rays, sems, model, args, h, w, r0)."""
     from spnerf_amd.satellite import image_rays, load_cameras
+    ds = c["img_downscale"] if img_downscale is None else img_downscale
     cams = load_cameras()
     meta = cams["images"][c["view"]]
-    h, w = int(meta["height"] // c["img_downscale"]), int(meta["width"] // c["img_downscale"])
+    h, w = int(meta["height"] // ds), int(meta["width"] // ds)
     r0, r1 = rank * h // world, (rank + 1) * h // world
-    rays = image_rays(meta, c["img_downscale"], cams["scene_loc"], crop=(r0, 0, r1 - r0, w), device=dev)
-    g = torch.Generator(device="cpu").manual_seed(rank)
-    sems = torch.multinomial(torch.tensor([0.45, 0.3, 0.15, 0.1]), rays.shape[0], replacement=True, generator=g)
-    sems = torch.where(sems == 3, torch.full_like(sems, -100), sems).to(dev)
+    rays = image_rays(meta, ds, cams["scene_loc"], crop=(r0, 0, r1 - r0, w), device=dev)
+    gid = torch.arange(r0 * w, r1 * w, device=dev, dtype=torch.int64)
+    u = ((gid * 0x9E3779B1) & 0xFFFFFFFF).double() / 2.0 ** 32     # labels 0/1/2/ignore at 45/30/15/10 %
+    sems = torch.full_like(gid, -100)
+    sems = torch.where(u < 0.9, torch.full_like(gid, 2), sems)
+    sems = torch.where(u < 0.75, torch.full_like(gid, 1), sems)
+    sems = torch.where(u < 0.45, torch.zeros_like(gid), sems)
     torch.manual_seed(0)
     model = spnerf_amd.SPNeRF(num_sem_classes=3, s_embedding_factor=1, layers=8, feat=512, mapping=True, sem=c["sem"],
                               precision=c["precision"]).to(dev)
-    args = make_args(c)
-    B, n = a.global_batch or c["batch"], rays.shape[0]
+    return rays, sems, model, make_args(c), h, w, r0
+
+
+def run_inference(a, config, rank, world, dev, steps=None, warmup=None, secondary=False):
+    """Config 5: ray-sharded whole-image inference.  Rank r generates rows [r·h/N, (r+1)·h/N)
+    of the image with the GPU RPC ray generator, then each step renders the next chunk of its
+    shard (render_rays in test mode: stratified samples, MLP without saved activations,
+    compositing).  No collective: the ranks only meet at the timing barriers.  Returns the JSON
+    record (``secondary``: the C5 line inside the default C4 line, its own batch, no CPU leg)."""
+    c = CONFIGS[config]
+    steps = a.steps if steps is None else steps
+    warmup = a.warmup if warmup is None else warmup
+    rays, sems, model, args, h, w, r0 = c5_shard(c, rank, world, dev)
+    B, n = (0 if secondary else a.global_batch) or c["batch"], rays.shape[0]
     pos = [0]
+    # stratified draws on-device (Philox keyed by the global ray id), as in training: no RNG launch
+    src = spnerf_amd.PhiloxRandom(seed=0)
 
     @torch.no_grad()
     def step():
         i0 = pos[0]
         idx = torch.arange(i0, i0 + B, device=dev) % n
         pos[0] = (i0 + B) % n
-        return spnerf_amd.render_rays({"coarse": model}, args, rays[idx], None, semantics=sems[idx], mode="test")
+        src.ray_offset = r0 * w + i0
+        with spnerf_amd.random_source(src):
+            return spnerf_amd.render_rays({"coarse": model}, args, rays[idx], None, semantics=sems[idx], mode="test")
 
-    for _ in range(a.warmup):
+    wd = dp.StepWatchdog(rank=rank, mode="eager inference")
+    for i in range(warmup):
+        wd.beat(i, "warmup")
         step()
+    wd.beat(0, "sync after warmup")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     _lib.prof_reset()
     _lib.prof_enable(True)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(steps):
+        wd.beat(i, "timed")
         res = step()
+    wd.beat(steps, "sync after timed steps")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    wd.close()
     _lib.prof_enable(False)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
@@ -604,49 +629,52 @@ def run_inference(a, c, rank, world, dev):
     elapsed = float(elapsed.item())
     dom = dominant_class()
     nt = _lib.prof_read(dom)
-    total = world * B * c["n_samples"] * a.steps
+    total = world * B * c["n_samples"] * steps
     value = total / elapsed
     out = {
         "metric": "ray-samples/sec (inference render)", "value": value, "unit": "ray-samples/s", "n_gpus": world,
-        "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
+        "steps": steps, "warmup": warmup, "ms_per_step": 1e3 * elapsed / steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": c["precision"],
         "data": "synthetic RPC camera rays (JAX_269_006 RPC at x5), synthetic semantic labels, seeded-random SPNeRF init",
         "config": {"workload": c["workload"], "global_batch": B * world, "samples_per_ray": c["n_samples"],
                    "parallelism": f"ray-shard{world}", "image_rays": h * w},
         "image_seconds_projected": h * w * c["n_samples"] / value,
-        "roofline": roofline_of(dom, nt, *measured_traffic(a.config, B, dom)),
-        "mlp_mfma_utilisation": gemm_totals(a.steps),
-        "kernels": kernel_table(a.steps),
+        "roofline": roofline_of(dom, nt, *measured_traffic(config, B, dom)),
+        "mlp_mfma_utilisation": gemm_totals(steps),
+        "kernels": kernel_table(steps),
         "finite": bool(torch.isfinite(res["rgb_coarse"]).all()),
     }
-    if a.full_image:
-        out["full_image"] = full_image(rays, sems, model, args, B, rank, world, dev, h, w, c)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if a.full_image and not secondary:
+        out["full_image"] = full_image(rays, sems, model, args, B, rank, world, dev, h, w, c, r0)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not secondary:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or 1024)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    return out
 
 
 @torch.no_grad()
-def full_image(rays, sems, model, args, B, rank, world, dev, h, w, c):
+def full_image(rays, sems, model, args, B, rank, world, dev, h, w, c, r0=0, return_image=False):
     """The whole C5 image: every rank renders all rays of its row shard in chunks of B into an
     HBM-resident [rows·w][4] (rgb, depth) buffer, then the shards are gathered to rank 0 (one
     all_gather of equal, padded shards; on CPU copies when the group is gloo).  Timed from the
-    first chunk to the gathered image on rank 0, max over ranks."""
+    first chunk to the gathered image on rank 0, max over ranks.  The stratified draws are
+    on-device Philox keyed by (seed, step 0, GLOBAL ray id = r0·w + index in the shard), so the
+    image does not depend on the sharding or the chunking (tests/test_gpu_bench_lines.py)."""
+    from spnerf_amd import PhiloxRandom, random_source
     n = rays.shape[0]
     shard = torch.empty(n, 4, device=dev)
+    src = PhiloxRandom(seed=0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i0 in range(0, n, B):
-        i1 = min(n, i0 + B)
-        res = spnerf_amd.render_rays({"coarse": model}, args, rays[i0:i1], None, semantics=sems[i0:i1], mode="test")
-        shard[i0:i1, 0:3] = res["rgb_coarse"]
-        shard[i0:i1, 3] = res["depth_coarse"]
+    with random_source(src):
+        for i0 in range(0, n, B):
+            i1 = min(n, i0 + B)
+            src.ray_offset = r0 * w + i0
+            src.reset_step(-1)
+            res = spnerf_amd.render_rays({"coarse": model}, args, rays[i0:i1], None, semantics=sems[i0:i1], mode="test")
+            shard[i0:i1, 0:3] = res["rgb_coarse"]
+            shard[i0:i1, 3] = res["depth_coarse"]
     torch.cuda.synchronize()
     t_render = time.perf_counter() - t0
     if world > 1:
@@ -674,6 +702,8 @@ def full_image(rays, sems, model, args, B, rank, world, dev, h, w, c):
         img = image.reshape(h, w, 4)
         info.update({"finite": bool(torch.isfinite(img).all()), "rgb_mean": [float(v) for v in img[..., :3].mean((0, 1))],
                      "depth_min_max": [float(img[..., 3].min()), float(img[..., 3].max())]})
+        if return_image:
+            info["image"] = img
     return info
 
 
@@ -736,6 +766,9 @@ def parse_args(argv=None):
                          "also SPNERF_NO_GRAPH_ALLREDUCE=1")
     ap.add_argument("--precision", choices=("bf16", "fp32"), default=None,
                     help="override the config's MLP precision (parity runs; the default line keeps the config's)")
+    ap.add_argument("--rehearse-collective", action="store_true",
+                    help="(N=1 rehearsal of the N>1 path) a one-rank RCCL group: the bucket all-reduces (identities) "
+                         "captured into the step graph, the exposed collective from paired replays")
     ap.add_argument("--share-device", action="store_true",
                     help="(rehearsal on a 1-GPU box) every rank on cuda:0 over gloo instead of RCCL")
     return ap.parse_args(argv)
@@ -750,6 +783,10 @@ def main():
     rank, local, world = dp.env_rank()
     if world != a.gpus:
         raise SystemExit(f"bench: launched with WORLD_SIZE={world} but --gpus {a.gpus}")
+    if world > 1:
+        # the deferred weight gradients' last group at most 2 GEMMs: the marks of trunk layers 4, 3
+        # fire a launch earlier and their all-reduce overlaps layers 2, 1 (smaller exposed bucket)
+        _lib.set_option("tn_group_last", 2)
     for o in a.option:
         name, value = o.split("=")
         _lib.set_option(name, int(value))
@@ -757,19 +794,28 @@ def main():
     torch.cuda.set_device(local)                  # before the process group: RCCL binds this device
     dev = torch.device("cuda", local)
     dp.init_from_env("gloo" if a.share_device else "nccl", device=dev)
+    if a.rehearse_collective and world == 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     c = CONFIGS[a.config]
     if c.get("inference"):
-        return run_inference(a, c, rank, world, dev)
-    out = run_train(a, a.config, rank, world, dev)
+        out = run_inference(a, a.config, rank, world, dev)
+    else:
+        out = run_train(a, a.config, rank, world, dev)
     if rank == 0 and world == 1 and a.config == "c4" and not a.no_secondary:
-        # configs[1] (C2, fp32) beside the headline, same process and GPU, no CPU leg
+        # configs[1] (C2, fp32) and configs[4] (C5, whole-image inference: 10 of its 32768-ray
+        # chunks) beside the headline, same process and GPU, no CPU leg
+        keys = ("value", "unit", "ms_per_step", "dtype", "config", "roofline", "mlp_mfma_utilisation")
         sec = run_train(a, "c2", rank, world, dev, secondary=True)
-        out["secondary"] = {"c2": {k: sec[k] for k in ("value", "unit", "ms_per_step", "dtype", "config", "roofline",
-                                                          "mlp_mfma_utilisation")}}
+        out["secondary"] = {"c2": {k: sec[k] for k in keys}}
+        sec = run_inference(a, "c5", rank, world, dev, steps=10, warmup=3, secondary=True)
+        out["secondary"]["c5"] = {k: sec[k] for k in keys + ("steps", "image_seconds_projected")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -836,7 +882,12 @@ class TrainStep:
         # the backward only and the buckets follow each replay.  allreduce_ms_per_step = the EXPOSED
         # part: HIP events on the compute stream from the end of the backward to the moment every
         # bucket has landed (not separable when the all-reduce is inside the graph: null then)
-        self.buckets = dp.GradBuckets(self.model, world) if (world > 1 and not a.flat_allreduce) else None
+        # --rehearse-collective (N=1): a one-rank RCCL group runs the N>1 bucket path (identity
+        # all-reduces, captured into the graph) so that path is exercised on one GPU
+        self.rehearse = (bool(getattr(a, "rehearse_collective", False)) and world == 1 and dist.is_initialized()
+                         and not secondary)
+        self.buckets = (dp.GradBuckets(self.model, world) if ((world > 1 or self.rehearse) and not a.flat_allreduce)
+                        else None)
         if self.buckets is not None:
             self.buckets.arm(True)
         self.ar_events = []
@@ -886,8 +937,8 @@ class TrainStep:
     def reduce_grads(self, overlap=True):
         if self.buckets is not None:
             flat = self.model._flat_grad
-            self.buckets.launch(flat, overlap=overlap)
-            self.buckets.finish(flat)
+            self.buckets.launch(flat, overlap=overlap, force=self.rehearse)
+            self.buckets.finish(flat, force=self.rehearse)
         else:
             dp.allreduce_grads(self.params, self.world)   # one RCCL all-reduce of the flat gradient
 
@@ -896,7 +947,7 @@ class TrainStep:
         holds the collectives)."""
         if self.in_graph and replayed:
             return                              # the graph reduced the gradients
-        if self.world > 1 and self.ar_timing:
+        if (self.world > 1 or self.rehearse) and self.ar_timing:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             self.reduce_grads(overlap=not replayed)
@@ -941,7 +992,8 @@ class TrainStep:
         """Warm up on a side stream, then capture render + loss + backward (+ the overlapped RCCL
         buckets) once as a HIP graph; replays overwrite the same gradient tensors.  Falls back to
         eager (and says so) when a capture is refused."""
-        a, dist_nccl = self.a, (self.world > 1 and dist.get_backend() == "nccl")
+        a = self.a
+        dist_nccl = (self.world > 1 or self.rehearse) and dist.is_initialized() and dist.get_backend() == "nccl"
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -958,8 +1010,8 @@ class TrainStep:
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     self.static_loss = self.fwd_bwd()
-                    self.buckets.launch(self.model._flat_grad, overlap=True)
-                    self.buckets.finish(self.model._flat_grad)
+                    self.buckets.launch(self.model._flat_grad, overlap=True, force=self.rehearse)
+                    self.buckets.finish(self.model._flat_grad, force=self.rehearse)
                 self.in_graph = True
             except Exception as e:
                 print(f"bench: capturing the all-reduce refused ({type(e).__name__}: {e}); it follows each replay",
@@ -979,6 +1031,49 @@ class TrainStep:
                 torch.cuda.synchronize()
         self.graph = graph
         return graph is not None
+
+    def probe(self) -> dict:
+        """Watchdog diagnosis: the gradient marks an EAGER backward reached (the marks inside a
+        replayed graph are its own edges and record nothing the host can query)."""
+        if self.graph is not None:
+            return {"marks": "inside the replayed graph (not queryable)", "allreduce_in_graph": self.in_graph}
+        if self.buckets is None:
+            return {"marks": None}
+        n = self.buckets.n_marks
+        done = [k for k in range(n) if _lib.grad_mark_query(k)]
+        return {"marks_completed": done, "n_marks": n}
+
+    def exposed_collective_ms(self, reps: int = 5, wd=None):
+        """With the bucket all-reduces captured INTO the step graph, the exposed collective per
+        step cannot be timed by host events around it: it is measured as the difference of paired
+        replays (each synchronized, medians of ``reps``) of the step graph with the buckets and of
+        a second capture of the same render + loss + backward without them.  None unless the
+        collectives are in the graph."""
+        if not self.in_graph or self.graph is None:
+            return None
+        import statistics
+        torch.cuda.synchronize()
+        self.opt.zero_grad(set_to_none=True)
+        self.model.invalidate_packed()           # both graphs contain the weight re-pack
+        plain = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(plain):
+            self.fwd_bwd()
+        torch.cuda.synchronize()
+        t = {"with": [], "without": []}
+        for r in range(reps):
+            for key, g in (("with", self.graph), ("without", plain)):
+                if wd is not None:
+                    wd.beat(r, f"paired replay ({key} buckets)")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                g.replay()
+                e1.record()
+                e1.synchronize()
+                t[key].append(e0.elapsed_time(e1))
+        del plain
+        med = {k: statistics.median(v) for k, v in t.items()}
+        return {"exposed_ms": max(0.0, med["with"] - med["without"]), "replay_ms_with_buckets": med["with"],
+                "replay_ms_without": med["without"], "reps": reps}
 
     def close(self):
         from spnerf_amd import set_random_source
@@ -1001,12 +1096,19 @@ def run_train(a, config, rank, world, dev, secondary=False):
     synchronize on both sides, max over ranks), per-kernel timings; returns the JSON record."""
     ts = TrainStep(a, config, rank, world, dev, secondary=secondary)
     c, B = ts.c, ts.B
+    # a step still running after SPNERF_STEP_DEADLINE seconds ends this rank with one JSON
+    # diagnosis and exit code 3 (dp.StepWatchdog) instead of blocking until the driver's limit
+    wd = dp.StepWatchdog(rank=rank, mode="graph" if a.graph else "eager", probe=ts.probe)
+    wd.beat(0, "capture" if a.graph else "warmup")
     if a.graph:
         if not ts.capture(a.warmup):
             a.graph = False
+    wd.mode = "graph" if ts.graph is not None else "eager"
     if ts.graph is None:
-        for _ in range(a.warmup):
+        for i in range(a.warmup):
+            wd.beat(i, "warmup")
             ts.step()
+    wd.beat(0, "sync after warmup")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1016,8 +1118,14 @@ def run_train(a, config, rank, world, dev, secondary=False):
     torch.cuda.synchronize()
     ts.ar_timing = True
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
+        wd.beat(i, "timed")
         loss = ts.step()
+        if i % 4 == 3 or i == a.steps - 1:   # (an event every few steps: where a hang stopped)
+            ev = torch.cuda.Event()
+            ev.record()
+            wd.mark(ev)
+    wd.beat(a.steps, "sync after timed steps")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1037,10 +1145,17 @@ def run_train(a, config, rank, world, dev, secondary=False):
         prof_steps = max(1, a.prof_steps)
         _lib.prof_reset()
         _lib.prof_enable(True)
-        for _ in range(prof_steps):
+        wd.mode = "eager"
+        for i in range(prof_steps):
+            wd.beat(i, "profiled eager step")
             ts.eager_step()
         torch.cuda.synchronize()
     _lib.prof_enable(False)
+    # graph mode with the collectives captured: the exposed all-reduce from paired replays
+    paired = ts.exposed_collective_ms(wd=wd) if (ts.in_graph and a.graph) else None
+    if paired is not None:
+        allreduce_ms = paired["exposed_ms"]
+    wd.close()
 
     kernels = kernel_table(prof_steps)
     # dominant kernel = the kernel function with the most time in the profiled steps
@@ -1071,8 +1186,10 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "rooflines_top3": top_rooflines(config, B, 3),
         "mlp_mfma_utilisation": gemm_totals(prof_steps),
         "allreduce_ms_per_step": allreduce_ms,
-        "allreduce": (None if world == 1 else
-                      f"{len(buckets.buckets)} buckets behind the backward's gradient marks, inside the HIP graph"
+        "allreduce_exposed_paired_replays": paired,
+        "allreduce": (None if (world == 1 and not ts.rehearse) else
+                      f"{len(buckets.buckets)} buckets behind the backward's gradient marks, inside the HIP graph "
+                      "(exposed ms = paired replays with / without the buckets)"
                       if ts.in_graph else
                       f"{len(buckets.buckets)} buckets after each graph replay (exposed ms above)"
                       if (buckets is not None and a.graph) else

@@ -100,6 +100,7 @@ SIGNATURES = {
     "spnerf_grad_marks": (c_int32, [POINTER(ModelCfg), POINTER(c_int32), c_int32]),
     "spnerf_grad_marks_arm": (c_int32, [c_int32]),
     "spnerf_grad_mark_wait": (c_int32, [c_int32, c_void_p]),
+    "spnerf_grad_mark_query": (c_int32, [c_int32]),
 }
 
 _lib = None
@@ -184,6 +185,14 @@ def grad_marks(cfg: ModelCfg, n_params: int):
 
 def grad_marks_arm(on: bool) -> None:
     check(lib().spnerf_grad_marks_arm(1 if on else 0), "grad_marks_arm")
+
+
+def grad_mark_query(mark: int) -> bool:
+    """Has the latest record of gradient mark ``mark`` completed? (spnerf_grad_mark_query)"""
+    r = lib().spnerf_grad_mark_query(int(mark))
+    if r < 0:
+        check(r, "grad_mark_query")
+    return r == 1
 
 
 def grad_mark_wait(mark: int, stream) -> None:

@@ -22,8 +22,10 @@ struct GatherArgs {
 };
 
 // blockIdx.y = field; a thread copies one word of one row (rows in order, words of a row
-// adjacent, so a wave's loads and stores are contiguous runs of rows); an index outside the
-// source rows leaves its destination row untouched
+// adjacent, so a wave's loads and stores are contiguous runs of rows).  An index outside the source
+// rows (torch indexing would raise; the launch cannot without a host sync) POISONS its destination
+// row with all-one bits — NaN in a float field, -1 in an integer one — so a sampler or offset bug
+// shows up as a non-finite loss at once instead of training on the previous batch's rows
 __global__ __launch_bounds__(256) void k_gather_rows(GatherArgs g) {
     const int f = blockIdx.y;
     const int wpr = g.words[f];
@@ -32,8 +34,7 @@ __global__ __launch_bounds__(256) void k_gather_rows(GatherArgs g) {
     const int64_t row = t / wpr;
     const int w = (int)(t - row * wpr);
     const int64_t r = g.idx[row];
-    if (r < 0 || r >= g.src_rows[f]) return;
-    g.dst[f][row * wpr + w] = g.src[f][r * wpr + w];
+    g.dst[f][row * wpr + w] = (r < 0 || r >= g.src_rows[f]) ? 0xFFFFFFFFu : g.src[f][r * wpr + w];
 }
 
 }  // namespace spn

@@ -40,6 +40,14 @@ void set_error(const char* fmt, ...);
 // compute units of the current device (hipDeviceProp_t::multiProcessorCount, cached per device):
 // the resident grid of the persistent kernels
 int num_cus();
+// CU count the weight-gradient split counts are sized for: the workspace layout sizes its slabs
+// for kLayoutCus (a pure function of the model dimensions, whatever device is current), and a
+// launch never uses more splits than that (split_cus: the device's CUs, capped at kLayoutCus)
+constexpr int kLayoutCus = 256;
+inline int split_cus() {
+    const int n = num_cus();
+    return n < kLayoutCus ? n : kLayoutCus;
+}
 
 // option prof_shapes: each launch's class is keyed by its FLOP count too ("class#<MFLOP>"), so
 // the in-library timer separates the launch shapes of one kernel function

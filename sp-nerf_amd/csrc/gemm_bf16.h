@@ -79,6 +79,7 @@ extern int g_nt16_ip, g_tn16_ip, g_nt16_ip_gen;
 extern int g_tn16_bias_split;  // option tn_bf16_bias_split
 extern int g_tn16_k64;         // option tn_bf16_k64: the narrow kernel for N = 512, K = 64 weight gradients
 extern int g_tn16_quad;        // option tn_bf16_quad: the quad-wave 128x128-per-wave DMA weight-gradient kernel
+extern int g_tn16_m16;         // option tn_bf16_m16: the 16x16x32 weight-gradient kernel (1: 4 stages, 2: 5)
 extern int g_tn16_pf;          // option tn_bf16_pf: prefetched LDS fragments in the DMA weight-gradient GEMM
 extern int g_tn16_few_tiles;   // option tn_bf16_few_tiles  // DMA kernels: issue placement of the next K-step (options nt_bf16_ip, tn_bf16_ip)
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant = -1);
@@ -89,7 +90,8 @@ extern int g_tn16_variant;
 extern int g_tn16_rounds;      // option tn_bf16_rounds: wide weight-gradient blocks per CU (1 or 2)
 extern int g_tn16_min_points;  // fewest points per split (option "tn_bf16_min_points")
 // few: the tn_bf16_few_tiles choice (-1: the option; the workspace layout takes the larger, 1)
-int tn_splits_bf16(int P, int N, int K, int variant = -1, int few = -1);
+// cus: the CU count to size for (-1: split_cus(); the workspace layout passes kLayoutCus)
+int tn_splits_bf16(int P, int N, int K, int variant = -1, int few = -1, int cus = -1);
 int32_t gemm_tn_bf16(const TN16Args& a, int splits, hipStream_t s);
 
 // Up to kTnGroup weight-gradient GEMMs (each its own operands, shape and slabs) in ONE launch

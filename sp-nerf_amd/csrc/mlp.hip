@@ -1203,6 +1203,7 @@ int g_tn_group = 9;
 // would otherwise take ≥ 64 K points (C4 at 4 096 rays: 26.29 / 26.32 -> 26.25 / 26.26 ms), else 1
 // (at 512 rays 2 rounds measured 3.976 / 3.977 against 3.963 / 3.964 ms)
 int g_tn_group_rounds = 0;
+int g_tn_group_last = 0;   // option "tn_group_last" (bench.py sets 2 when N > 1): the last group's size cap
 // option "defer_heads": under deferred trunk weight gradients the output heads' G / Q weight
 // gradients run in trunk_wgrad too (one GEMM over every pass's points, inside the group launch)
 // — 1 always, 0 never, 2 (default) for passes of at most 2^18 points: C4 at 512 rays 3.970 / 3.973
@@ -1409,7 +1410,7 @@ static bool pe_inline_on(const Ctx& c, bool save) { return g_pe_inline && trunk_
 
 static bool trunk_l0_on(const Ctx& c, bool save) {
     return fused_trunk_on(c) && g_l0_split && (g_trunk_l0 == 2 || (g_trunk_l0 == 1 && !save)) && c.k.Wf16[0] >= 0 &&
-           trunk_l0_supported(c.d.K0p, save);
+           trunk_l0_supported(c.d.K0p, save, c.d.bf && g_zsave);
 }
 
 // the fused heads' arguments and counted work (k_heads_bf16, or inside the inference trunk)
@@ -2107,7 +2108,12 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
                                c.k.Kp[0] == d.K0p;
         bool tail_pending = false;
         for (size_t g0 = 0; g0 < items.size();) {
-            const size_t g1 = std::min(items.size(), g0 + (size_t)std::min(g_tn_group, kTnGroup));
+            size_t g1 = std::min(items.size(), g0 + (size_t)std::min(g_tn_group, kTnGroup));
+            // option tn_group_last: the final group at most that many GEMMs (the ones before it one
+            // launch more), so the marks of all but the lowest layers fire a group earlier and their
+            // all-reduce overlaps the last group (data parallelism: a smaller exposed last bucket)
+            if (g_tn_group_last > 0 && g1 == items.size() && g1 - g0 > (size_t)g_tn_group_last)
+                g1 = items.size() - (size_t)g_tn_group_last;
             // one split count per point: GEMM q takes sp · P_q / Pt splits, rounds x the CUs' worth
             // of blocks, within the workspace's slab capacity
             double tiles = 0, nk = 0, nn = 0;
@@ -2117,10 +2123,10 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
                 nk += w * items[q].t.N * items[q].t.K;
                 nn += w * items[q].t.N;
             }
-            const int64_t sp1 = std::max<int64_t>(1, (int64_t)(num_cus() / tiles));
+            const int64_t sp1 = std::max<int64_t>(1, (int64_t)(split_cus() / tiles));
             const int rounds = g_tn_group_rounds > 0 ? std::min(g_tn_group_rounds, kTnGroupRounds)
                                                      : (Pt / sp1 >= 65536 ? 2 : 1);
-            const int64_t sp = std::max<int64_t>(1, std::min({(int64_t)(rounds * num_cus() / tiles), (int64_t)cdiv(Pt, g_tn16_min_points),
+            const int64_t sp = std::max<int64_t>(1, std::min({(int64_t)(rounds * split_cus() / tiles), (int64_t)cdiv(Pt, g_tn16_min_points),
                                                              (int64_t)(c.w.slab_n / nk), (int64_t)(c.w.slab_b_n / nn)}));
             TN16Args t[kTnGroup];
             int spl[kTnGroup];
@@ -2368,8 +2374,10 @@ static int* option_slot(const char* name) {
     if (n == "pack_table") return &g_pack_table;
     if (n == "tn_bf16_pf") return &g_tn16_pf;
     if (n == "tn_bf16_quad") return &g_tn16_quad;
+    if (n == "tn_bf16_m16") return &g_tn16_m16;
     if (n == "tn_bf16_rounds") return &g_tn16_rounds;
     if (n == "tn_group_rounds") return &g_tn_group_rounds;
+    if (n == "tn_group_last") return &g_tn_group_last;
     if (n == "defer_heads") return &g_defer_heads;
     if (n == "tn_k64_pair") return &g_tn_k64_pair;
     if (n == "heads_epi") return &g_heads_epi;
@@ -2458,6 +2466,16 @@ extern "C" int32_t spnerf_grad_mark_wait(int32_t mark, void* stream) {
     SPN_ARG(m && mark >= 0 && mark < 64, "spnerf_grad_mark_wait: bad mark");
     SPN_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), m->ev[mark], 0));
     return SPNERF_OK;
+}
+
+extern "C" int32_t spnerf_grad_mark_query(int32_t mark) {
+    Marks* m = marks_of_device();
+    SPN_ARG(m && mark >= 0 && mark < 64, "spnerf_grad_mark_query: bad mark");
+    const hipError_t e = hipEventQuery(m->ev[mark]);
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    SPN_HIP(e);
+    return 0;
 }
 
 extern "C" int32_t spnerf_param_count(const spnerf_model_cfg* cfg) {

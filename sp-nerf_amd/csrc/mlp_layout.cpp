@@ -232,7 +232,8 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         int64_t slab = 0, slab_b = 0;
         auto need = [&](int N, int K) {
             // bf16: either TN tiling may run (tn_bf16_variant can change after the layout is made)
-            const int sp = d.bf ? std::max(tn_splits_bf16((int)P, N, K, 1), tn_splits_bf16((int)P, N, K, 2, 1))
+            const int sp = d.bf ? std::max(tn_splits_bf16((int)P, N, K, 1, -1, kLayoutCus),
+                                           tn_splits_bf16((int)P, N, K, 2, 1, kLayoutCus))
                                 : tn_splits((int)P, N, K);
             slab = std::max(slab, (int64_t)sp * N * K);
             slab_b = std::max(slab_b, (int64_t)sp * N);
@@ -243,9 +244,9 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         need(H, H);
         if (d.bf && d.W % 256 == 0) {
             // grouped weight gradients (mlp.hip trunk_wgrad, option tn_group): up to
-            // kTnGroupRounds x num_cus() 256 x 256 blocks of the DMA kernel, each its own slab tile,
+            // kTnGroupRounds x kLayoutCus 256 x 256 blocks of the DMA kernel, each its own slab tile,
             // over both passes' points (at most 2P here; trunk_wgrad clamps to this capacity)
-            const int64_t blocks = std::min<int64_t>((int64_t)kTnGroupRounds * num_cus(),
+            const int64_t blocks = std::min<int64_t>((int64_t)kTnGroupRounds * kLayoutCus,
                                                      (int64_t)kTnGroup * 4 * ((2 * P + 1023) / 1024));
             slab = std::max(slab, blocks * 256 * 256);
             slab_b = std::max(slab_b, blocks * 256);

@@ -195,7 +195,7 @@ extern int g_trunk_dreg;   // 64-point training tiles: D stored from the registe
 extern int g_trunk_nt;     // 1 = trunk H stores non-temporal, 2 = fused heads' H loads non-temporal, 4 = training D stores
 bool trunk_bf16_supported(int W, int L, int skip, int K0p);
 // layer 0 inside the launch (TrunkArgs::X0) for this PE width when saving / not saving
-bool trunk_l0_supported(int K0p, bool save);
+bool trunk_l0_supported(int K0p, bool save, bool zround = false);  // zround: the zsave (64-point) tiling
 int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes);
 // the launch trunk_bf16 would make for a (saving) computes the σ rows (TrunkArgs::sig_hsave)
 bool trunk_sigma_ok(const TrunkArgs& a, bool save);

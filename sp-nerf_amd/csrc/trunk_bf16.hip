@@ -873,8 +873,10 @@ bool trunk_bf16_supported(int W, int L, int skip, int K0p) {
 // (pairs in one call; the 64-point tiling halves the points each weight byte from L2 serves)
 static int trunk_tile(bool save) { return g_trunk_tile ? g_trunk_tile : 128; }
 
-bool trunk_l0_supported(int K0p, bool save) {
-    const int tpd = trunk_tile(save) == 64 ? TrunkGeo<64>::TPD : TrunkGeo<128>::TPD;
+bool trunk_l0_supported(int K0p, bool save, bool zround) {
+    // the tiling trunk_bf16 runs: the fp16-Z (zsave) path exists on 64-point tiles only
+    const int tm = zround ? 64 : trunk_tile(save);
+    const int tpd = tm == 64 ? TrunkGeo<64>::TPD : TrunkGeo<128>::TPD;
     return K0p % 4 == 0 && (K0p / 4) % tpd == 0;  // layer 0's k-loop in whole prefetch rounds
 }
 
@@ -928,7 +930,7 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
             "trunk_bf16: inline encoding needs z, rs, and when saving the X0b output");
     if (!a.X0b_out && trunk2_supported(a, save)) return trunk2_bf16(a, s, save, flop, bytes);
     const int tm = a.zround ? 64 : trunk_tile(save);  // the 128-point tiling has no fp16-Z path
-    SPN_ARG(!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, save)), "trunk_bf16: layer 0 unsupported for K0p=%d",
+    SPN_ARG(!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, save, a.zround != 0)), "trunk_bf16: layer 0 unsupported for K0p=%d",
             a.K0p);
     TrunkArgs ad = a;
     ad.dbg = g_trunk_dbg;

@@ -48,6 +48,86 @@ def init_from_env(backend: str = "nccl", device=None):
     return rank, local, world
 
 
+def step_deadline_seconds() -> float:
+    """Host-side deadline of one step of a timed loop: SPNERF_STEP_DEADLINE seconds (default 120;
+    0 = off).  A C4 step is tens of milliseconds, so a step still running after minutes is a hang."""
+    return float(os.environ.get("SPNERF_STEP_DEADLINE", "120"))
+
+
+class StepWatchdog:
+    """Make a hung step end the process with a diagnosis instead of blocking until the driver's
+    limit.  The loop calls ``beat(step, phase)`` before each step and ``mark(event)`` after it
+    (an optional CUDA event recorded behind the step's work); a daemon thread checks once a
+    second, and when no beat came for ``deadline`` seconds it prints ONE JSON line (rank, step,
+    phase, mode, seconds since the beat, the last step whose event had completed, and the
+    optional ``probe()`` dict, e.g. which gradient buckets' marks had fired) to stdout and stderr
+    and calls ``os._exit(code)`` — a non-zero exit of THIS process (never a re-exec), which
+    torchrun turns into the job's failure.  The GIL is released while the main thread blocks in
+    a device synchronize or a collective, so the thread runs then."""
+
+    def __init__(self, rank: int = 0, mode: str = "", deadline: float | None = None, code: int = 3, probe=None,
+                 poll: float = 1.0):
+        import threading
+        self.rank, self.mode, self.code, self.probe, self.poll = rank, mode, code, probe, poll
+        self.deadline = step_deadline_seconds() if deadline is None else float(deadline)
+        self.step, self.phase = -1, "start"
+        self.events = []       # (step, event) of the steps marked so far (the last few)
+        self._t = None
+        self._stop = threading.Event()
+        self._last = None
+        if self.deadline > 0:
+            import time
+            self._last = time.monotonic()
+            self._t = threading.Thread(target=self._run, name="spnerf-step-watchdog", daemon=True)
+            self._t.start()
+
+    def beat(self, step: int, phase: str) -> None:
+        import time
+        self.step, self.phase = step, phase
+        self._last = time.monotonic()
+
+    def mark(self, event) -> None:
+        self.events = (self.events + [(self.step, event)])[-4:]
+
+    def _completed(self):
+        done = None
+        for st, ev in list(self.events):
+            try:
+                if ev.query():
+                    done = st
+            except Exception:   # a faulted device: the query itself fails
+                return "query failed"
+        return done
+
+    def diagnosis(self) -> dict:
+        import time
+        d = {"watchdog": "step deadline exceeded", "rank": self.rank, "step": self.step, "phase": self.phase,
+             "mode": self.mode, "seconds_since_beat": round(time.monotonic() - self._last, 1),
+             "deadline_s": self.deadline, "last_completed_step": self._completed()}
+        if self.probe is not None:
+            try:
+                d.update(self.probe())
+            except Exception as e:   # the diagnosis must not fail
+                d["probe_error"] = f"{type(e).__name__}: {e}"
+        return d
+
+    def _run(self):
+        import json
+        import sys
+        import time
+        while not self._stop.wait(self.poll):
+            if time.monotonic() - self._last > self.deadline:
+                line = json.dumps(self.diagnosis())
+                print(line, flush=True)
+                print(line, file=sys.stderr, flush=True)
+                os._exit(self.code)
+
+    def close(self) -> None:
+        self._stop.set()
+        if self._t is not None:
+            self._t.join(timeout=2 * self.poll + 1)
+
+
 class SharedSeedSampler:
     """Every rank draws the same permutation of the N training rays per epoch (uniform
     shuffle, main.py:108-115) and takes rows [rank·b, (rank+1)·b) of each global batch."""

@@ -85,8 +85,11 @@ class PhiloxRandom:
         self._host_step = -1   # host mirror of the device step (eager renders only; see _gen)
 
     def begin_render(self, device):
-        if self._state is None or self._state.device != torch.device(device):
+        if self._state is None:
             self._state = torch.tensor([self.seed, self._host_step], dtype=torch.int64, device=device)
+        elif self._state.device != torch.device(device):
+            # moved with its DEVICE step: graph replays advance that one, not the host mirror
+            self._state = self._state.to(device)
         self._state[1:].add_(1)
         self._host_step += 1
         self._snap = self._state.clone()
@@ -98,9 +101,17 @@ class PhiloxRandom:
         if self._state is not None:
             self._state[1].fill_(int(step))
 
+    def sync_host_step(self) -> int:
+        """Re-read the host mirror of the step from the device state (a host sync).  The mirror
+        only follows eager renders: replays of a captured graph advance the device step alone."""
+        if self._state is not None:
+            self._host_step = int(self._state[1].item())
+        return self._host_step
+
     def copy_state_from(self, other: "PhiloxRandom") -> None:
-        """Continue from ``other``'s step (same draws from the next render on)."""
-        self._host_step = other._host_step
+        """Continue from ``other``'s step (same draws from the next render on), its device step
+        included (``other`` may have been advanced by graph replays)."""
+        self._host_step = other.sync_host_step()
         self._state = None if other._state is None else other._state.clone()
 
     def key(self, device, nslots: int = 1):
@@ -117,6 +128,8 @@ class PhiloxRandom:
     # mirror (no device read, so no sync); these fallbacks cannot be captured into a HIP graph
     # (a replay would not advance the mirror and torch generators are host state).
     def _gen(self, device):
+        if self._state is not None and not torch.cuda.is_current_stream_capturing():
+            self.sync_host_step()   # (graph replays may have moved the device step on)
         g = torch.Generator(device=device)
         g.manual_seed(_mix64(self.seed, max(self._host_step, 0), self._slot) & ((1 << 63) - 1))
         self._slot += 1

@@ -200,3 +200,58 @@ def test_shard_ce_handles_a_shard_without_labels():
     assert torch.is_tensor(dp.ce_scale(labels[:10], labels, 4))
     assert torch.isfinite(parts[0]) and float(parts[0]) == 0.0
     np.testing.assert_allclose(float(sum(parts) / 4), float(glob), rtol=1e-6)
+
+
+_STALL_SCRIPT = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["SPN_ROOT"])
+import torch, torch.distributed as dist
+from spnerf_amd import dp
+r, _, w = dp.init_from_env("gloo")
+wd = dp.StepWatchdog(rank=r, mode="test", deadline=3.0, poll=0.2,
+                     probe=lambda: {"buckets_done": [0, 1]})
+x = torch.ones(4)
+for step in range(6):
+    wd.beat(step, "timed")
+    if r == 1 and step == 2:
+        time.sleep(60)          # the injected stall: rank 0 waits in the collective
+    dist.all_reduce(x)
+wd.close()
+print("finished", flush=True)
+"""
+
+
+def test_step_watchdog_ends_a_stalled_rank_with_a_diagnosis():
+    """A rank that stalls mid-loop (and the rank blocked in the collective behind it) exits
+    non-zero within the step deadline, printing one JSON diagnosis (rank, step, phase) instead of
+    hanging until the process group's timeout (dp.StepWatchdog, used by bench.py's loops)."""
+    import json
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _free_port()
+    procs = []
+    t0 = time.monotonic()
+    for r in range(2):
+        env = dict(os.environ, SPN_ROOT=root, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE="2", LOCAL_RANK=str(r), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, "-c", _STALL_SCRIPT], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=45)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("the watchdog did not end the stalled job")
+        outs.append((p.returncode, o, e))
+    assert time.monotonic() - t0 < 40
+    for r, (code, o, e) in enumerate(outs):
+        assert code == 3, (r, code, o, e[-2000:])
+        line = [ln for ln in o.splitlines() if ln.startswith("{")][-1]
+        d = json.loads(line)
+        assert d["watchdog"] == "step deadline exceeded" and d["rank"] == r and d["step"] == 2, d
+        assert d["phase"] == "timed" and d["buckets_done"] == [0, 1] and d["seconds_since_beat"] >= 3.0
+        assert "finished" not in o

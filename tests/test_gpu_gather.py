@@ -40,3 +40,24 @@ def test_gather_rows_matches_torch_indexing(n_src, B):
 def test_gather_rows_rejects_unaligned_rows():
     with pytest.raises(ValueError):
         dp.BatchGather({"flags": torch.zeros(16, 2, dtype=torch.uint8, device=DEV)}, 4)
+
+
+def test_gather_rows_poisons_out_of_range_indices():
+    """An index outside the source rows (-1, n) poisons its destination row with all-one bits
+    (NaN in float fields, -1 in integer ones) — a sampler bug surfaces as a non-finite loss —
+    while the in-range rows are exact copies."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    f = _fields(100, g)
+    gather = dp.BatchGather(f, 6)
+    gather(torch.arange(6, device=DEV))          # rows a stale batch would leave behind
+    idx = torch.tensor([5, -1, 7, 100, 0, 99], device=DEV)
+    out = gather(idx)
+    torch.cuda.synchronize()
+    bad = torch.tensor([1, 3], device=DEV)
+    good = torch.tensor([0, 2, 4, 5], device=DEV)
+    for k, t in f.items():
+        assert torch.equal(out[k][good], t[idx[good]]), k
+        if t.dtype.is_floating_point:
+            assert torch.isnan(out[k][bad]).all(), k
+        else:
+            assert (out[k][bad] == -1).all(), k

@@ -296,6 +296,38 @@ def test_bf16_tn_quad_wave_grouped_bitwise_equal():
         assert torch.equal(out[0][k], out[1][k]), k
 
 
+@pytest.mark.parametrize("m16", [1, 2, 3, 4])
+@pytest.mark.parametrize("n,ns", [(300, 64), (2048, 64)])
+def test_bf16_tn_m16_agrees(m16, n, ns):
+    """Option tn_bf16_m16: the weight gradients on 16x16x32 MFMAs (32-point blocks per output
+    element; 4 or 5 DMA stages) against the 32x32x16 kernel: renders bit for bit, every gradient
+    within 1e-5 of its largest entry (fp32 sums of the same bf16 products in another grouping)."""
+    r0, g0 = _render_bf16({"tn_bf16_m16": 0}, n=n, ns=ns)
+    r1, g1 = _render_bf16({"tn_bf16_m16": m16}, n=n, ns=ns)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        err = (g0[k] - g1[k]).abs().max().item() / max(g0[k].abs().max().item(), 1e-30)
+        assert err <= 1e-5, (k, err)
+
+
+def test_bf16_tn_m16_grouped_agrees():
+    from test_gpu_flatgrad import _deferred_grads
+    old = _lib.get_option("tn_bf16_m16")
+    out = []
+    try:
+        for m in (0, 1, 3):
+            _lib.set_option("tn_bf16_m16", m)
+            out.append(_deferred_grads(9, n_rays=256)[0])
+    finally:
+        _lib.set_option("tn_bf16_m16", old)
+    for o in out[1:]:
+        for k in out[0]:
+            err = (out[0][k] - o[k]).abs().max().item() / max(out[0][k].abs().max().item(), 1e-30)
+            assert err <= 1e-5, (k, err)
+
+
 def test_pack_table_bitwise_equal():
     """Option pack_table: the weight re-pack from a device-resident piece table (one launch)
     writes the same packed buffer as the kernarg-table launches (two for the bf16 MLP)."""

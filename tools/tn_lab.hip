@@ -111,7 +111,17 @@ int main(int argc, char** argv) {
         memcpy(&u, &x, 4);
         return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
     };
-    for (auto& v : a) v = rnd();
+    // TN_ASCALE: scale of A (the bench's A is a gradient dZ, orders of magnitude below B = H)
+    const float ascale = getenv("TN_ASCALE") ? (float)atof(getenv("TN_ASCALE")) : 1.f;
+    for (auto& v : a) {
+        const uint16_t r = rnd();
+        uint32_t u = (uint32_t)r << 16;
+        float x;
+        memcpy(&x, &u, 4);
+        x *= ascale;
+        memcpy(&u, &x, 4);
+        v = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
     for (auto& v : b) v = rnd();
     for (int p = 0; p < P; ++p) {
         for (int f = 0; f < N; ++f) ai[((size_t)(p / 8) * N + f) * 8 + p % 8] = a[(size_t)p * N + f];
@@ -147,15 +157,17 @@ int main(int argc, char** argv) {
     };
     const double flop = 2.0 * P * N * K, bytes = 2.0 * P * (N + K);
     // profiling mode (argv[3]): one configuration only, for PMC passes — 1 DMA one-row, 2 quad
-    // one-row, 3 DMA, 4 quad, 5 prefetched one-row
+    // one-row, 3 DMA, 4 quad, 5 prefetched one-row, 6 16x16x32 one-row, 7 16x16x32
     const int mode = argc > 3 ? atoi(argv[3]) : 0;
     if (mode) {
         TN16Args t;
-        t.A = dA; t.lda = (mode == 1 || mode == 2 || mode == 5) ? 0 : N; t.B = dB; t.ldb = t.lda ? K : 0; t.K1 = K;
+        t.A = dA; t.lda = (mode == 1 || mode == 2 || mode == 5 || mode == 6) ? 0 : N; t.B = dB; t.ldb = t.lda ? K : 0; t.K1 = K;
         t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K; t.slab_b = slab_b;
         t.P = P; t.N = N; t.K = K;
         g_tn16_quad = mode == 2 || mode == 4;
         g_tn16_pf = mode == 5;
+        g_tn16_m16 = mode == 6 || mode == 7 ? 1 : 0;
+        if (mode == 7) { t.lda = N; t.ldb = K; }
         const double u = timeit([&] { gemm_tn_bf16(t, splits, 0); });
         printf("mode %d: %8.1f us  %7.1f TF/s\n", mode, u, flop / u * 1e-6);
         return 0;
@@ -191,6 +203,38 @@ int main(int argc, char** argv) {
         printf("  ... %3d splits: %8.1f us  %7.1f TF/s\n", 2 * splits, u2, flop / u2 * 1e-6);
         g_tn16_pf = 0;
         g_tn16_quad = 0;
+    }
+    for (int m16 : {1, 2, 3, 4}) {   // option tn_bf16_m16: 16x16x32 kernels (1/2: 8 waves, 3/4: 16 waves; 4 / 5 DMA stages)
+        g_tn16_m16 = m16;
+        const double up = timeit([&] { gemm_tn_bf16(t, splits, 0); });
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, got);
+        std::vector<float> hr((size_t)N * K), hg(hr.size()), br((size_t)N), bg((size_t)N);
+        CK(hipMemcpy(hr.data(), ref, hr.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hg.data(), got, hg.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0, mx = 0;
+        for (size_t i = 0; i < hr.size(); ++i) {
+            md = fmax(md, fabs((double)hr[i] - hg[i]));
+            mx = fmax(mx, fabs((double)hr[i]));
+        }
+        // bias sums of split 0 against the 32x32x16 kernel's (same row order: bitwise)
+        CK(hipMemcpy(bg.data(), slab_b, bg.size() * 4, hipMemcpyDeviceToHost));
+        g_tn16_m16 = 0;
+        gemm_tn_bf16(t, splits, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(br.data(), slab_b, br.size() * 4, hipMemcpyDeviceToHost));
+        g_tn16_m16 = m16;
+        printf("16x16x32 TN m16=%d, %d stages: %8.1f us  %7.1f TF/s  %6.2f TB/s  max|diff|/max|ref| %.2e  bias %s\n", m16, m16 % 2 == 0 ? 5 : 4,
+               up, flop / up * 1e-6, bytes / up * 1e-6, md / mx,
+               memcmp(br.data(), bg.data(), br.size() * 4) == 0 ? "bitwise" : "DIFFERENT");
+        TN16Args t0 = t;
+        t0.lda = 0;
+        t0.ldb = 0;
+        const double u0 = timeit([&] { gemm_tn_bf16(t0, splits, 0); });
+        printf("  ... one row (on-chip): %8.1f us  %7.1f TF/s\n", u0, flop / u0 * 1e-6);
+        const double u2 = timeit([&] { gemm_tn_bf16(t, 2 * splits, 0); });
+        printf("  ... %3d splits: %8.1f us  %7.1f TF/s\n", 2 * splits, u2, flop / u2 * 1e-6);
+        g_tn16_m16 = 0;
     }
     {   // the register-staged 256x256 kernel (tn_bf16_variant 2), normal and one-row operands
         g_tn16_variant = 2;
