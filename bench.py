@@ -492,9 +492,10 @@ def roofline_of(dom, nt, traffic=None, traffic_src=None):
     kernel without MFMAs is HBM-bound.  Both fractions are reported; ``frac`` is the binding one."""
     if dom in GEMM_CLASSES:
         dom_name, peak = GEMM_CLASSES[dom]
-        if "<IP>" in dom_name:   # the template instance the library launches under the current option
-            dom_name = dom_name.replace("<IP>", f"<{_lib.get_option('tn_bf16_ip')}, "
-                                                f"{'true' if _lib.get_option('tn_bf16_pf') == 1 else 'false'}>")
+        if "<IP>" in dom_name:   # the template instance the library launches (product build: <1, false>)
+            ip = _lib.get_option("tn_bf16_ip") if _lib.has_option("tn_bf16_ip") else 1
+            pf = _lib.has_option("tn_bf16_pf") and _lib.get_option("tn_bf16_pf") == 1
+            dom_name = dom_name.replace("<IP>", f"<{ip}, {'true' if pf else 'false'}>")
     else:
         dom_name, peak = HBM_CLASSES.get(dom, dom), None
     secs = nt["ms"] * 1e-3

@@ -149,12 +149,26 @@ def require_device(*tensors) -> None:
                               f"{t.device}. Move rays / models to the GPU.")
 
 
+class OptionUnavailable(SpnerfError):
+    """A kernel switch the loaded library does not have: the A/B switches of kernels measured
+    slower than the defaults exist only in a -DSPN_ABLATIONS build."""
+
+
+def has_option(name: str) -> bool:
+    v = ctypes.c_int32()
+    return lib().spnerf_get_option(name.encode(), ctypes.byref(v)) == 0
+
+
 def set_option(name: str, value: int) -> None:
     """Kernel-selection switch (spnerf_set_option): "fused_trunk", "nt_f32_variant", ..."""
+    if not has_option(name):
+        raise OptionUnavailable(f"set_option: the library has no option {name!r} (ablation build only?)")
     check(lib().spnerf_set_option(name.encode(), int(value)), f"set_option({name})")
 
 
 def get_option(name: str) -> int:
+    if not has_option(name):
+        raise OptionUnavailable(f"get_option: the library has no option {name!r} (ablation build only?)")
     v = ctypes.c_int32()
     check(lib().spnerf_get_option(name.encode(), ctypes.byref(v)), f"get_option({name})")
     return v.value

@@ -1663,6 +1663,10 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     }
 }
 
+#ifdef SPN_ABLATIONS
+// Weight-gradient kernels measured slower than k_gemm_tn_bf16d in the C4 step: the
+// 16x16x32 pipelined kernels (8 and 16 waves) and the quad-wave kernel — compiled only into
+// -DSPN_ABLATIONS builds (tools/tn_lab, the A/B variant libraries).
 // Weight gradients on v_mfma_f32_16x16x32_bf16 (option tn_bf16_m16): k_gemm_tn_bf16d's 256 x 256
 // block tile, 32-point LDS-DMA stages and bias sums, but a wave's 128 x 64 is 8 x 4 accumulators
 // of 16 x 16 and one stage is exactly one 32-point k-step.  The same LDS bytes per FLOP as the
@@ -2364,6 +2368,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_bf16q(TN16Group G) {
         }
     }
 }
+#endif  // SPN_ABLATIONS
 
 // ------------------------------------------------------------------------------------------
 // host
@@ -2424,6 +2429,12 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
         const dim3 grid(std::min(nt, num_cus())), block(512);
         if (dm) {
             const bool z = a.dmul_z != 0;   // zsave: Dmul holds Z
+#ifndef SPN_ABLATIONS
+            // product build: the default issue placement (2) and no saved-Z (zsave) epilogue
+            SPN_ARG(!z, "gemm_nt_bf16: a saved-Z Dmul (zsave) needs the ablation build");
+            (void)ip;
+            hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 0>), grid, block, 0, s, a, nt);
+#else
             if (ip == 2) {
                 if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 1>), grid, block, 0, s, a, nt);
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 0>), grid, block, 0, s, a, nt);
@@ -2434,6 +2445,7 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
                 if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 0, 1>), grid, block, 0, s, a, nt);
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 0, 0>), grid, block, 0, s, a, nt);
             }
+#endif
         } else {
             // the epilogue's inputs as a compile-time variant (see k_gemm_nt_bf16d); option
             // nt_bf16_epi 0 forces the generic one
@@ -2445,7 +2457,11 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
                 else if (!a.Dmul && !a.r1_a && a.rowbias && a.rows_per_ray % 32 == 0) ev = 2;
                 else if (a.Dmul && a.r1_a && !a.rowbias && a.act == 0 && !a.Dout) ev = 3;
             }
+#ifdef SPN_ABLATIONS
             const bool ip2 = g_nt16_ip_gen == 2;
+#else
+            constexpr bool ip2 = true;   // product build: the default issue placement only
+#endif
             if (a.hd.n > 0) {
                 SPN_ARG((ev == 1 || ev == 2) && ip2 && a.hd.n <= kNTHeads && a.hd.out && a.hd.hsave && a.N % 256 == 0,
                         "gemm_nt_bf16: output heads need the bias / per-ray-row DMA epilogue");
@@ -2456,16 +2472,24 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 2, true>), grid, block, 0, s, a, nt);
             } else if (ev == 1) {
                 if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 1>), grid, block, 0, s, a, nt);
+#ifdef SPN_ABLATIONS
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 1>), grid, block, 0, s, a, nt);
+#endif
             } else if (ev == 2) {
                 if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 2>), grid, block, 0, s, a, nt);
+#ifdef SPN_ABLATIONS
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 2>), grid, block, 0, s, a, nt);
+#endif
             } else if (ev == 3) {
                 if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 3>), grid, block, 0, s, a, nt);
+#ifdef SPN_ABLATIONS
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 3>), grid, block, 0, s, a, nt);
+#endif
             } else {
                 if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 0>), grid, block, 0, s, a, nt);
+#ifdef SPN_ABLATIONS
                 else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 0>), grid, block, 0, s, a, nt);
+#endif
             }
         }
         SPN_HIP(hipGetLastError());
@@ -2538,6 +2562,7 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
         G.start[i + 1] = G.start[i] + blocks[i];
     }
     const dim3 grid(G.start[n]), block(512);
+#ifdef SPN_ABLATIONS
     if (g_tn16_m16 >= 3) {
         if (g_tn16_m16 == 4) hipLaunchKernelGGL(k_gemm_tn_bf16x<5>, grid, dim3(1024), 0, s, G);
         else hipLaunchKernelGGL(k_gemm_tn_bf16x<4>, grid, dim3(1024), 0, s, G);
@@ -2556,9 +2581,18 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
         hipLaunchKernelGGL((k_gemm_tn_bf16d<1, true>), grid, block, 0, s, G);
         return;
     }
-    if (ip == 2) hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, grid, block, 0, s, G);
-    else if (ip == 1) hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, grid, block, 0, s, G);
-    else hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, grid, block, 0, s, G);
+    if (ip == 2) {
+        hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, grid, block, 0, s, G);
+        return;
+    }
+    if (ip == 0) {
+        hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, grid, block, 0, s, G);
+        return;
+    }
+#else
+    (void)ip;   // the product build: IP = 1 (the default placement), no variant kernels
+#endif
+    hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, grid, block, 0, s, G);
 }
 
 bool tn_k64_ok(int N, int K) { return tn_k64(N, K); }

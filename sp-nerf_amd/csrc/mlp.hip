@@ -2348,60 +2348,63 @@ using namespace spn;
 
 static int* option_slot(const char* name) {
     const std::string n(name);
-    if (n == "fused_trunk") return &g_fused_trunk;
-    if (n == "trunk_tile") return &g_trunk_tile;
+    // The product library's switches (at most 15): the default kernels and their one documented
+    // alternate each (INTEGRATION.md §Kernel selection).
+    if (n == "fused_trunk") return &g_fused_trunk;        // 0: layer-by-layer trunk GEMMs
+    if (n == "trunk_tile") return &g_trunk_tile;          // 64 / 128-point training tiles
+    if (n == "trunk_heads") return &g_trunk_heads;        // 0: inference heads in their own launch
+    if (n == "heads_epi") return &g_heads_epi;            // 0: narrow training heads wave-per-point
+    if (n == "trunk_l0") return &g_trunk_l0;              // layer 0 inside the fused trunk (1: inference only)
+    if (n == "pe_inline") return &g_pe_inline;            // 0: k_encode writes the PE rows
+    if (n == "tn_group") return &g_tn_group;              // weight-gradient GEMMs per group launch (1: none)
+    if (n == "tn_group_last") return &g_tn_group_last;    // cap of the last group (bench.py: 2 when N > 1)
+    if (n == "defer_heads") return &g_defer_heads;        // the heads' weight gradients in the group launch
+    if (n == "fused_bwd") return &g_fused_bwd;            // 0: the dX chain layer by layer
+    if (n == "tn_bf16_variant") return &g_tn16_variant;   // 1: 128x128 TN tiles, 2: register-staged 256x256
+    if (n == "tn_bf16_k64") return &g_tn16_k64;           // 0: N = 512, K = 64 weight gradients on 128x128 tiles
+    if (n == "nt_f32_variant") return &g_nt_variant;      // the fp32 (parity) NT GEMM tilings
+    if (n == "pack_table") return &g_pack_table;          // 0: one re-pack launch per parameter group
+    if (n == "prof_shapes") return &g_prof_shapes;        // in-library timer keyed by launch shape
 #ifdef SPN_ABLATIONS
+    // A/B switches of kernels measured slower than the defaults and
     // profiling ablations whose outputs are INVALID: only in a -DSPN_ABLATIONS build
-    // (make variant VDEF=-DSPN_ABLATIONS VLIB=libspnerf_amd_abl.so), never in the product library
+    // (make -C sp-nerf_amd variant VDEF=-DSPN_ABLATIONS VLIB=libspnerf_amd_abl.so)
     if (n == "trunk_dbg") return &g_trunk_dbg;
     if (n == "trunk_var") return &g_trunk_var;
     if (n == "heads_dbg") return &g_heads_dbg;
-#endif
-    if (n == "prof_shapes") return &g_prof_shapes;
     if (n == "trunk_nt") return &g_trunk_nt;
     if (n == "trunk_dreg") return &g_trunk_dreg;
     if (n == "trunk_bwd_dreg") return &g_trunk_bwd_dreg;
     if (n == "trunk_bwd_nt") return &g_trunk_bwd_nt;
     if (n == "trunk_sigma") return &g_trunk_sigma;
-    if (n == "nt_f32_variant") return &g_nt_variant;
     if (n == "tn_f32_variant") return &g_tn_variant;
     if (n == "nt_bf16_variant") return &g_nt16_variant;
     if (n == "nt_bf16_ip") return &g_nt16_ip;
     if (n == "tn_bf16_ip") return &g_tn16_ip;
     if (n == "tn_bf16_bias_split") return &g_tn16_bias_split;
     if (n == "tn_bf16_few_tiles") return &g_tn16_few_tiles;
-    if (n == "tn_group") return &g_tn_group;
-    if (n == "pack_table") return &g_pack_table;
     if (n == "tn_bf16_pf") return &g_tn16_pf;
     if (n == "tn_bf16_quad") return &g_tn16_quad;
     if (n == "tn_bf16_m16") return &g_tn16_m16;
     if (n == "tn_bf16_rounds") return &g_tn16_rounds;
     if (n == "tn_group_rounds") return &g_tn_group_rounds;
-    if (n == "tn_group_last") return &g_tn_group_last;
-    if (n == "defer_heads") return &g_defer_heads;
     if (n == "tn_k64_pair") return &g_tn_k64_pair;
-    if (n == "heads_epi") return &g_heads_epi;
     if (n == "ray_tiles_pair") return &g_ray_tiles_pair;
-    if (n == "tn_bf16_k64") return &g_tn16_k64;
     if (n == "nt_bf16_ip_gen") return &g_nt16_ip_gen;
     if (n == "nt_bf16_epi") return &g_nt16_epi;
     if (n == "grad_marks_flags") return &g_marks_flags;
-    if (n == "tn_bf16_variant") return &g_tn16_variant;
     if (n == "heads_variant") return &g_heads_variant;
     if (n == "l0_split") return &g_l0_split;
-    if (n == "trunk_l0") return &g_trunk_l0;
     if (n == "bwd_streams") return &g_bwd_streams;
     if (n == "tn_bf16_min_points") return &g_tn16_min_points;
     if (n == "fused_heads") return &g_fused_heads;
     if (n == "zsave") return &g_zsave;
-    if (n == "pe_inline") return &g_pe_inline;
     if (n == "tn_split_tail") return &g_tn_split_tail;
-    if (n == "fused_bwd") return &g_fused_bwd;
     if (n == "tile_rowsum") return &g_tile_rowsum;
     if (n == "trunk2") return &g_trunk2;
     if (n == "trunk2_tile") return &g_trunk2_tile;
-    if (n == "trunk_heads") return &g_trunk_heads;
     if (n == "emu_bf16") return &g_emu_bf16;
+#endif
     return nullptr;
 }
 

@@ -34,6 +34,14 @@
 
 namespace spn {
 
+// Measured slower than the one-workgroup k_trunk_bf16 since round 4 (comments below): the kernel is
+// compiled only into -DSPN_ABLATIONS builds; the product build keeps the option variables, and its
+// trunk2_supported / trunk2_heads_ok are false.
+int g_trunk2 = 0;
+int g_trunk2_tile = 128;
+int g_trunk_heads = 2;
+
+#ifdef SPN_ABLATIONS
 #if SPN_TRUNK_KMAJOR
 #error "trunk2_bf16.hip reads the wave-contiguous fragment streams (SPN_TRUNK_KMAJOR 0)"
 #endif
@@ -52,7 +60,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Round 4: 0 is the default again — the one-workgroup k_trunk_bf16<128> is now the faster inference
 // trunk (C5 trunk alone, trunk_heads 0: 15.49 against 16.65 ms per step, one call) and carries the
 // fused heads itself (trunk_heads 2).
-int g_trunk2 = 0;
+// (g_trunk2 is defined at the top of the namespace)
 
 namespace {
 constexpr int TW = 512;
@@ -459,7 +467,7 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(
 // which puts C4's guided pass 1 on the two-workgroup kernel: measured slower than the one-workgroup
 // k_trunk_bf16<128> it otherwise falls back to (0.161 vs 0.145 ms per 512-ray step, 1.17 vs 1.05 at
 // 4 096 rays; same call)
-int g_trunk2_tile = 128;
+// (g_trunk2_tile is defined at the top of the namespace)
 
 static int trunk2_tm(const TrunkArgs& a) {
     if (g_trunk2_tile == 64 || g_trunk2_tile == 128) return g_trunk2_tile;
@@ -511,7 +519,7 @@ int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, d
 // option trunk_heads: a bf16 inference forward runs the fused heads inside its trunk launch (H_L
 // stays in LDS): 2 = in the one-workgroup k_trunk_bf16<128> (trunk_bf16.hip, the default), 1 = in
 // the two-workgroup kernel here; 0 = the trunk, then k_heads_bf16
-int g_trunk_heads = 2;
+// (g_trunk_heads is defined at the top of the namespace)
 
 bool trunk2_heads_ok(const TrunkArgs& a) {
     return g_trunk_heads == 1 && trunk2_tm(a) == 128 && trunk2_supported(a, false);
@@ -541,12 +549,31 @@ int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const Pac
     return SPNERF_OK;
 }
 
+#else   // product build: the two-workgroup trunk is not compiled
+bool trunk2_supported(const TrunkArgs&, bool) { return false; }
+int32_t trunk2_bf16(const TrunkArgs&, hipStream_t, bool, double, double) {
+    SPN_ARG(false, "trunk2_bf16: the two-workgroup trunk is an ablation-build kernel (-DSPN_ABLATIONS)");
+    return SPNERF_OK;
+}
+bool trunk2_heads_ok(const TrunkArgs&) { return false; }
+int32_t trunk2_heads_bf16(const TrunkArgs&, const HeadsFusedArgs&, const PackedOffs&, hipStream_t, double, double) {
+    SPN_ARG(false, "trunk2_heads_bf16: the two-workgroup trunk is an ablation-build kernel (-DSPN_ABLATIONS)");
+    return SPNERF_OK;
+}
+#endif  // SPN_ABLATIONS
+
 }  // namespace spn
 
-// resident workgroups per CU of the 64-point tiling (profiling aid: 2 expected)
+// resident workgroups per CU of the 64-point tiling (profiling aid: 2 expected; -1 in the product
+// build, which does not compile that kernel)
 extern "C" int32_t spnerf_debug_trunk2_occupancy(int32_t save) {
     int n = -1;
+#ifndef SPN_ABLATIONS
+    (void)save;
+    return n;
+#else
     const void* f = save ? (const void*)spn::k_trunk2_bf16<64, false, true, false> : (const void*)spn::k_trunk2_bf16<64, true, false, false>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, spn::T2Geo<64>::NT, 0) != hipSuccess) return -1;
     return n;
+#endif
 }

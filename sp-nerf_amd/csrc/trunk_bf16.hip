@@ -859,8 +859,11 @@ int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double
     ad.dbg = g_trunk_dbg;
     ad.nt = g_trunk_bwd_nt;
     ProfScope prof("trunk_bwd_bf16", s, flop, bytes);
+#ifdef SPN_ABLATIONS
     if (g_trunk_bwd_dreg) hipLaunchKernelGGL(k_trunk_bwd_bf16<true>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else hipLaunchKernelGGL(k_trunk_bwd_bf16<false>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+    else
+#endif
+        hipLaunchKernelGGL(k_trunk_bwd_bf16<false>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
@@ -939,20 +942,30 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     // the saving launches (training) are their own profiling class: their roofline (HBM-heavy,
     // H and D of every layer out) is not the inference launches' (MFMA-bound)
     ProfScope prof(save ? "trunk_bf16_train" : "trunk_bf16", s, flop, bytes);
+    const dim3 grid(std::min(ntiles, num_cus())), block(512);
+    bool done = false;
+#ifdef SPN_ABLATIONS
+    // profiling ablations (outputs invalid) and the measured-slower 64-point tiling without the
+    // register-D epilogue: compiled only into -DSPN_ABLATIONS builds
+    done = true;
     if (tm == 64 && g_trunk_dreg && g_trunk_var == 32)  // ablation: no sin / cos in the epilogue
-        hipLaunchKernelGGL((k_trunk_bf16<64, 544>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+        hipLaunchKernelGGL((k_trunk_bf16<64, 544>), grid, block, 0, s, ad, ntiles);
     else if (tm == 64 && g_trunk_dreg && g_trunk_var == 256)  // ablation: no epilogue at all
-        hipLaunchKernelGGL((k_trunk_bf16<64, 768>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (tm == 64 && g_trunk_dreg) hipLaunchKernelGGL((k_trunk_bf16<64, 512>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (tm == 64) hipLaunchKernelGGL(k_trunk_bf16<64>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 64) hipLaunchKernelGGL((k_trunk_bf16<128, 64>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 128) hipLaunchKernelGGL((k_trunk_bf16<128, 128>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 256) hipLaunchKernelGGL((k_trunk_bf16<128, 256>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (g_trunk_var == 464) hipLaunchKernelGGL((k_trunk_bf16<128, 464>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else if (save) hipLaunchKernelGGL((k_trunk_bf16<128, 2048>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
-    else hipLaunchKernelGGL((k_trunk_bf16<128, 0>), dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, ntiles);
+        hipLaunchKernelGGL((k_trunk_bf16<64, 768>), grid, block, 0, s, ad, ntiles);
+    else if (tm == 64 && !g_trunk_dreg) hipLaunchKernelGGL(k_trunk_bf16<64>, grid, block, 0, s, ad, ntiles);
+    else if (tm == 128 && g_trunk_var == 16) hipLaunchKernelGGL((k_trunk_bf16<128, 16>), grid, block, 0, s, ad, ntiles);
+    else if (tm == 128 && g_trunk_var == 32) hipLaunchKernelGGL((k_trunk_bf16<128, 32>), grid, block, 0, s, ad, ntiles);
+    else if (tm == 128 && g_trunk_var == 64) hipLaunchKernelGGL((k_trunk_bf16<128, 64>), grid, block, 0, s, ad, ntiles);
+    else if (tm == 128 && g_trunk_var == 128) hipLaunchKernelGGL((k_trunk_bf16<128, 128>), grid, block, 0, s, ad, ntiles);
+    else if (tm == 128 && g_trunk_var == 256) hipLaunchKernelGGL((k_trunk_bf16<128, 256>), grid, block, 0, s, ad, ntiles);
+    else if (tm == 128 && g_trunk_var == 464) hipLaunchKernelGGL((k_trunk_bf16<128, 464>), grid, block, 0, s, ad, ntiles);
+    else done = false;
+#endif
+    if (!done) {
+        if (tm == 64) hipLaunchKernelGGL((k_trunk_bf16<64, 512>), grid, block, 0, s, ad, ntiles);
+        else if (save) hipLaunchKernelGGL((k_trunk_bf16<128, 2048>), grid, block, 0, s, ad, ntiles);
+        else hipLaunchKernelGGL((k_trunk_bf16<128, 0>), grid, block, 0, s, ad, ntiles);
+    }
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -119,11 +119,17 @@ def test_seeded_init_matches_reference():
             assert abs(proj - ref[f"{tag}|{n}|proj"]) <= 1e-9 * max(1.0, abs(ref[f"{tag}|{n}|proj"])), n
 
 
+PRODUCT_OPTIONS = ("fused_trunk", "trunk_tile", "trunk_heads", "heads_epi", "trunk_l0", "pe_inline", "tn_group",
+                   "tn_group_last", "defer_heads", "fused_bwd", "tn_bf16_variant", "tn_bf16_k64", "nt_f32_variant",
+                   "pack_table", "prof_shapes")
+ABLATION_OPTIONS = ("trunk_dbg", "trunk_var", "trunk_dreg", "trunk_bwd_dreg", "tn_bf16_pf", "tn_bf16_quad",
+                    "tn_bf16_m16", "tn_bf16_rounds", "zsave", "trunk2", "trunk2_tile", "nt_bf16_ip", "tn_bf16_ip",
+                    "emu_bf16", "bwd_streams", "heads_variant", "fused_heads", "tile_rowsum")
+
+
 def test_kernel_options_roundtrip_and_reject_unknown_names():
     L = _lib.lib()
-    for name in ("fused_trunk", "trunk_tile", "nt_f32_variant", "tn_f32_variant", "nt_bf16_variant", "tn_bf16_variant", "heads_variant",
-                 "l0_split", "trunk_l0", "fused_heads", "zsave", "pe_inline", "tn_split_tail", "tn_bf16_k64", "trunk_dreg", "trunk_bwd_dreg", "trunk_bwd_nt", "trunk_sigma", "nt_bf16_ip", "tn_bf16_ip", "nt_bf16_epi", "tn_group", "tn_group_rounds", "defer_heads", "tn_k64_pair", "tn_bf16_pf", "tn_bf16_rounds", "tn_bf16_quad", "pack_table", "heads_epi", "ray_tiles_pair",
-                 "bwd_streams"):
+    for name in PRODUCT_OPTIONS:
         old = _lib.get_option(name)
         _lib.set_option(name, old)
         assert _lib.get_option(name) == old
@@ -137,3 +143,18 @@ def test_kernel_options_roundtrip_and_reject_unknown_names():
     for name in (b"trunk_dbg", b"trunk_var", b"heads_dbg"):
         assert L.spnerf_set_option(name, 1) < 0, name
     _lib.set_option("prof_shapes", 0)
+
+
+def test_product_library_has_at_most_15_switches():
+    """The product build accepts exactly its 15 documented kernel switches; the A/B switches of
+    kernels measured slower (and the output-invalidating ablations) exist only in -DSPN_ABLATIONS
+    builds — setting one raises OptionUnavailable (tests that need them skip)."""
+    from spnerf_amd import _lib
+    assert len(PRODUCT_OPTIONS) <= 15
+    for n in PRODUCT_OPTIONS:
+        assert _lib.has_option(n), n
+        _lib.set_option(n, _lib.get_option(n))
+    for n in ABLATION_OPTIONS:
+        assert not _lib.has_option(n), n
+        with pytest.raises(_lib.OptionUnavailable):
+            _lib.set_option(n, 0)
