@@ -330,6 +330,8 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
     every = max(1, steps // checkpoints)
     curves = {a: [] for a in arms}
     loss_curve = {a: [] for a in arms}
+    # every step's training loss of every arm, kept on the device (no per-step host sync)
+    loss_trace = torch.zeros(len(arms), steps, device=dev)
     grad_err, grad_err_top = [], []
     t0 = time.perf_counter()
     for step in range(steps):
@@ -365,6 +367,7 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
                 parts.sort(reverse=True)
                 grad_err_top.append((step, [(nm, round(d, 6), round(r, 6)) for d, nm, r in parts[:3]]))
             opts[a].step()
+            loss_trace[arms.index(a), step] = loss.detach()
             if check:
                 loss_curve[a].append((step, float(loss.detach())))
         if check and step > 0:
@@ -380,6 +383,20 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
         for q, p in zip(probe.parameters(), models["fp32"].parameters()):
             q.copy_(p)
     p16 = held_psnr(probe)
+    lt = loss_trace.cpu().numpy()
+    # loss spikes (SIREN at lr 5e-4): per arm the largest loss after the first 10 % of the run, as a
+    # multiple of the arm's running median of the preceding 50 steps, and where it happened
+    spikes = {}
+    for k, a in enumerate(arms):
+        v = lt[k]
+        best = (0.0, -1)
+        for t in range(max(50, steps // 10), steps):
+            med = float(np.median(v[t - 50:t]))
+            if med > 0 and v[t] / med > best[0]:
+                best = (float(v[t] / med), t)
+        spikes[a] = {"max_ratio_to_running_median": best[0], "step": best[1],
+                     "final_loss_mean_last_50": float(v[-50:].mean()) if steps >= 50 else float(v.mean())}
+    worst = max(range(len(grad_err)), key=lambda k: grad_err[k][1])
     return {"psnr_bf16_db": final["bf16"], "psnr_fp32_hip_db": final["fp32"],
             "delta_db": final["bf16"] - final["fp32"],
             "control_delta_db": final["fp32_control"] - final["fp32"],
@@ -388,6 +405,13 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
             "bf16_inference_at_fp32_trained": {"psnr_db": p16, "delta_db": p16 - final["fp32"]},
             "grad_rel_err": grad_err, "max_grad_rel_err": max(e for _, e in grad_err),
             "grad_err_top_params": grad_err_top,
+            "worst_grad_checkpoint": {"step": grad_err[worst][0], "grad_rel_err": grad_err[worst][1],
+                                      "top_params": grad_err_top[worst][1],
+                                      "fp32_loss_there": float(lt[0, grad_err[worst][0]]),
+                                      "fp32_loss_median_before": float(np.median(lt[0, max(0, grad_err[worst][0] - 50):
+                                                                                     max(1, grad_err[worst][0])]))},
+            "loss_spikes": spikes,
+            "loss_trace_every_10": {a: [float(x) for x in lt[k, ::10]] for k, a in enumerate(arms)},
             "psnr_curve": curves, "loss_curve": loss_curve,
             "steps": steps, "batch_rays": batch, "held_out_rays": n_eval, "train_seconds": train_s,
             "targets": R.rgb_source,
@@ -397,7 +421,8 @@ def psnr_long(steps: int = 2000, batch: int = 1024, n_eval: int = 8192, seed: in
                      "fp32 HIP path is the reference-pinned one (1e-4 per step)"}
 
 
-def psnr_seeds(seeds=(3, 4, 5, 6, 7, 8), steps: int = 1000, batch: int = 512, n_eval: int = 4096, dev="cuda:0"):
+def psnr_seeds(seeds=(3, 4, 5, 6, 7, 8), steps: int = 1000, batch: int = 512, n_eval: int = 4096, dev="cuda:0",
+               checkpoints: int = 8):
     """Paired multi-seed trained-PSNR statistics (BASELINE.json "PSNR vs ref", north star within
     0.05 dB): ``psnr_long`` once per seed (its own init, batches and on-device draws), three arms
     each (fp32 = the reference-pinned HIP path, bf16, fp32_control = fp32 from the init x (1 +
@@ -411,12 +436,16 @@ def psnr_seeds(seeds=(3, 4, 5, 6, 7, 8), steps: int = 1000, batch: int = 512, n_
     per = []
     t0 = time.perf_counter()
     for sd in seeds:
-        r = psnr_long(steps=steps, batch=batch, n_eval=n_eval, seed=sd, dev=dev, checkpoints=4)
+        r = psnr_long(steps=steps, batch=batch, n_eval=n_eval, seed=sd, dev=dev, checkpoints=checkpoints)
         per.append({"seed": sd, "fp32_db": r["psnr_fp32_hip_db"], "bf16_db": r["psnr_bf16_db"],
                     "control_db": r["psnr_fp32_hip_db"] + r["control_delta_db"], "delta_db": r["delta_db"],
                     "control_delta_db": r["control_delta_db"],
                     "infer_delta_db": r["bf16_inference_at_fp32_trained"]["delta_db"],
                     "max_grad_rel_err": r["max_grad_rel_err"],
+                    "grad_rel_err": r["grad_rel_err"],
+                    "worst_grad_checkpoint": r["worst_grad_checkpoint"],
+                    "loss_spikes": r["loss_spikes"],
+                    "loss_trace_every_10": r["loss_trace_every_10"],
                     "final_loss": {a: v[-1][1] for a, v in r["loss_curve"].items()}})
         print(f"psnr_seeds: seed {sd} done ({time.perf_counter() - t0:.0f} s): " +
               " ".join(f"{k} {v:.3f}" for k, v in per[-1].items() if k.endswith("_db")), file=sys.stderr, flush=True)
@@ -435,6 +464,11 @@ def psnr_seeds(seeds=(3, 4, 5, 6, 7, 8), steps: int = 1000, batch: int = 512, n_
             "delta_control_minus_fp32_db": {"mean": c_m, "se": c_se},
             "bf16_inference_at_fp32_trained_db": {"mean": i_m, "se": i_se},
             "max_grad_rel_err": max(q["max_grad_rel_err"] for q in per),
+            "worst_grad_checkpoint": max(({"seed": q["seed"], **q["worst_grad_checkpoint"]} for q in per),
+                                         key=lambda w: w["grad_rel_err"]),
+            "grad_rel_err_quantiles": (lambda v: {"median": float(np.median(v)), "p90": float(np.quantile(v, 0.9)),
+                                                  "max": float(np.max(v)), "n": int(len(v))})(
+                np.array([e for q in per for _, e in q["grad_rel_err"]])),
             "resolvable_0p05_db": resolvable,
             "statement": (f"trained-PSNR difference bf16 - fp32 = {d_m:+.3f} +- {d_se:.3f} dB (mean +- SE over {len(per)} "
                           f"seeds), fp32 control - fp32 = {c_m:+.3f} +- {c_se:.3f} dB: 0.05 dB is "

@@ -254,7 +254,7 @@ int main(int argc, char** argv) {
         t0.ldb = 0;
         const double u0 = timeit([&] { gemm_tn_bf16(t0, splits, 0); });
         printf("library DMA TN, one row (on-chip): %8.1f us  %7.1f TF/s\n", u0, flop / u0 * 1e-6);
-        for (int sp : {splits / 2, splits * 2}) {
+        for (int sp : {splits / 2, splits * 2, splits * 4}) {
             const double u1 = timeit([&] { gemm_tn_bf16(t, sp, 0); });
             printf("library DMA TN, %3d splits: %8.1f us  %7.1f TF/s  %6.2f TB/s\n", sp, u1, flop / u1 * 1e-6, bytes / u1 * 1e-6);
         }
