@@ -70,6 +70,7 @@ struct TN16Args {
     // same leading dimensions.  P1 >= P (the default) = one segment.
     int64_t P1 = INT64_MAX;
     const bf16 *A_s2 = nullptr, *B_s2 = nullptr, *B2_s2 = nullptr;
+    unsigned long long* stamps = nullptr;  // diagnostic builds (-DND_STAMPS, tools/tn_lab_stamps only)
 };
 
 // variant: prefetch depth in K-steps (1 or 2); <= 0 = library default (g_nt16_variant)

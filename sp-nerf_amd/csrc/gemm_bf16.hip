@@ -1383,6 +1383,12 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     while (gi + 1 < G.n && wg >= G.start[gi + 1]) ++gi;
     const int w = wg - G.start[gi];
     const TN16Args& g = G.g[gi];
+#ifdef ND_STAMPS
+    // diagnostic build: lane 0 of waves 0 and 4 of blocks 0 and 128 stamp the IP = 1 main loop
+    const bool st_on = g.stamps && (blockIdx.x == 0 || blockIdx.x == 128) && (wid == 0 || wid == 4) && lane == 0;
+    const int st_base = ((blockIdx.x ? 2 : 0) + (wid >> 2)) * 4096;
+    int st_n = 0;
+#endif
     const int nK = (g.K + TW - 1) / TW;
     const int ntiles = cdiv(g.N, TW) * nK;
     const int split = w / ntiles, t = w % ntiles;
@@ -1486,6 +1492,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
                            "+v"(ah[2]), "+v"(ah[3]), "+v"(bl[0]), "+v"(bl[1]), "+v"(bh[0]), "+v"(bh[1])
                          :
                          : "memory");
+            ND_STAMP(3 + 2 * ks);   // this k-step's fragments in registers
             bf16x8 a[4], b[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) b[j] = join(bl[j], bh[j]);
@@ -1496,6 +1503,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+            ND_STAMP(4 + 2 * ks);   // its MFMAs issued
             if (ks == 0) mid();
         }
     };
@@ -1604,23 +1612,31 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
         for (int st = 0; st < ns; ++st) {
             // step st has landed when at most steps st+1, st+2 (4 DMAs each) are outstanding; the
             // barrier publishes every wave's DMAs and retires step st-1's reads of stage (st+3)%4
+            ND_STAMP(0);
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            ND_STAMP(1);
             __builtin_amdgcn_s_barrier();
+            ND_STAMP(2);
             auto nxt = [&] { issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES); };
             if constexpr (IP == 2) {
                 compute(st % TD_STAGES, nxt);
             } else if constexpr (IP == 1) {
                 compute(st % TD_STAGES, [] {});
                 nxt();
+                ND_STAMP(7);
             } else {
                 nxt();
                 if (!(g.dbg & 1)) compute(st % TD_STAGES, [] {});
             }
             if (do_bias) bias_rows(st % TD_STAGES);
+            ND_STAMP(8);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
         __builtin_amdgcn_s_barrier();
     }
+#ifdef ND_STAMPS
+    if (st_on) g.stamps[st_base + 4095] = st_n;
+#endif
 
     float* slab = g.slab + (int64_t)split * g.slab_stride;
     const int r32 = lane & 31;

@@ -156,6 +156,44 @@ int main(int argc, char** argv) {
         return 1e3 * ms / iters;
     };
     const double flop = 2.0 * P * N * K, bytes = 2.0 * P * (N + K);
+#ifdef ND_STAMPS
+    {   // phase stamps of the library kernel's main loop (tools/tn_lab_stamps): lane 0 of waves 0 / 4
+        // of blocks 0 / 128; per phase transition the mean s_memtime cycles over the stages
+        unsigned long long* st;
+        CK(hipMalloc(&st, 4 * 4096 * 8));
+        CK(hipMemset(st, 0, 4 * 4096 * 8));
+        TN16Args t;
+        t.A = dA; t.lda = N; t.B = dB; t.ldb = K; t.K1 = K;
+        t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K; t.slab_b = slab_b;
+        t.P = P; t.N = N; t.K = K;
+        for (int rep = 0; rep < 5; ++rep) gemm_tn_bf16(t, splits, 0);   // warm clocks
+        t.stamps = st;
+        gemm_tn_bf16(t, splits, 0);
+        CK(hipDeviceSynchronize());
+        std::vector<unsigned long long> h(4 * 4096);
+        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+        for (int w = 0; w < 4; ++w) {
+            const unsigned long long* r = h.data() + w * 4096;
+            const int n = (int)r[4095];
+            double sum[16][16] = {};
+            int cnt[16][16] = {};
+            double total = 0;
+            for (int i = 1; i < n && i < 4095; ++i) {
+                const int a = (int)(r[i - 1] & 15), b = (int)(r[i] & 15);
+                const double d = (double)((r[i] >> 4) - (r[i - 1] >> 4));
+                sum[a][b] += d;
+                cnt[a][b] += 1;
+                total += d;
+            }
+            printf("stream %d (block %d wave %d): %d stamps, %.0f cycles\n", w, w >= 2 ? 128 : 0, (w & 1) * 4, n, total);
+            for (int a = 0; a < 16; ++a)
+                for (int b = 0; b < 16; ++b)
+                    if (cnt[a][b]) printf("   %2d -> %2d: n=%4d mean %7.1f cyc  share %5.1f%%\n", a, b, cnt[a][b], sum[a][b] / cnt[a][b],
+                                          100.0 * sum[a][b] / total);
+        }
+        return 0;
+    }
+#endif
     // profiling mode (argv[3]): one configuration only, for PMC passes — 1 DMA one-row, 2 quad
     // one-row, 3 DMA, 4 quad, 5 prefetched one-row, 6 16x16x32 one-row, 7 16x16x32
     const int mode = argc > 3 ? atoi(argv[3]) : 0;
