@@ -527,7 +527,8 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
     // lane l lands at row 16 q + l / 4, chunk position l % 4, so it loads the logical chunk
     // (l % 4) ^ ((row >> 2) & 3)
     int is_t = t, is_k = 0;  // issue pointer: tile, K-step
-    auto issue = [&](int stg) {
+    // instruction i of the step at the issue pointer (i = 3 advances the pointer)
+    auto issue1 = [&](int stg, int i) {
         const int tile = is_t < ntiles ? is_t : t;  // past the last tile: re-reads, never consumed
         const int bm = (tile / nN) * 256, bn = (tile % nN) * 256;
         const int k0 = is_k * ND_K;
@@ -536,9 +537,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
         const int lda = seg2 ? g.lda2 : g.lda;
         const int el = opaque(lane);
         const int ni = (g.dbg & 16) ? 2 : 4;  // ablation: A only
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i >= ni) break;
+        if (i < ni) {
             const int q = wid + 8 * i;
             const int row = 16 * q + (el >> 2);
             const int c8 = ((el & 3) ^ ((row >> 2) & 3)) * 8;
@@ -546,10 +545,14 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                                     : g.B + (int64_t)min(bn + row - 256, g.N - 1) * g.ldb + k0 + c8;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(smem + stg * ND_STG + q * 1024), 16, 0, 0);
         }
-        if (++is_k == nk) {
+        if (i == 3 && ++is_k == nk) {
             is_k = 0;
             is_t += G;
         }
+    };
+    auto issue = [&](int stg) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) issue1(stg, i);
     };
 
     f32x16 acc[MI][NJ];
@@ -567,10 +570,21 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(sB + j * 32 * 64 + off);
 #pragma unroll
-            for (int i = 0; i < MI; ++i)
+            for (int i = 0; i < MI; ++i) {
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-            if (ks == 0) mid();
+                if constexpr (IP == 3) {
+                    // IP 3: the next step's 4 DMA instructions one per two MFMA groups
+                    if (i & 1) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        mid(2 * ks + (i >> 1));
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            }
+            if constexpr (IP != 3) {
+                if (ks == 0) mid(0);
+            }
         }
     };
 
@@ -661,15 +675,17 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             ND_STAMP(1);
             __builtin_amdgcn_s_barrier();
             ND_STAMP(2);
-            if constexpr (IP == 2) {  // the next step's DMAs between this step's two k-halves
-                compute(gs % ND_STAGES, [&] { issue((gs + 3) % ND_STAGES); });
+            if constexpr (IP == 3) {  // spread over this step's MFMAs
+                compute(gs % ND_STAGES, [&](int i) { issue1((gs + 3) % ND_STAGES, i); });
+            } else if constexpr (IP == 2) {  // the next step's DMAs between this step's two k-halves
+                compute(gs % ND_STAGES, [&](int) { issue((gs + 3) % ND_STAGES); });
             } else if constexpr (IP == 1) {  // after this step's MFMAs
-                compute(gs % ND_STAGES, [] {});
+                compute(gs % ND_STAGES, [](int) {});
                 issue((gs + 3) % ND_STAGES);
             } else {
                 issue((gs + 3) % ND_STAGES);
                 ND_STAMP(3);
-                if (!(g.dbg & 1)) compute(gs % ND_STAGES, [] {});
+                if (!(g.dbg & 1)) compute(gs % ND_STAGES, [](int) {});
             }
         }
         ND_STAMP(4);
@@ -1431,15 +1447,17 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
         }
     }
     const int64_t P1 = g.P1;  // (a local: no scalar loads from the argument inside the loops)
-    auto issue = [&](int st, int stg) {
+    // one of the lane's 4 DMA instructions (IP 3 spreads them over a step's MFMAs)
+    auto issue1 = [&](int st, int stg, int i) {
         const int64_t p0 = p_beg + (int64_t)TD_STEP * st;
         const bool sg2 = p0 >= P1;
+        const int q = wid + 8 * i;
+        const char* a = reinterpret_cast<const char*>(src[i] + p0 * ld[i]) + (sg2 ? dl[i] : 0);
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)a, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
+    };
+    auto issue = [&](int st, int stg) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = wid + 8 * i;
-            const char* a = reinterpret_cast<const char*>(src[i] + p0 * ld[i]) + (sg2 ? dl[i] : 0);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)a, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
-        }
+        for (int i = 0; i < 4; ++i) issue1(st, stg, i);
     };
 
     f32x16 acc[4][2];
@@ -1499,12 +1517,24 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) a[i] = join(al[i], ah[i]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+                if constexpr (IP == 3) {
+                    // IP 3: the next DMA step's 4 instructions one per two MFMA groups, each issued
+                    // among MFMAs already in flight instead of in one burst with every other wave
+                    if (i & 1) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        mid(2 * ks + (i >> 1));
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            }
             ND_STAMP(4 + 2 * ks);   // its MFMAs issued
-            if (ks == 0) mid();
+            if constexpr (IP != 3) {
+                if (ks == 0) mid(0);
+            }
         }
     };
     // bias: thread (chunk ch of 32, row phase lrow of 16) sums rows lrow, lrow + 16 of each step;
@@ -1617,16 +1647,20 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
             ND_STAMP(1);
             __builtin_amdgcn_s_barrier();
             ND_STAMP(2);
-            auto nxt = [&] { issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES); };
-            if constexpr (IP == 2) {
+            auto nxt = [&](int) { issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES); };
+            auto nxt1 = [&](int i) { issue1(min(st + 3, ns - 1), (st + 3) % TD_STAGES, i); };
+            if constexpr (IP == 3) {
+                compute(st % TD_STAGES, nxt1);
+                ND_STAMP(7);
+            } else if constexpr (IP == 2) {
                 compute(st % TD_STAGES, nxt);
             } else if constexpr (IP == 1) {
-                compute(st % TD_STAGES, [] {});
-                nxt();
+                compute(st % TD_STAGES, [](int) {});
+                nxt(0);
                 ND_STAMP(7);
             } else {
-                nxt();
-                if (!(g.dbg & 1)) compute(st % TD_STAGES, [] {});
+                nxt(0);
+                if (!(g.dbg & 1)) compute(st % TD_STAGES, [](int) {});
             }
             if (do_bias) bias_rows(st % TD_STAGES);
             ND_STAMP(8);
@@ -2414,6 +2448,29 @@ static bool tn_wide(int N, int K, int variant, int few = -1) {
     return (v == 2 || v == 3) && N % TW == 0 && K % TW == 0 && (tiles >= 4 || ((few < 0 ? g_tn16_few_tiles : few) && tiles >= 1));
 }
 
+// The DMA NT GEMM's issue placement of the next K-step (IP, k_gemm_nt_bf16d): the product build
+// compiles the default only; -DSPN_ABLATIONS builds every placement (options nt_bf16_ip, nt_bf16_ip_gen)
+constexpr int kNt16IpDefault = 2;
+template <bool DM, int EV, bool HD>
+static void launch_nt16d(int ip, dim3 grid, dim3 block, hipStream_t s, const NT16Args& a, int nt) {
+#ifdef SPN_ABLATIONS
+    if (ip == 3) {
+        hipLaunchKernelGGL((k_gemm_nt_bf16d<DM, 3, EV, HD>), grid, block, 0, s, a, nt);
+        return;
+    }
+    if (ip == 1) {
+        hipLaunchKernelGGL((k_gemm_nt_bf16d<DM, 1, EV, HD>), grid, block, 0, s, a, nt);
+        return;
+    }
+    if (ip == 0) {
+        hipLaunchKernelGGL((k_gemm_nt_bf16d<DM, 0, EV, HD>), grid, block, 0, s, a, nt);
+        return;
+    }
+#endif
+    (void)ip;
+    hipLaunchKernelGGL((k_gemm_nt_bf16d<DM, kNt16IpDefault, EV, HD>), grid, block, 0, s, a, nt);
+}
+
 int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
     SPN_ARG(a.M >= 0 && a.N > 0 && a.K > 0, "gemm_nt_bf16: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
     SPN_ARG(a.K % 8 == 0 && a.N % 8 == 0 && a.n_lin % 8 == 0, "gemm_nt_bf16: K, N, n_lin must be multiples of 8");
@@ -2441,26 +2498,18 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
                           (double)a.M * dcols));
     if (v == 8) {
         const int nt = cdiv(a.M, 256) * cdiv(a.N, 256);
-        const int ip = (a.dbg & 64) ? 2 : (a.dbg & 32) ? 1 : g_nt16_ip;
         const dim3 grid(std::min(nt, num_cus())), block(512);
         if (dm) {
             const bool z = a.dmul_z != 0;   // zsave: Dmul holds Z
+            const int ip = (a.dbg & 64) ? 2 : (a.dbg & 32) ? 1 : g_nt16_ip;
 #ifndef SPN_ABLATIONS
-            // product build: the default issue placement (2) and no saved-Z (zsave) epilogue
+            // product build: the default issue placement and no saved-Z (zsave) epilogue
             SPN_ARG(!z, "gemm_nt_bf16: a saved-Z Dmul (zsave) needs the ablation build");
             (void)ip;
-            hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 0>), grid, block, 0, s, a, nt);
+            launch_nt16d<true, 0, false>(kNt16IpDefault, grid, block, s, a, nt);
 #else
-            if (ip == 2) {
-                if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 1>), grid, block, 0, s, a, nt);
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 2, 0>), grid, block, 0, s, a, nt);
-            } else if (ip == 1) {
-                if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1, 1>), grid, block, 0, s, a, nt);
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 1, 0>), grid, block, 0, s, a, nt);
-            } else {
-                if (z) hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 0, 1>), grid, block, 0, s, a, nt);
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<true, 0, 0>), grid, block, 0, s, a, nt);
-            }
+            if (z) launch_nt16d<true, 1, false>(ip, grid, block, s, a, nt);
+            else launch_nt16d<true, 0, false>(ip, grid, block, s, a, nt);
 #endif
         } else {
             // the epilogue's inputs as a compile-time variant (see k_gemm_nt_bf16d); option
@@ -2473,39 +2522,23 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
                 else if (!a.Dmul && !a.r1_a && a.rowbias && a.rows_per_ray % 32 == 0) ev = 2;
                 else if (a.Dmul && a.r1_a && !a.rowbias && a.act == 0 && !a.Dout) ev = 3;
             }
-#ifdef SPN_ABLATIONS
-            const bool ip2 = g_nt16_ip_gen == 2;
-#else
-            constexpr bool ip2 = true;   // product build: the default issue placement only
-#endif
+            const int ip = g_nt16_ip_gen;
             if (a.hd.n > 0) {
-                SPN_ARG((ev == 1 || ev == 2) && ip2 && a.hd.n <= kNTHeads && a.hd.out && a.hd.hsave && a.N % 256 == 0,
+                SPN_ARG((ev == 1 || ev == 2) && a.hd.n <= kNTHeads && a.hd.out && a.hd.hsave && a.N % 256 == 0,
                         "gemm_nt_bf16: output heads need the bias / per-ray-row DMA epilogue");
                 for (int i = 0; i < a.hd.n; ++i)
                     SPN_ARG(a.hd.col0[i] % 256 == 0 && a.hd.col0[i] + 256 <= a.N && a.hd.nout[i] >= 1 && a.hd.nout[i] <= 3,
                             "gemm_nt_bf16: head group %d", i);
-                if (ev == 1) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 1, true>), grid, block, 0, s, a, nt);
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 2, true>), grid, block, 0, s, a, nt);
+                if (ev == 1) launch_nt16d<false, 1, true>(ip, grid, block, s, a, nt);
+                else launch_nt16d<false, 2, true>(ip, grid, block, s, a, nt);
             } else if (ev == 1) {
-                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 1>), grid, block, 0, s, a, nt);
-#ifdef SPN_ABLATIONS
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 1>), grid, block, 0, s, a, nt);
-#endif
+                launch_nt16d<false, 1, false>(ip, grid, block, s, a, nt);
             } else if (ev == 2) {
-                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 2>), grid, block, 0, s, a, nt);
-#ifdef SPN_ABLATIONS
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 2>), grid, block, 0, s, a, nt);
-#endif
+                launch_nt16d<false, 2, false>(ip, grid, block, s, a, nt);
             } else if (ev == 3) {
-                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 3>), grid, block, 0, s, a, nt);
-#ifdef SPN_ABLATIONS
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 3>), grid, block, 0, s, a, nt);
-#endif
+                launch_nt16d<false, 3, false>(ip, grid, block, s, a, nt);
             } else {
-                if (ip2) hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 2, 0>), grid, block, 0, s, a, nt);
-#ifdef SPN_ABLATIONS
-                else hipLaunchKernelGGL((k_gemm_nt_bf16d<false, 0, 0>), grid, block, 0, s, a, nt);
-#endif
+                launch_nt16d<false, 0, false>(ip, grid, block, s, a, nt);
             }
         }
         SPN_HIP(hipGetLastError());
@@ -2599,6 +2632,10 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
     }
     if (ip == 2) {
         hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, grid, block, 0, s, G);
+        return;
+    }
+    if (ip == 3) {
+        hipLaunchKernelGGL(k_gemm_tn_bf16d<3>, grid, block, 0, s, G);
         return;
     }
     if (ip == 0) {

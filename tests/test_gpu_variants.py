@@ -296,6 +296,28 @@ def test_bf16_tn_quad_wave_grouped_bitwise_equal():
         assert torch.equal(out[0][k], out[1][k]), k
 
 
+@pytest.mark.parametrize("ip", [2, 3])
+def test_bf16_tn_dma_issue_placement_bitwise_equal(ip):
+    """Option tn_bf16_ip (ablation build): where the weight-gradient GEMM issues the next DMA
+    step (2: between its k-halves, 3: one instruction per two MFMA groups) changes no MFMA and
+    no order — gradients bit for bit equal to the default placement, per pass and grouped."""
+    from test_gpu_flatgrad import _deferred_grads
+    r0, g0 = _render_bf16({"tn_bf16_ip": 1}, n=2048, ns=64)
+    r1, g1 = _render_bf16({"tn_bf16_ip": ip}, n=2048, ns=64)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+    old = _lib.get_option("tn_bf16_ip")
+    out = []
+    try:
+        for v in (1, ip):
+            _lib.set_option("tn_bf16_ip", v)
+            out.append(_deferred_grads(9, n_rays=256)[0])
+    finally:
+        _lib.set_option("tn_bf16_ip", old)
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
+
+
 @pytest.mark.parametrize("m16", [1, 2, 3, 4])
 @pytest.mark.parametrize("n,ns", [(300, 64), (2048, 64)])
 def test_bf16_tn_m16_agrees(m16, n, ns):
