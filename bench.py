@@ -803,7 +803,7 @@ def parse_args(argv=None):
                     help="override the config's MLP precision (parity runs; the default line keeps the config's)")
     ap.add_argument("--rehearse-collective", action="store_true",
                     help="(N=1 rehearsal of the N>1 path) a one-rank RCCL group: the bucket all-reduces (identities) "
-                         "captured into the step graph, the exposed collective from paired replays")
+                         "captured into the step graph, the exposed collective timed over the profiled eager steps")
     ap.add_argument("--share-device", action="store_true",
                     help="(rehearsal on a 1-GPU box) every rank on cuda:0 over gloo instead of RCCL")
     return ap.parse_args(argv)
@@ -1078,38 +1078,6 @@ class TrainStep:
         done = [k for k in range(n) if _lib.grad_mark_query(k)]
         return {"marks_completed": done, "n_marks": n}
 
-    def exposed_collective_ms(self, reps: int = 5, wd=None):
-        """With the bucket all-reduces captured INTO the step graph, the exposed collective per
-        step cannot be timed by host events around it: it is measured as the difference of paired
-        replays (each synchronized, medians of ``reps``) of the step graph with the buckets and of
-        a second capture of the same render + loss + backward without them.  None unless the
-        collectives are in the graph."""
-        if not self.in_graph or self.graph is None:
-            return None
-        import statistics
-        torch.cuda.synchronize()
-        self.opt.zero_grad(set_to_none=True)
-        self.model.invalidate_packed()           # both graphs contain the weight re-pack
-        plain = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(plain):
-            self.fwd_bwd()
-        torch.cuda.synchronize()
-        t = {"with": [], "without": []}
-        for r in range(reps):
-            for key, g in (("with", self.graph), ("without", plain)):
-                if wd is not None:
-                    wd.beat(r, f"paired replay ({key} buckets)")
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                g.replay()
-                e1.record()
-                e1.synchronize()
-                t[key].append(e0.elapsed_time(e1))
-        del plain
-        med = {k: statistics.median(v) for k, v in t.items()}
-        return {"exposed_ms": max(0.0, med["with"] - med["without"]), "replay_ms_with_buckets": med["with"],
-                "replay_ms_without": med["without"], "reps": reps}
-
     def close(self):
         from spnerf_amd import set_random_source
         self.graph = None
@@ -1181,15 +1149,18 @@ def run_train(a, config, rank, world, dev, secondary=False):
         _lib.prof_reset()
         _lib.prof_enable(True)
         wd.mode = "eager"
+        # with the collectives inside the graph their exposed part cannot be timed around a replay:
+        # it is timed over these eager steps — the same buckets behind the same backward marks
+        ts.ar_events = []
+        ts.ar_timing = ts.in_graph
         for i in range(prof_steps):
             wd.beat(i, "profiled eager step")
             ts.eager_step()
         torch.cuda.synchronize()
+        ts.ar_timing = False
+        if ts.in_graph and ts.ar_events:
+            allreduce_ms = sum(e0.elapsed_time(e1) for e0, e1 in ts.ar_events) / len(ts.ar_events)
     _lib.prof_enable(False)
-    # graph mode with the collectives captured: the exposed all-reduce from paired replays
-    paired = ts.exposed_collective_ms(wd=wd) if (ts.in_graph and a.graph) else None
-    if paired is not None:
-        allreduce_ms = paired["exposed_ms"]
     wd.close()
 
     kernels = kernel_table(prof_steps)
@@ -1221,10 +1192,9 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "rooflines_top3": top_rooflines(config, B, 3),
         "mlp_mfma_utilisation": gemm_totals(prof_steps),
         "allreduce_ms_per_step": allreduce_ms,
-        "allreduce_exposed_paired_replays": paired,
         "allreduce": (None if (world == 1 and not ts.rehearse) else
                       f"{len(buckets.buckets)} buckets behind the backward's gradient marks, inside the HIP graph "
-                      "(exposed ms = paired replays with / without the buckets)"
+                      "(exposed ms timed over the profiled eager steps: the same buckets behind the same marks)"
                       if ts.in_graph else
                       f"{len(buckets.buckets)} buckets after each graph replay (exposed ms above)"
                       if (buckets is not None and a.graph) else

@@ -1537,6 +1537,38 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
             }
         }
     };
+    // one 16-point k-step of stage stg (IP 4's shifted schedule)
+    auto kstep = [&](int stg, int ks) {
+        const char* sA = smem + stg * TD_STG + wa * HALF;
+        const char* sB = smem + stg * TD_STG + (2 + (wb >> 1)) * HALF;
+        const int cb = (wb & 1) * 64;
+        const int r0 = 16 * ks + 8 * h;
+        s16x4 al[4], ah[4], bl[2], bh[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            bl[j] = trd(sB, r0, cb + 32 * j + 16 * grp);
+            bh[j] = trd(sB, r0 + 4, cb + 32 * j + 16 * grp);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            al[i] = trd(sA, r0, 32 * i + 16 * grp);
+            ah[i] = trd(sA, r0 + 4, 32 * i + 16 * grp);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(ah[0]), "+v"(ah[1]), "+v"(ah[2]),
+                       "+v"(ah[3]), "+v"(bl[0]), "+v"(bl[1]), "+v"(bh[0]), "+v"(bh[1])
+                     :
+                     : "memory");
+        bf16x8 av[4], bv[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = join(bl[j], bh[j]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = join(al[i], ah[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    };
     // bias: thread (chunk ch of 32, row phase lrow of 16) sums rows lrow, lrow + 16 of each step;
     // bsplit: thread (chunk ch of the tile's 16, row phase lrow of 32) sums row lrow
     const int ch = bsplit ? 16 * kt + (tid & 15) : tid & 31, lrow = bsplit ? tid >> 4 : tid >> 5;
@@ -1607,7 +1639,34 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     };
 
-    if (PF && ns > 0) {  // block-uniform
+    if (IP == 4 && ns > 0) {  // block-uniform
+        // IP 4 (ablation build): the two waves of a SIMD (wid and wid + 4, the halves wa = 0 / 1)
+        // run one k-step apart, so one waits on its LDS reads, the DMA or the barrier while the
+        // other issues MFMAs (with one barrier per stage the two otherwise run in lockstep and wait
+        // together).  The lagging half still reads stage st - 1 after stage st's barrier, so the
+        // ring keeps two stages ahead (slots: st - 1, st, st + 1, st + 2).  Same MFMAs in the same
+        // order per wave (bit-identical).
+        issue(0, 0);
+        issue(min(1, ns - 1), 1);
+        const int lag = wa;
+        for (int it = 0; it <= 2 * ns; ++it) {
+            if ((it & 1) == 0 && it < 2 * ns) {  // uniform: every wave meets ns barriers
+                const int st = it >> 1;
+                // stage st landed (own DMAs: st + 1 outstanding); the barrier publishes it and
+                // retires every wave's reads of stage st - 2 (the lagging half's last: iteration 2st-2)
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                issue(min(st + 2, ns - 1), (st + 2) % TD_STAGES);
+            }
+            const int hs = it - lag;  // this wave's half-step (wave-uniform)
+            if (hs >= 0 && hs < 2 * ns) {
+                kstep((hs >> 1) % TD_STAGES, hs & 1);
+                if (do_bias && (hs & 1)) bias_rows((hs >> 1) % TD_STAGES);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
+        __builtin_amdgcn_s_barrier();
+    } else if (PF && ns > 0) {  // block-uniform
         issue(0, 0);
         issue(min(1, ns - 1), 1);
         issue(min(2, ns - 1), 2);
@@ -2636,6 +2695,10 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
     }
     if (ip == 3) {
         hipLaunchKernelGGL(k_gemm_tn_bf16d<3>, grid, block, 0, s, G);
+        return;
+    }
+    if (ip == 4) {
+        hipLaunchKernelGGL(k_gemm_tn_bf16d<4>, grid, block, 0, s, G);
         return;
     }
     if (ip == 0) {

@@ -131,6 +131,7 @@ class SPNeRF(torch.nn.Module):
         self._order = None
         self._packed = None
         self._pack_pool = []
+        self._graph_packs = []   # packed-weight buffers captured into HIP graphs (kept alive)
         self._flat_grad = None
         self.flat_grads = False  # opt-in direct gradient path (use_flat_grads)
         # with flat gradients: one trunk weight-gradient GEMM per layer over all passes of a render
@@ -332,6 +333,12 @@ class WeightPack:
             # backward still reads it
             if not torch.cuda.is_current_stream_capturing():
                 self.model.release_packed(self.buf)
+            else:
+                # ... and it must stay ALLOCATED for the graph's lifetime: a buffer taken from the
+                # free list was allocated outside the capture, so with its last reference gone
+                # the caching allocator would hand its memory to later eager tensors while every
+                # replay still writes the packed weights into it
+                self.model._graph_packs.append(self.buf)
             self.buf = None
 
 

@@ -296,11 +296,12 @@ def test_bf16_tn_quad_wave_grouped_bitwise_equal():
         assert torch.equal(out[0][k], out[1][k]), k
 
 
-@pytest.mark.parametrize("ip", [2, 3])
+@pytest.mark.parametrize("ip", [2, 3, 4])
 def test_bf16_tn_dma_issue_placement_bitwise_equal(ip):
     """Option tn_bf16_ip (ablation build): where the weight-gradient GEMM issues the next DMA
-    step (2: between its k-halves, 3: one instruction per two MFMA groups) changes no MFMA and
-    no order — gradients bit for bit equal to the default placement, per pass and grouped."""
+    step (2: between its k-halves, 3: one instruction per two MFMA groups) or the shifted schedule
+    (4: the two waves of a SIMD a k-step apart) changes no MFMA and no order — gradients bit for
+    bit equal to the default placement, per pass and grouped."""
     from test_gpu_flatgrad import _deferred_grads
     r0, g0 = _render_bf16({"tn_bf16_ip": 1}, n=2048, ns=64)
     r1, g1 = _render_bf16({"tn_bf16_ip": ip}, n=2048, ns=64)

@@ -242,6 +242,20 @@ int main(int argc, char** argv) {
         g_tn16_pf = 0;
         g_tn16_quad = 0;
     }
+    for (int ip : {3, 4, 1}) {   // option tn_bf16_ip: 3 = DMAs spread over the MFMAs, 4 = the two waves of a SIMD a k-step apart
+        g_tn16_ip = ip;
+        const double up = timeit([&] { gemm_tn_bf16(t, splits, 0); });
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(k_reduce, dim3(N * K / 256), dim3(256), 0, 0, slab, splits, (int64_t)N * K, got);
+        std::vector<float> hr((size_t)N * K), hg(hr.size());
+        CK(hipMemcpy(hr.data(), ref, hr.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hg.data(), got, hg.size() * 4, hipMemcpyDeviceToHost));
+        const double u2 = timeit([&] { gemm_tn_bf16(t, 2 * splits, 0); });
+        printf("library DMA TN, IP %d: %8.1f us  %7.1f TF/s  %6.2f TB/s  bitwise %s;  %d splits: %8.1f us\n", ip, up,
+               flop / up * 1e-6, bytes / up * 1e-6, memcmp(hr.data(), hg.data(), hr.size() * 4) == 0 ? "equal" : "DIFFERENT",
+               2 * splits, u2);
+    }
+    g_tn16_ip = 1;
     for (int m16 : {1, 2, 3, 4}) {   // option tn_bf16_m16: 16x16x32 kernels (1/2: 8 waves, 3/4: 16 waves; 4 / 5 DMA stages)
         g_tn16_m16 = m16;
         const double up = timeit([&] { gemm_tn_bf16(t, splits, 0); });
