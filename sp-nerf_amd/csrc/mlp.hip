@@ -2104,8 +2104,10 @@ static int32_t trunk_wgrad(const Dims& d, int n_seg, void* const* wss, const int
             }
         // the skip layer's PE tail and fc_net.0 (both N = W, K = K0p over the PE rows X0b) share one
         // launch of the narrow kernel at the end, with half the splits each
-        const bool pair_tail = g_tn_k64_pair && tn_k64_ok(W, d.K0p) && d.skip >= 1 && d.skip < 16 && grouped[d.skip] &&
-                               c.k.Kp[0] == d.K0p;
+        // (not with tn_group_last: the skip layer's tail then runs right after its group, so its mark
+        // fires a launch earlier instead of with fc_net.0's at the very end)
+        const bool pair_tail = g_tn_k64_pair && g_tn_group_last == 0 && tn_k64_ok(W, d.K0p) && d.skip >= 1 && d.skip < 16 &&
+                               grouped[d.skip] && c.k.Kp[0] == d.K0p;
         bool tail_pending = false;
         for (size_t g0 = 0; g0 < items.size();) {
             size_t g1 = std::min(items.size(), g0 + (size_t)std::min(g_tn_group, kTnGroup));

@@ -95,9 +95,15 @@ def _deferred_grads(tn_group, n_rays=96, rounds=1, beta=False, defer_heads=1):
     valid = (torch.rand(n_rays, generator=g) > 0.3).long().to(DEV)
     sems = torch.randint(0, 3, (n_rays,), generator=g).to(DEV)
     ts = torch.randint(0, 4, (n_rays,), generator=g).to(DEV)
-    names = ("tn_group", "tn_group_rounds", "defer_heads")
+    # (tn_group_rounds is an ablation-build switch; the product library runs its automatic choice,
+    # rounds = 0, which is 1 block per CU below 2^16 points per split — so rounds 0 and, at these
+    # small sizes, 1 need no switch; 2 skips in the product build)
+    opts = {"tn_group": tn_group, "defer_heads": defer_heads}
+    if _lib.has_option("tn_group_rounds") or rounds not in (0, 1):
+        opts["tn_group_rounds"] = rounds
+    names = tuple(opts)
     old = [_lib.get_option(k) for k in names]
-    for k, v in zip(names, (tn_group, rounds, defer_heads)):
+    for k, v in opts.items():
         _lib.set_option(k, v)
     try:
         torch.manual_seed(0)
