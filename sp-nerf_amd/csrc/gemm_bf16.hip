@@ -1418,6 +1418,13 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     const bool bsplit = g.bias_split && nK == 2;
     const int kt = t % nK;
     const bool do_bias = g.slab_b != nullptr && (bsplit || k0 == 0);
+    // IP 4 / 5: the bias sums from the A fragments already in registers (no LDS row reads): wave
+    // (wa, wb) sums A fragment i = wb — feature 128 wa + 32 wb + lane % 32, 8 points per k-step per
+    // lane — when its half wa is summed by this tile (bsplit: wa == kt; else every wave of the
+    // k0 == 0 tile); lanes l and l + 32 (the two point halves) are added at the end
+    constexpr bool BR = IP >= 4;
+    const bool rb_on = BR && do_bias && (!bsplit || (wid >> 2) == kt);  // wave-uniform
+    float rbias = 0.f;
     const int ns = p_end > p_beg ? (p_end - p_beg) / TD_STEP : 0;  // whole steps (host-checked)
 
     // this lane's 4 DMA sources (instructions q = wid + 8 i: i < 2 → A, else B), advanced by
@@ -1559,6 +1566,19 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
                        "+v"(ah[3]), "+v"(bl[0]), "+v"(bl[1]), "+v"(bh[0]), "+v"(bh[1])
                      :
                      : "memory");
+        if constexpr (BR) {
+            if (rb_on) {  // wave-uniform
+                // the fragment of A column block wb (a compile-time index per branch)
+                s16x4 xl = al[0], xh = ah[0];
+                if (wb == 1) xl = al[1], xh = ah[1];
+                if (wb == 2) xl = al[2], xh = ah[2];
+                if (wb == 3) xl = al[3], xh = ah[3];
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) rbias += __uint_as_float((uint32_t)(uint16_t)xl[e2] << 16);
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) rbias += __uint_as_float((uint32_t)(uint16_t)xh[e2] << 16);
+            }
+        }
         bf16x8 av[4], bv[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) bv[j] = join(bl[j], bh[j]);
@@ -1661,8 +1681,23 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
             const int hs = it - lag;  // this wave's half-step (wave-uniform)
             if (hs >= 0 && hs < 2 * ns) {
                 kstep((hs >> 1) % TD_STAGES, hs & 1);
-                if (do_bias && (hs & 1)) bias_rows((hs >> 1) % TD_STAGES);
+                if (!BR && do_bias && (hs & 1)) bias_rows((hs >> 1) % TD_STAGES);
             }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
+        __builtin_amdgcn_s_barrier();
+    } else if (IP == 5 && ns > 0) {  // block-uniform
+        // IP 5 (ablation build): IP 1's schedule (4 stages, 3 in flight, DMAs after the MFMAs) with
+        // the bias sums from the fragments in registers
+        issue(0, 0);
+        issue(min(1, ns - 1), 1);
+        issue(min(2, ns - 1), 2);
+        for (int st = 0; st < ns; ++st) {
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            kstep(st % TD_STAGES, 0);
+            kstep(st % TD_STAGES, 1);
+            issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing may land in the reused LDS
         __builtin_amdgcn_s_barrier();
@@ -1745,7 +1780,12 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
                 if (n < g.N) slab[(int64_t)n * g.ld_slab + k] = acc[i][j][r];
             }
     }
-    if (do_bias && bsplit) {
+    if constexpr (BR) {
+        if (rb_on) {  // wave-uniform: lanes l and l + 32 hold the two point halves of one feature
+            const float other = __shfl_down(rbias, 32, 64);
+            if (lane < 32) g.slab_b[(int64_t)split * g.N + n0 + 128 * (wid >> 2) + 32 * wb + lane] = rbias + other;
+        }
+    } else if (do_bias && bsplit) {
         __syncthreads();
         float* red = reinterpret_cast<float*>(smem);  // [32 phases][128 features]
         const int cl = ch & 15;
@@ -2699,6 +2739,10 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
     }
     if (ip == 4) {
         hipLaunchKernelGGL(k_gemm_tn_bf16d<4>, grid, block, 0, s, G);
+        return;
+    }
+    if (ip == 5) {
+        hipLaunchKernelGGL(k_gemm_tn_bf16d<5>, grid, block, 0, s, G);
         return;
     }
     if (ip == 0) {

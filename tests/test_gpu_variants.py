@@ -296,17 +296,27 @@ def test_bf16_tn_quad_wave_grouped_bitwise_equal():
         assert torch.equal(out[0][k], out[1][k]), k
 
 
-@pytest.mark.parametrize("ip", [2, 3, 4])
+def _close_or_equal(a, b, bitwise, k):
+    if bitwise:
+        assert torch.equal(a, b), k
+    else:
+        assert torch.isfinite(b).all(), k
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-30)
+        assert err <= 1e-5, (k, err)
+
+
+@pytest.mark.parametrize("ip", [2, 3, 4, 5])
 def test_bf16_tn_dma_issue_placement_bitwise_equal(ip):
     """Option tn_bf16_ip (ablation build): where the weight-gradient GEMM issues the next DMA
-    step (2: between its k-halves, 3: one instruction per two MFMA groups) or the shifted schedule
-    (4: the two waves of a SIMD a k-step apart) changes no MFMA and no order — gradients bit for
-    bit equal to the default placement, per pass and grouped."""
+    step (2: between its k-halves, 3: one instruction per two MFMA groups) changes no MFMA and no
+    order — gradients bit for bit equal to the default placement, per pass and grouped; 4 (the two
+    waves of a SIMD a k-step apart) and 5 (the default schedule) sum the biases from the fragments
+    in registers — another fixed order: weight gradients bitwise, biases within 1e-5."""
     from test_gpu_flatgrad import _deferred_grads
     r0, g0 = _render_bf16({"tn_bf16_ip": 1}, n=2048, ns=64)
     r1, g1 = _render_bf16({"tn_bf16_ip": ip}, n=2048, ns=64)
     for k in g0:
-        assert torch.equal(g0[k], g1[k]), k
+        _close_or_equal(g0[k], g1[k], ip < 4 or not k.endswith("bias"), k)
     old = _lib.get_option("tn_bf16_ip")
     out = []
     try:
@@ -316,7 +326,7 @@ def test_bf16_tn_dma_issue_placement_bitwise_equal(ip):
     finally:
         _lib.set_option("tn_bf16_ip", old)
     for k in out[0]:
-        assert torch.equal(out[0][k], out[1][k]), k
+        _close_or_equal(out[0][k], out[1][k], ip < 4 or not k.endswith("bias"), k)
 
 
 @pytest.mark.parametrize("m16", [1, 2, 3, 4])

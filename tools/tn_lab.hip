@@ -242,7 +242,7 @@ int main(int argc, char** argv) {
         g_tn16_pf = 0;
         g_tn16_quad = 0;
     }
-    for (int ip : {3, 4, 1}) {   // option tn_bf16_ip: 3 = DMAs spread over the MFMAs, 4 = the two waves of a SIMD a k-step apart
+    for (int ip : {3, 4, 5, 1}) {   // option tn_bf16_ip: 3 = DMAs spread over the MFMAs, 4 = the two waves of a SIMD a k-step apart, 5 = bias in registers
         g_tn16_ip = ip;
         const double up = timeit([&] { gemm_tn_bf16(t, splits, 0); });
         CK(hipDeviceSynchronize());
