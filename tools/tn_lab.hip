@@ -138,8 +138,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dBi, bi.data(), bi.size() * 2, hipMemcpyHostToDevice));
     const int splits = tn_splits_bf16(P, N, K);
     float *slab, *slab_b, *ref, *got;
-    CK(hipMalloc(&slab, (size_t)2 * splits * N * K * 4));   // (room for the 2x-splits run)
-    CK(hipMalloc(&slab_b, (size_t)2 * splits * N * 4));
+    CK(hipMalloc(&slab, (size_t)4 * splits * N * K * 4));   // (room for the 4x-splits runs)
+    CK(hipMalloc(&slab_b, (size_t)4 * splits * N * 4));
     CK(hipMalloc(&ref, (size_t)N * K * 4));
     CK(hipMalloc(&got, (size_t)N * K * 4));
     hipEvent_t e0, e1;
