@@ -526,8 +526,8 @@ def roofline_of(dom, nt, traffic=None, traffic_src=None):
     kernel without MFMAs is HBM-bound.  Both fractions are reported; ``frac`` is the binding one."""
     if dom in GEMM_CLASSES:
         dom_name, peak = GEMM_CLASSES[dom]
-        if "<IP>" in dom_name:   # the template instance the library launches (product build: <1, false>)
-            ip = _lib.get_option("tn_bf16_ip") if _lib.has_option("tn_bf16_ip") else 1
+        if "<IP>" in dom_name:   # the template instance the library launches (product build: <3, false>)
+            ip = _lib.get_option("tn_bf16_ip") if _lib.has_option("tn_bf16_ip") else 3
             pf = _lib.has_option("tn_bf16_pf") and _lib.get_option("tn_bf16_pf") == 1
             dom_name = dom_name.replace("<IP>", f"<{ip}, {'true' if pf else 'false'}>")
     else:

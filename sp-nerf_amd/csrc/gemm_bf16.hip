@@ -2527,7 +2527,11 @@ int g_nt16_ip = 2;  // DMA NT / TN: where a K-step issues the next step's DMAs (
 // the weight-gradient GEMM: 1 (after a step's MFMAs) re-measured on the final round-3 tree: C4 26.69 /
 // 26.72 / 26.71 -> 26.62 / 26.64 / 26.61 ms, the TN class 6.20 -> 6.09 ms per step, C4@512 level
 // (tools/gpu_r3zf.sh); 2 was the better placement when the TN was measured in isolation (r02)
-int g_tn16_ip = 1;
+// round 5: 3 = the four DMA instructions of the next step one per two MFMA groups (bit-identical):
+// C4 25.92 / 25.96 / 25.96 -> 25.65 / 25.77 ms, the TN class 6.52 -> 6.30 ms per step, C4@512
+// 3.844 / 3.826 -> 3.812 / 3.808 ms (pairs in one call); the product build compiles only this one
+constexpr int kTn16IpDefault = 3;
+int g_tn16_ip = kTn16IpDefault;
 int g_tn16_bias_split = 1;
 int g_nt16_ip_gen = 2;  // the same for the general (bias / sine / rank-1) epilogue instances
 int g_nt16_epi = 1;     // option "nt_bf16_epi": 1 = compile-time epilogue variants of the DMA NT, 0 = the generic one
@@ -2733,10 +2737,6 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
         hipLaunchKernelGGL(k_gemm_tn_bf16d<2>, grid, block, 0, s, G);
         return;
     }
-    if (ip == 3) {
-        hipLaunchKernelGGL(k_gemm_tn_bf16d<3>, grid, block, 0, s, G);
-        return;
-    }
     if (ip == 4) {
         hipLaunchKernelGGL(k_gemm_tn_bf16d<4>, grid, block, 0, s, G);
         return;
@@ -2749,10 +2749,14 @@ static void launch_tn_bf16d(const TN16Args* a, int n, const int* blocks, int ip,
         hipLaunchKernelGGL(k_gemm_tn_bf16d<0>, grid, block, 0, s, G);
         return;
     }
+    if (ip == 1) {
+        hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, grid, block, 0, s, G);
+        return;
+    }
 #else
-    (void)ip;   // the product build: IP = 1 (the default placement), no variant kernels
+    (void)ip;   // the product build: the default placement only, no variant kernels
 #endif
-    hipLaunchKernelGGL(k_gemm_tn_bf16d<1>, grid, block, 0, s, G);
+    hipLaunchKernelGGL(k_gemm_tn_bf16d<kTn16IpDefault>, grid, block, 0, s, G);
 }
 
 bool tn_k64_ok(int N, int K) { return tn_k64(N, K); }

@@ -1557,7 +1557,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
     T* S3buf = save ? G::buf(c, c.w.S3) : G::buf(c, c.w.Hb[2]);
     // option heads_epi: the narrow heads in the G / Q / sun_v.3 epilogues (bf16 DMA NT with the
     // bias / per-ray-row epilogue; σ from the trunk's hsave column)
-    const bool hepi = BF && g_heads_epi && g_nt16_epi && g_nt16_ip_gen == 2 && !zs && g_nt16_variant == 8 && save &&
+    const bool hepi = BF && g_heads_epi && g_nt16_epi && (g_nt16_ip_gen == 2 || g_nt16_ip_gen == 3) && !zs && g_nt16_variant == 8 && save &&
                       sig_done && *sig_done && c.out && c.heads_epi_done &&
                       W == 512 && H == 256 && (!d.sem || d.C <= 3) && S % 32 == 0 && mode != 1 &&
                       d.NG % 256 == 0 && d.NQ % 256 == 0;

@@ -296,6 +296,19 @@ def test_bf16_tn_quad_wave_grouped_bitwise_equal():
         assert torch.equal(out[0][k], out[1][k]), k
 
 
+def test_bf16_nt_dma_issue_placement_bitwise_equal():
+    """Options nt_bf16_ip / nt_bf16_ip_gen (ablation build): the head and dX GEMMs issuing the next
+    DMA step one instruction per two MFMA groups (3) instead of between the k-halves (2, the
+    default) change no MFMA and no order — renders and gradients bit for bit, the heads in the GEMM
+    epilogues included."""
+    r0, g0 = _render_bf16({"heads_epi": 1, "nt_bf16_ip": 2, "nt_bf16_ip_gen": 2}, n=2048, ns=64)
+    r1, g1 = _render_bf16({"heads_epi": 1, "nt_bf16_ip": 3, "nt_bf16_ip_gen": 3}, n=2048, ns=64)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+
+
 def _close_or_equal(a, b, bitwise, k):
     if bitwise:
         assert torch.equal(a, b), k
