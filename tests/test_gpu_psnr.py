@@ -38,11 +38,19 @@ def test_long_horizon_bf16_psnr_matches_fp32_hip():
         curve = r["loss_curve"][arm]
         assert curve[-1][1] < curve[0][1]   # every arm trains
     assert abs(r["bf16_inference_at_fp32_trained"]["delta_db"]) <= 0.05, r
-    # at init the fixtures' bf16 bound; along the run the norm-relative error grows where the
-    # gradient shrinks and cancels over the batch (measured at 256 rays: 0.4% at init, 5.0% at
-    # step 100, 1.1-1.7% after step 150) — held at 2x that
+    # at init the fixtures' bf16 bound (0.4% measured at 256 rays); along the run the
+    # norm-relative error grows where the gradient shrinks and cancels over the batch — the worst
+    # tensors are the sun-visibility head's — so the run is held to the bench's
+    # gradient gates (bench.GRAD_GATES, the same ones the bench line evaluates over 6 seeds x 8
+    # checkpoints): median and max of that error, and the max of its ratio to the fp32 gradient's
+    # own change between two batches at the same weights (the minibatch noise)
+    import numpy as np
     assert r["grad_rel_err"][0][1] <= 2e-2, r["grad_rel_err"]
-    assert r["max_grad_rel_err"] <= 0.1, r["grad_rel_err"]
+    errs = np.array([e for _, e in r["grad_rel_err"]])
+    ratios = np.array([e / f["other_batch"] for (_, e), f in zip(r["grad_rel_err"], r["grad_floors"])])
+    gates = bench.grad_gates(errs, ratios)
+    print("gates", gates, "floors", r["grad_floors"])
+    assert all(g["pass"] for g in gates.values()), gates
     # the trained-PSNR difference of two trajectories is reported (with the control beside it,
     # and as paired multi-seed statistics in the bench line: bench.psnr_seeds), not gated: at this
     # horizon it measures trajectory noise, not precision
