@@ -67,6 +67,9 @@ GEMM_CLASSES = {
     "trunk_bf16": ("k_trunk_bf16<128> (fused bf16 trunk, inference: 128-point LDS-resident tiles; the "
                    "two-workgroup k_trunk2_bf16 only in the ablation build)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bf16_train": ("k_trunk_bf16<128, 2048> (fused bf16 trunk, 128-point training tiles saving H and D)", BF16_MFMA_PEAK_TFLOPS),
+    "heads_train": ("k_heads_train_bf16 (fused bf16 training heads after the trunk, 128-point LDS-resident tiles: "
+                    "semantic hidden, feat, Q, sun_v 2 / 3 saving their activations, and the narrow heads; option "
+                    "heads_epi 2)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_bwd_bf16": ("k_trunk_bwd_bf16 (fused bf16 backward dX chain, LDS-resident dZ)", BF16_MFMA_PEAK_TFLOPS),
     "heads_fused": ("k_heads_bf16 (fused bf16 inference heads, LDS-resident activations)", BF16_MFMA_PEAK_TFLOPS),
     "trunk_heads_bf16": ("k_trunk_bf16<128, 4096> (fused bf16 inference trunk with the heads on its last LDS "

@@ -67,6 +67,73 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
     }
 }
 
+// Training (option heads_epi 2): the same tile loop with hd::heads_tile_train — H_L staged from
+// HBM (the saving trunk writes it for the weight gradients anyway), σ from the trunk's hsave[p·8],
+// every activation the backward reads stored, the layers' biases staged once in the RQ area.  Its
+// own launch keeps the heads' registers out of the trunk's allocation: inside the trunk launch
+// the trunk's tile loop spilled (64-bit values reloaded from scratch behind the copy-out stores)
+// and the main pass took 5.78 ms against 2.78 + 1.72 ms for the two launches.
+static_assert(SB_N * 4 <= RQ_BYTES, "the training heads' biases in the RQ area");
+__global__ __launch_bounds__(512) void k_heads_train_bf16(HeadsFusedArgs g, PackedOffs k, int ntiles) {
+    __shared__ __attribute__((aligned(16))) char smem[LDS];
+    const int tid = threadIdx.x;
+    float* ost = reinterpret_cast<float*>(smem + OST_OFF);
+    float* part = reinterpret_cast<float*>(smem + PART_OFF);
+    float* sbias = reinterpret_cast<float*>(smem + RQ_OFF);
+    for (int i = tid; i < SB_N; i += 512) {
+        const float* P = g.packed;
+        sbias[i] = i < SB_Q ? (g.C > 0 || i < HW ? P[k.bG + i] : 0.f)
+                 : i < SB_S2 ? P[k.bQ + (i - SB_Q)] : i < SB_S3 ? P[k.bs2 + (i - SB_S2)] : P[k.bs3 + (i - SB_S3)];
+    }
+    __syncthreads();
+    for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
+        const int64_t p0 = (int64_t)tile * TM;
+#pragma unroll
+        for (int q0 = 0; q0 < 16; q0 += 8) {
+            u32x4 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int c = tid + 512 * (q0 + q), row = c >> 6, ch = c & 63;
+                v[q] = *reinterpret_cast<const u32x4*>(g.HL + std::min<int64_t>(p0 + row, g.P - 1) * HW + ch * 8);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int c = tid + 512 * (q0 + q), row = c >> 6, ch = c & 63;
+                *reinterpret_cast<u32x4*>(smem + img_off(row, ch)) = v[q];
+            }
+        }
+        const int r = opaque(tid);
+        if (r < TM) ost[r * OST_LD + 3] = softplusf_(g.hsave[std::min<int64_t>(p0 + r, g.P - 1) * 8]);
+        __syncthreads();
+        heads_tile_train(g, k, smem, ost, part, sbias, p0);
+        __syncthreads();  // the next tile restages the image
+    }
+}
+
+bool heads_train_bf16_ok(const HeadsFusedArgs& h, const PackedOffs& k) {
+    return h.HL && (h.mode == 0 || h.mode == 2) && h.NO <= OST_LD && h.C <= 3 && h.G && h.Q && h.DQ && h.S2 && h.DS2 &&
+           h.S3 && h.DS3 && h.hsave && (h.mode != 0 || h.C == 0 || h.DG) && h.ldG % 8 == 0 && h.ldQ % 8 == 0 &&
+           k.Fnar16 >= 0 && k.Ffeat16 >= 0 && k.FQ16 >= 0 && k.Fs2_16 >= 0 && k.Fs3_16 >= 0 && (h.C == 0 || k.Fsem16 >= 0);
+}
+
+int32_t heads_train_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes) {
+    SPN_ARG(a.P >= 0 && a.S > 0 && heads_train_bf16_ok(a, k), "heads_train_bf16: bad arguments");
+    if (a.P == 0) return SPNERF_OK;
+    SPN_ARG(a.P < (1ll << 31) / HW, "heads_train_bf16: too many points (%lld)", (long long)a.P);
+    const int ntiles = (int)((a.P + TM - 1) / TM);
+    HeadsFusedArgs ad = a;
+    ad.nt = 0;
+#ifdef SPN_ABLATIONS
+    ad.dbg = g_heads_dbg;
+#else
+    ad.dbg = 0;
+#endif
+    ProfScope prof("heads_train", s, flop, bytes);
+    hipLaunchKernelGGL(k_heads_train_bf16, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, k, ntiles);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
 bool heads_bf16_shape_ok(const Dims& d) {
     return d.bf && d.W == HW && d.H == HH && !d.beta && d.C <= 4 && d.NQ == 2 * d.H && d.NO <= OST_LD && d.sem_col == 8;
 }

@@ -327,6 +327,390 @@ __device__ __forceinline__ void heads_tile(GA& g, KA& k, char* smem, float* ost,
     }
 }
 
+// ---- training (option heads_epi 2, k_heads_train_bf16): the same layers after the SAVING trunk,
+// with every activation the backward reads stored at the layer-by-layer GEMMs' addresses
+// (HeadsFusedArgs G / DG / Q / DQ / S2 / DS2 / S3 / DS3, hsave).  The wide layers run the
+// layer-by-layer GEMMs' arithmetic — the same MFMA (32x32x16 bf16, the K-steps of 16 in
+// ascending order, weights and activations in swapped operand roles: the same products in the
+// same order), then + bias (+ the per-ray row), fast_sincos, RNE to bf16 — so G, Q, sun_v 2 / 3
+// and their D equal the DMA NT GEMMs' (k_gemm_nt_bf16d) bit for bit; the narrow heads run on
+// MFMA (narrow_mm, hi / lo weight rows) as in inference instead of in those GEMMs' epilogues.
+//
+// The stores are kept off the MFMAs' critical path the way the training trunk does it: a
+// layer's image leaves for HBM in slices inside the NEXT layer's k-loop, each slice after that
+// k-step group's weight refills (so no ring wait counts it), and the next layer's weight ring is
+// primed before a layer's epilogue, so the register stores of D there (v_permlane32_swap-joined
+// 16-B pieces) are younger than every load the next k-loop waits for.
+
+// 16-B stores of one accumulator tile's 16-feature group pairs: cq[gq] holds the bf16 of
+// features fbase + 8·gq + 4·eh .. +3 at tile row `row`; pairs (0, 1) and (2, 3) are joined by
+// v_permlane32_swap so lane l < 32 stores features fbase + 8k .. +7 and lane l + 32 the next 8
+// (the training trunk's register-D store).  Rows past P fall outside the descriptor: dropped.
+__device__ __forceinline__ void store_rows16(__amdgpu_buffer_rsrc_t rs, int ld, int fbase, int row, int eh, u32x2 (&cq)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const auto r = __builtin_amdgcn_permlane32_swap(cq[k][e], cq[k + 1][e], false, false);
+            cq[k][e] = r[0];
+            cq[k + 1][e] = r[1];
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]}, rs,
+                                               (row * ld + fbase + 8 * k + 8 * eh) * 2, 0, 0);
+    }
+}
+
+// chunks [q0, q0 + N) (per thread) of image columns [0, 8·NCH) to the rows of a descriptor (ld
+// elements): chunk c = tid + 512·q, consecutive lanes on consecutive 16-B pieces of a row
+template <int NCH, int N>
+__device__ __forceinline__ void image_out(const char* smem, __amdgpu_buffer_rsrc_t rs, int ld, int tid_, int q0) {
+    const int tid = opaque(tid_);  // per-thread offsets computed here, not hoisted across the tile loop
+    u32x4 v[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        const int c = tid + 512 * (q0 + q);
+        v[q] = *reinterpret_cast<const u32x4*>(smem + img_off(c / NCH, c % NCH));
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        const int c = tid + 512 * (q0 + q);
+        __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, ((c / NCH) * ld + 8 * (c % NCH)) * 2, 0, 0);
+    }
+}
+
+// layer_mm with drain(group) after each group of TPD k-steps (behind that group's refills); the
+// ring must be primed (layer_prime) by the caller
+template <int NA, typename Drain>
+__device__ __forceinline__ void layer_mm_d(const bf16* __restrict__ wsrc, int nks, const char* smem, int lane,
+                                           f32x16 (&acc)[NA][NJ], u32x4 (&ring)[TPD][NA], Drain&& drain) {
+    const int r32 = lane & 31, h = lane >> 5, sw = r32 & 15;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][j][r] = 0.f;
+    const char* brow = smem + r32 * 1024;
+    bf16x8 bc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
+#pragma unroll 1
+    for (int ks0 = 0; ks0 < nks; ks0 += TPD) {
+#pragma unroll
+        for (int d = 0; d < TPD; ++d) {
+            const int ks = ks0 + d;
+            const int offn = ((2 * (ks + 1) + h) ^ sw) << 4;
+            bf16x8 bn[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int a = 0; a < NA; ++a)
+                    acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ring[d][a]), bc[j],
+                                                                      acc[a][j], 0, 0, 0);
+            const int kn = min(ks + TPD, nks - 1);
+#pragma unroll
+            for (int a = 0; a < NA; ++a) ring[d][a] = ldg16(wsrc + (kn * NA + a) * 512);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x020, NA, 0);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bc[j] = bn[j];
+        }
+        drain(ks0 / TPD);
+    }
+}
+
+// narrow_mm's A fragments loaded ahead (before an epilogue's stores) and the MFMAs on them
+template <int KPER>
+__device__ __forceinline__ void narrow_load(const bf16* __restrict__ a, int lane_, int w, u32x4 (&af)[KPER]) {
+    const int lane = opaque(lane_);
+#pragma unroll
+    for (int d = 0; d < KPER; ++d) af[d] = ldg16(a + (w * KPER + d) * 512 + lane * 8);
+}
+template <int KPER>
+__device__ __forceinline__ void narrow_run(const u32x4 (&af)[KPER], int kb, const char* smem, int lane_, int w, float* part) {
+    const int lane = opaque(lane_), r32 = lane & 31, h = lane >> 5, sw = r32 & 15;
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const char* brow = smem + r32 * 1024;
+#pragma unroll
+    for (int d = 0; d < KPER; ++d) {
+        const int off = ((2 * (kb + w * KPER + d) + h) ^ sw) << 4;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const bf16x8 b = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + off);
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[d]), b, acc[j], 0, 0, 0);
+        }
+    }
+    if (h == 0) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            *reinterpret_cast<f32x4*>(part + (w * TM + 32 * j + r32) * 4) =
+                f32x4{acc[j][0] + acc[j][1], acc[j][2] + acc[j][3], acc[j][4] + acc[j][5], 0.f};
+    }
+}
+
+// the heads' biases staged once per launch (floats): G = [feat | sem hidden], Q, sun_v 2, sun_v 3
+constexpr int SB_G = 0, SB_Q = HW + HH, SB_S2 = SB_Q + 2 * HH, SB_S3 = SB_S2 + HH, SB_N = SB_S3 + HH;
+
+// One 128-point tile of the training heads.  On entry H_L is the [128][512] image at smem,
+// complete and visible; ost[row][3] = softplus(σ pre-activation) of each row (from the trunk's
+// hsave[p·8]); sbias holds the SB_* biases.  mode 0: every head; mode 2 (the solar pass): feat,
+// sun1, sun_v 2 / 3 and the sun, the other output columns zero.  Writes the tile's output rows;
+// every thread of the 8-wave workgroup calls it (it contains barriers).
+// (g.dbg, profiling ablations of the -DSPN_ABLATIONS build, outputs invalid: 1 = no image
+// copy-outs, 2 = no register stores (D, semantic hidden), 8 = no sin / cos in the wide layers'
+// epilogues)
+template <typename GA, typename KA>
+__device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float* ost, float* part, const float* sbias,
+                                                 int64_t p0) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int dbg = g.dbg;
+    const float* Pk = g.packed;
+    const bf16* P16 = reinterpret_cast<const bf16*>(g.packed);
+    const bool full = g.mode == 0;
+    const int C = full ? g.C : 0;
+    const int rows = (int)std::min<int64_t>(TM, g.P - p0);
+    auto stream = [&](int64_t off, int nks, int NA) {
+        return P16 + off + (int64_t)w * nks * NA * 512 + opaque(lane) * 8;
+    };
+    auto rsrc = [&](bf16* base, int ld) {
+        return __builtin_amdgcn_make_buffer_rsrc(base + p0 * ld, 0, (dbg & 1) ? 0 : rows * ld * 2, 0x00020000);
+    };
+    auto rsrc_r = [&](bf16* base, int ld) {  // register stores (dbg 2: dropped)
+        return __builtin_amdgcn_make_buffer_rsrc(base + p0 * ld, 0, (dbg & 2) ? 0 : rows * ld * 2, 0x00020000);
+    };
+    auto sincos = [&](float x, float* sn, float* cs) {
+        if (dbg & 8) {
+            *sn = x;
+            *cs = -x;
+        } else {
+            fast_sincos(x, sn, cs);
+        }
+    };
+    auto put4 = [&](int row, int f0, const float (&y)[4]) {
+        *reinterpret_cast<u32x2*>(smem + img_off(row, f0 >> 3) + 8 * ((f0 >> 2) & 1)) =
+            u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+    };
+    auto nodrain = [](int) {};
+    const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
+
+    u32x4 ring2f[TPD][2];  // feat's weights
+    // semantic hidden = sin(W_m1 H_L + b) → G[:, W..W+H) and DG; its logits' partials → part
+    if (C > 0) {
+        f32x16 acc[1][NJ];
+        u32x4 ring1[TPD][1];
+        layer_prime<1>(stream(k.Fsem16, HW / 16, 1), ring1);
+        layer_mm_d<1>(stream(k.Fsem16, HW / 16, 1), HW / 16, smem, lane, acc, ring1, nodrain);
+        layer_prime<2>(stream(k.Ffeat16, HW / 16, 2), ring2f);
+        const auto rsG = rsrc_r(g.G, g.ldG), rsD = rsrc_r(g.DG, g.ldG);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            u32x2 yq[4], cq[4];
+            float sacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 32 * w + 8 * gq + 4 * eh;
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_G + HW + f0);
+                float y[4], cs[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sincos(acc[0][j][4 * gq + e] + bv[e], &y[e], &cs[e]);
+                yq[gq] = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                cq[gq] = u32x2{pack2(cs[0], cs[1]), pack2(cs[2], cs[3])};
+                const f32x4 yb = raw_f32(yq[gq]);  // the stored (bf16) values feed the logits
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const f32x4 wm = c < C ? ld4(Pk + k.Wm2 + c * HH + f0) : f32x4{0.f, 0.f, 0.f, 0.f};
+                    sacc[c] += (yb[0] * wm[0] + yb[1] * wm[1]) + (yb[2] * wm[2] + yb[3] * wm[3]);
+                }
+            }
+            store_rows16(rsG, g.ldG, HW + 32 * w, 32 * j + er32, eh, yq);
+            store_rows16(rsD, g.ldG, HW + 32 * w, 32 * j + er32, eh, cq);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float t = sacc[c] + __shfl_xor(sacc[c], 32, 64);
+                if (eh == 0 && c < C) part[(w * TM + 32 * j + er32) * 4 + c] = t;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        layer_prime<2>(stream(k.Ffeat16, HW / 16, 2), ring2f);
+    }
+    // feat = W_f H_L + b (linear) → the image (to G[:, 0..W) during Q's k-loop)
+    u32x4 ring2q[TPD][2];  // Q's weights
+    {
+        f32x16 acc[2][NJ];
+        layer_mm_d<2>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc, ring2f, nodrain);
+        layer_prime<2>(stream(k.FQ16, HW / 16, 2), ring2q);
+        __syncthreads();  // every wave is done reading H_L
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_G + f0);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const float y[4] = {acc[a][j][4 * gq] + bv[0], acc[a][j][4 * gq + 1] + bv[1],
+                                        acc[a][j][4 * gq + 2] + bv[2], acc[a][j][4 * gq + 3] + bv[3]};
+                    put4(32 * j + er32, f0, y);
+                }
+            }
+        __syncthreads();
+    }
+    // [sun1 | rgb1] = sin(W_Q feat + b + per-ray sun rows) → the image and DQ; feat leaves for G
+    // in 8 slices behind Q's k-step groups (the solar pass keeps sun1: waves 0..3's features)
+    u32x4 ring1s2[TPD][1];  // sun_v 2's weights
+    u32x4 afr[HH / 16 / 8];  // albedo's narrow A fragments
+    {
+        f32x16 acc[2][NJ];
+        const auto rsF = rsrc(g.G, g.ldG);
+        layer_mm_d<2>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2q,
+                      [&](int grp) { image_out<64, 2>(smem, rsF, g.ldG, tid, 2 * grp); });
+        layer_prime<1>(stream(k.Fs2_16, HH / 16, 1), ring1s2);
+        if (full) narrow_load<HH / 16 / 8>(P16 + k.Fnar16 + narrow_off(1), lane, w, afr);
+        __syncthreads();  // every wave is done reading feat (its copy-out included)
+        const auto rsD = rsrc_r(g.DQ, g.ldQ);
+        const bool dq = full || w < 4;  // wave-uniform
+        const int rlast = (int)(g.P - 1 - p0);  // P < 2^31 / 512 (host check)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                u32x2 cq[4];
+                const int64_t ray = (p0 + std::min(32 * j + er32, rlast)) / g.S;
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                    const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_Q + f0);
+                    const f32x4 rv = ld4(g.rbQ + ray * (2 * HH) + f0);
+                    float y[4], cs[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) sincos((acc[a][j][4 * gq + e] + bv[e]) + rv[e], &y[e], &cs[e]);
+                    put4(32 * j + er32, f0, y);
+                    cq[gq] = u32x2{pack2(cs[0], cs[1]), pack2(cs[2], cs[3])};
+                }
+                if (dq) store_rows16(rsD, g.ldQ, 64 * w + 32 * a, 32 * j + er32, eh, cq);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        __syncthreads();
+    }
+    if (full) {
+        // semantic logits: the 8 waves' partials in wave order
+        for (int i = opaque(tid); i < TM * C; i += 512) {
+            const int r = i / C, c = i % C;
+            float t = 0.f;
+            for (int v = 0; v < 8; ++v) t += part[(v * TM + r) * 4 + c];
+            ost[r * OST_LD + g.sem_col + c] = t + Pk[k.bm2 + c];
+        }
+        __syncthreads();  // the logits are read from part
+        // albedo from rgb1 (image k-steps 16..31) on MFMA; its gates saved for the backward
+        narrow_run<HH / 16 / 8>(afr, HH / 16, smem, lane, w, part);
+        __syncthreads();
+        const int r = opaque(tid);  // (row addresses computed here, not hoisted across the tile loop)
+        if (r < TM) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                float t = 0.f;
+                for (int v = 0; v < 8; ++v) t += part[(v * TM + r) * 4 + c];
+                const float gv = sigmoidf_(t + Pk[k.br2 + c]);
+                ost[r * OST_LD + c] = __fsub_rn(__fmul_rn(gv, 1.002f), 0.001f);
+                if (r < rows) g.hsave[(p0 + r) * 8 + 1 + c] = gv;
+            }
+        }
+    }
+    // sun_v 2 on image columns 0..255 → the image and DS2; Q leaves for HBM behind its k-step groups
+    u32x4 ring1s3[TPD][1];
+    {
+        f32x16 acc[1][NJ];
+        const auto rsQ = rsrc(g.Q, g.ldQ);
+        if (full)
+            layer_mm_d<1>(stream(k.Fs2_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s2,
+                          [&](int grp) { image_out<64, 4>(smem, rsQ, g.ldQ, tid, 4 * grp); });
+        else
+            layer_mm_d<1>(stream(k.Fs2_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s2,
+                          [&](int grp) { image_out<32, 2>(smem, rsQ, g.ldQ, tid, 2 * grp); });
+        layer_prime<1>(stream(k.Fs3_16, HH / 16, 1), ring1s3);
+        __syncthreads();  // every wave is done reading sun1 (and rgb1: the albedo head; Q's copy-out)
+        const auto rsD = rsrc_r(g.DS2, HH);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            u32x2 cq[4];
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 32 * w + 8 * gq + 4 * eh;
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_S2 + f0);
+                float y[4], cs[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sincos(acc[0][j][4 * gq + e] + bv[e], &y[e], &cs[e]);
+                put4(32 * j + er32, f0, y);
+                cq[gq] = u32x2{pack2(cs[0], cs[1]), pack2(cs[2], cs[3])};
+            }
+            store_rows16(rsD, HH, 32 * w, 32 * j + er32, eh, cq);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+    }
+    // sun_v 3 → the image and DS3; S2 leaves behind its k-step groups
+    u32x4 afs[HH / 16 / 8];  // the sun head's narrow A fragments
+    {
+        f32x16 acc[1][NJ];
+        const auto rsS2 = rsrc(g.S2, HH);
+        layer_mm_d<1>(stream(k.Fs3_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s3,
+                      [&](int grp) { image_out<32, 2>(smem, rsS2, HH, tid, 2 * grp); });
+        narrow_load<HH / 16 / 8>(P16 + k.Fnar16 + narrow_off(2), lane, w, afs);
+        __syncthreads();
+        const auto rsD = rsrc_r(g.DS3, HH);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            u32x2 cq[4];
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 32 * w + 8 * gq + 4 * eh;
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_S3 + f0);
+                float y[4], cs[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sincos(acc[0][j][4 * gq + e] + bv[e], &y[e], &cs[e]);
+                put4(32 * j + er32, f0, y);
+                cq[gq] = u32x2{pack2(cs[0], cs[1]), pack2(cs[2], cs[3])};
+            }
+            store_rows16(rsD, HH, 32 * w, 32 * j + er32, eh, cq);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+    }
+    // the sun visibility (MFMA) on S3, then S3 to HBM and, for the main pass, the ray's sky colour
+    narrow_run<HH / 16 / 8>(afs, 0, smem, lane, w, part);
+    image_out<32, 8>(smem, rsrc(g.S3, HH), HH, tid, 0);
+    __syncthreads();
+    const int r = opaque(tid);
+    if (r < TM) {
+        float t = 0.f;
+        for (int v = 0; v < 8; ++v) t += part[(v * TM + r) * 4];
+        const float sun = sigmoidf_(t + Pk[k.bs4]);
+        ost[r * OST_LD + 4] = sun;
+        if (r < rows) g.hsave[(p0 + r) * 8 + 4] = sun;
+        if (full) {
+            const float* sk = g.sky + (std::min<int64_t>(p0 + r, g.P - 1) / g.S) * 4;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) ost[r * OST_LD + 5 + c] = sk[c];
+        } else {
+            for (int c = 0; c < g.NO; ++c)
+                if (c != 3 && c != 4) ost[r * OST_LD + c] = 0.f;
+        }
+    }
+    __syncthreads();
+    for (int i = opaque(tid); i < rows * g.NO; i += 512) g.out[p0 * g.NO + i] = ost[(i / g.NO) * OST_LD + i % g.NO];
+}
+
 }  // namespace hd
 
 // The argument of a fused trunk launch that runs the heads on its last image: the trunk's (first,

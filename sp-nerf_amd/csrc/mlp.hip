@@ -1214,7 +1214,9 @@ int g_tn_k64_pair = 1;  // option "tn_k64_pair": the skip layer's PE tail and fc
 // option "heads_epi": the training forward's narrow heads (rgb, sun, beta, semantic logits; σ and the
 // sky columns with the sun) in the epilogues of the G / Q / sun_v.3 GEMMs instead of k_heads_fwd_v:
 // C4 26.39 / 26.35 -> 26.13 / 26.08 ms (heads_fwd's 0.58 ms for +0.31 ms of epilogue), C4@512
-// 3.950 / 3.945 -> 3.919 / 3.921 ms (same call)
+// 3.950 / 3.945 -> 3.919 / 3.921 ms (same call).  2: the whole training heads (G, Q, sun_v 2 / 3
+// with their saved activations, and the narrow heads) in one LDS-resident launch after the trunk
+// (k_heads_train_bf16, train_heads_on), the epilogue GEMMs where the shape does not fit
 int g_heads_epi = 1;
 int g_ray_tiles_pair = 1;  // option "ray_tiles_pair": the per-ray dZ sums of layer 0 and the skip layer in one launch
 static bool defer_heads_for(int64_t P) { return g_defer_heads == 1 || (g_defer_heads == 2 && P <= (1 << 18)); }
@@ -1413,6 +1415,33 @@ static bool trunk_l0_on(const Ctx& c, bool save) {
            trunk_l0_supported(c.d.K0p, save, c.d.bf && g_zsave);
 }
 
+// option heads_epi 2: the training forward's heads (k_heads_train_bf16) as one launch after the
+// saving trunk, where the shape allows: W = 512, H = 256, no β head, C <= 3
+static bool train_heads_shape(const Ctx& c, int mode) {
+    const Dims& d = c.d;
+    return d.bf && (mode == 0 || mode == 2) && d.W == 512 && d.H == 256 && !d.beta && (!d.sem || d.C <= 3) &&
+           c.k.Ffeat16 >= 0 && c.k.Fnar16 >= 0 && c.out && c.heads_done && !g_zsave;
+}
+static bool train_heads_on(const Ctx& c, int mode) { return g_heads_epi == 2 && train_heads_shape(c, mode); }
+static HeadsFusedArgs heads_args(const Ctx& c, int mode, int64_t hl, double* flop, double* bytes);
+// the training heads' arguments: what they store, and their counted work (the wide layers as
+// computed — the solar pass's Q runs all 2H columns — and the narrow heads; stored: feat (+ the
+// semantic hidden and its D), Q and DQ, S2 / S3 and their D, the output rows, the gates)
+static HeadsFusedArgs train_heads_args(const Ctx& c, int mode, int64_t hl, double* flop, double* bytes) {
+    const Dims& d = c.d;
+    const int64_t P = c.w.P;
+    const int W = d.W, H = d.H;
+    HeadsFusedArgs h = heads_args(c, mode, hl, flop, bytes);
+    h.G = c.hb(c.w.G); h.DG = d.sem ? c.hb(c.w.DG) : nullptr; h.ldG = d.NG;
+    h.Q = c.hb(c.w.Q); h.DQ = c.hb(c.w.DQ); h.ldQ = d.NQ;
+    h.S2 = c.hb(c.w.S2); h.DS2 = c.hb(c.w.DS2); h.S3 = c.hb(c.w.S3); h.DS3 = c.hb(c.w.DS3);
+    h.hsave = c.at(c.w.hsave);
+    const bool m0 = mode == 0, sm = m0 && d.sem;
+    *flop = 2.0 * P * ((double)W * W + 2.0 * H * W + 2.0 * H * H + (sm ? (double)H * W + H * d.C : 0.0) + (m0 ? 3.0 * H : 0.0) + H);
+    *bytes = 2.0 * P * (W + (sm ? 2.0 * H : 0.0) + 2.0 * (m0 ? 2 * H : H) + 4.0 * H) + 4.0 * P * (d.NO + (m0 ? 4 : 1));
+    return h;
+}
+
 // the fused heads' arguments and counted work (k_heads_bf16, or inside the inference trunk)
 static HeadsFusedArgs heads_args(const Ctx& c, int mode, int64_t hl, double* flop, double* bytes) {
     const Dims& d = c.d;
@@ -1553,6 +1582,18 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
     }
     if (mode == 1) return SPNERF_OK;
     if (BF && heads_fused_on(c, save, mode)) return SPNERF_OK;  // G, Q, sun_v 2/3 inside the fused heads
+    if constexpr (BF) {
+        // option heads_epi 2: the training heads as one launch after the trunk (H_L from HBM)
+        if (save && train_heads_on(c, mode) && sig_done && *sig_done) {
+            double hflop = 0.0, hbytes = 0.0;
+            const HeadsFusedArgs h = train_heads_args(c, mode, c.w.Hb[d.L - 1], &hflop, &hbytes);
+            if (heads_train_bf16_ok(h, c.k)) {
+                SPN_TRY(heads_train_bf16(h, c.k, s, hflop, hbytes + 2.0 * P * W));
+                *c.heads_done = true;
+                return SPNERF_OK;
+            }
+        }
+    }
     T* S2buf = save ? G::buf(c, c.w.S2) : G::buf(c, c.w.Hb[((d.L - 1) & 1) ^ 1]);
     T* S3buf = save ? G::buf(c, c.w.S3) : G::buf(c, c.w.Hb[2]);
     // option heads_epi: the narrow heads in the G / Q / sun_v.3 epilogues (bf16 DMA NT with the

@@ -169,12 +169,23 @@ struct HeadsFusedArgs {
     int S = 1, NO = 8, C = 0, sem_col = 8, mode = 0;  // mode: 0 all heads, 1 σ only
     int nt = 0;  // non-temporal loads of HL (g_trunk_nt & 2)
     int dbg = 0;  // profiling ablations (g_heads_dbg; outputs invalid): 2 = no H staging loads
+    // training (k_heads_train_bf16, hd::heads_tile_train; mode 0 or 2 = the solar pass): every
+    // activation the backward reads, at the layer-by-layer GEMMs' addresses —
+    // G = [feat | sem hidden] and DG [P][ldG], Q = [sun1 | rgb1] and DQ [P][ldQ], sun_v 2 / 3 and
+    // their D [P][H]; hsave[p·8] = the heads' saved gates (σ pre-activation written by the trunk)
+    bf16 *G = nullptr, *DG = nullptr, *Q = nullptr, *DQ = nullptr;
+    bf16 *S2 = nullptr, *DS2 = nullptr, *S3 = nullptr, *DS3 = nullptr;
+    float* hsave = nullptr;
+    int ldG = 0, ldQ = 0;
 };
 struct PackedOffs;
 struct Dims;
 bool heads_bf16_shape_ok(const Dims& d);   // the packed layout carries the fused heads' weights
 bool heads_bf16_supported(const Dims& d);  // ... and the option is on
 int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes);
+// training heads as their own launch after the saving trunk (option heads_epi 2): H_L from HBM
+bool heads_train_bf16_ok(const HeadsFusedArgs& h, const PackedOffs& k);
+int32_t heads_train_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes);
 // the inference trunk with the fused heads on its last LDS image (k_trunk2_bf16 HEADS): no H_L in HBM
 extern int g_trunk_heads;
 bool trunk2_heads_ok(const TrunkArgs& a);

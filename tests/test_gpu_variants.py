@@ -448,3 +448,77 @@ def test_heads_in_gemm_epilogue_agree(beta):
         assert torch.isfinite(g1[k]).all(), k
         scale = g0[k].abs().max().item()
         assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
+
+
+def _render_train_heads(opts, sem, n, n_samples, guided):
+    """A bf16 training render (solar pass on, semantic head optional) and its gradients."""
+    old = {k: _lib.get_option(k) for k in opts}
+    for k, v in opts.items():
+        _lib.set_option(k, v)
+    try:
+        args = gu.args_of({"args": dict(n_samples=n_samples, n_importance=0, model="sp-nerf", beta=False,
+                                        guidedsample=guided, sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120,
+                                        noise_std=0.0)})
+        rays = torch.tensor(gu_rays(n, 31), device=DEV)
+        g = torch.Generator(device="cpu").manual_seed(8)
+        kw = {}
+        if guided:
+            kw = dict(valid_depth=(torch.rand(n, generator=g) < 0.7).long().to(DEV),
+                      target_depths=torch.stack([rays[:, 7] * 0.5, torch.ones(n, device=DEV)], 1),
+                      target_std=torch.full((n,), 0.01, device=DEV))
+        labels = torch.randint(0, 3, (n,), generator=g).to(DEV) if sem else None
+        model = make_model(ModelDims(width=512, sem=sem), 9, "bf16")
+        torch.manual_seed(7)
+        res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels, mode="train", **kw)
+        loss = sum((v.float() ** 2).mean() for k, v in sorted(res.items()) if v.requires_grad)
+        loss.backward()
+        torch.cuda.synchronize()
+        return ({k: v.detach().cpu() for k, v in res.items()},
+                {k: p.grad.detach().cpu() for k, p in model.named_parameters() if p.grad is not None})
+    finally:
+        for k, v in old.items():
+            _lib.set_option(k, v)
+
+
+@pytest.mark.parametrize("sem,n,n_samples,guided", [(True, 300, 64, True), (False, 97, 40, False), (True, 97, 40, False)])
+def test_training_heads_kernel_agree(sem, n, n_samples, guided):
+    """Option heads_epi 2: the training heads (G, Q, sun_v 2 / 3 with every saved activation, and
+    the narrow heads) in one LDS-resident launch after the saving trunk, main and solar pass.
+    The wide layers are the layer-by-layer GEMMs' arithmetic, so what the backward reads from them
+    is the same; the narrow heads sum in another fp32 order (MFMA instead of the GEMM epilogues /
+    k_heads_fwd_v): renders and gradients agree to fp32 rounding.  97 rays x 40 samples: a ragged
+    last tile, and a sample count the epilogue heads do not take (their fallback is the reference)."""
+    r0, g0 = _render_train_heads({"heads_epi": 1}, sem, n, n_samples, guided)
+    r1, g1 = _render_train_heads({"heads_epi": 2}, sem, n, n_samples, guided)
+    assert sorted(r0) == sorted(r1) and sorted(g0) == sorted(g1)
+    for k in r0:
+        assert torch.isfinite(r1[k]).all(), k
+        scale = r0[k].abs().max().item()
+        assert (r0[k] - r1[k]).abs().max().item() <= 1e-5 * scale + 1e-7, k
+    # (the narrow heads' weights ride as bf16 hi + lo rows, ~2^-17 relative, as in the inference
+    # heads: per tensor within 5e-4 of its largest entry, the whole gradient within 1e-4)
+    worst, num, den = {}, 0.0, 0.0
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        scale = g0[k].abs().max().item()
+        worst[k] = (g0[k] - g1[k]).abs().max().item() / (scale + 1e-30)
+        num += float(((g0[k] - g1[k]).double() ** 2).sum())
+        den += float((g0[k].double() ** 2).sum())
+    print({k: f"{v:.1e}" for k, v in sorted(worst.items(), key=lambda x: -x[1])[:6]}, (num / den) ** 0.5)
+    assert max(worst.values()) <= 5e-4, worst
+    assert (num / den) ** 0.5 <= 1e-4
+
+
+def test_training_heads_kernel_launches():
+    """heads_epi 2 replaces the forward's head GEMM launches by one heads launch per pass (main
+    and solar)."""
+    from spnerf_amd import _lib as L
+    L.prof_reset()
+    L.prof_enable(True)
+    try:
+        _render_train_heads({"heads_epi": 2}, True, 300, 64, True)
+    finally:
+        L.prof_enable(False)
+    classes = L.prof_classes()
+    assert "heads_train" in classes, classes
+    assert L.prof_read("heads_train")["launches"] == 2   # main and solar pass

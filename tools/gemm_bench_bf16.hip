@@ -321,6 +321,34 @@ int main(int argc, char** argv) {
         printf("%s\n", fails ? "SOME CHECKS FAILED" : "all checks ok");
         return fails ? 1 : 0;
     }
+    if (argc > 3 && !strcmp(argv[3], "epi")) {  // forward sine epilogue share: full vs no epilogue (dbg 2)
+        const int shapes[][3] = {{512, 512, 0}, {768, 512, 512}, {512, 512, 512}, {256, 256, 0}};
+        for (auto& sh : shapes) {
+            const int N = sh[0], K = sh[1];
+            HMat A(P, K, 1.f, 1), B(N, K, 0.1f, 3);
+            bf16 *C, *D;
+            CK(hipMalloc(&C, (size_t)P * N * 2));
+            CK(hipMalloc(&D, (size_t)P * N * 2));
+            std::vector<float> bias(N, 0.01f);
+            float* dbias;
+            CK(hipMalloc(&dbias, N * 4));
+            CK(hipMemcpy(dbias, bias.data(), N * 4, hipMemcpyHostToDevice));
+            NT16Args g;
+            g.A = A.d; g.lda = K; g.K1 = K; g.B = B.d; g.ldb = K; g.C = C; g.ldc = N; g.M = P; g.N = N; g.K = K;
+            g.bias = dbias; g.act = 1; g.w0 = 1.f; g.n_lin = sh[2]; g.Dout = D; g.ld_dout = N;
+            const double full = time_it([&] { gemm_nt_bf16(g, 0, 8); });
+            g.dbg = 2;
+            const double noepi = time_it([&] { gemm_nt_bf16(g, 0, 8); });
+            g.dbg = 0;
+            g.act = 0; g.Dout = nullptr;
+            const double lin = time_it([&] { gemm_nt_bf16(g, 0, 8); });
+            const double gb = ((double)P * K + 2.0 * P * N) * 2 / 1e9;
+            printf("nt8 P=%d N=%d K=%d n_lin=%d: full %.1f us (%.2f TB/s alg), no epilogue %.1f us, linear (C only) %.1f us\n",
+                   P, N, K, sh[2], full, gb / full * 1e3, noepi, lin);
+            CK(hipFree(C)); CK(hipFree(D)); CK(hipFree(dbias));
+        }
+        return 0;
+    }
     if (argc > 3 && !strcmp(argv[3], "z")) {  // saved-Z epilogues / staging only
         check_z(4100);
         check_z(20000);

@@ -46,7 +46,8 @@ def main():
     rays[:, 9] = 1.0
     z = torch.sort(torch.rand(B, S, device=dev), 1)[0].contiguous()
     lab = torch.randint(0, 3, (B,), device=dev)
-    classes = ["trunk_bf16", "trunk_bf16_train", "gemm_nt_bf16", "gemm_nt_f32", "heads_fwd", "heads_fused", "encode"]
+    classes = ["trunk_bf16", "trunk_bf16_train", "heads_train", "gemm_nt_bf16", "gemm_nt_bf16d", "gemm_nt_f32", "heads_fwd",
+               "heads_fused", "encode"]
     for mode in a.modes.split(","):
         for fused in ((1,) if a.option else (1, 0)):
             _lib.set_option("fused_trunk", fused)
