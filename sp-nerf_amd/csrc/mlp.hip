@@ -1216,8 +1216,10 @@ int g_tn_k64_pair = 1;  // option "tn_k64_pair": the skip layer's PE tail and fc
 // C4 26.39 / 26.35 -> 26.13 / 26.08 ms (heads_fwd's 0.58 ms for +0.31 ms of epilogue), C4@512
 // 3.950 / 3.945 -> 3.919 / 3.921 ms (same call).  2: the whole training heads (G, Q, sun_v 2 / 3
 // with their saved activations, and the narrow heads) in one LDS-resident launch after the trunk
-// (k_heads_train_bf16, train_heads_on), the epilogue GEMMs where the shape does not fit
-int g_heads_epi = 1;
+// (k_heads_train_bf16, train_heads_on), the epilogue GEMMs where the shape does not fit: the same
+// step time (C4 25.34 / 25.39 against 25.32 / 25.37 ms, C4@512 3.712 / 3.709 ms, pairs in one
+// call), 2.5 GB fewer HBM bytes per C4 step (PMC 88.3 against 90.8 GB) and 6 fewer launches
+int g_heads_epi = 2;
 int g_ray_tiles_pair = 1;  // option "ray_tiles_pair": the per-ray dZ sums of layer 0 and the skip layer in one launch
 static bool defer_heads_for(int64_t P) { return g_defer_heads == 1 || (g_defer_heads == 2 && P <= (1 << 18)); }
 
