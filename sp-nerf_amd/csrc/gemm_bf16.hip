@@ -897,7 +897,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
                         out[3] = softplusf_(hs[0]);
                         if (H.full) {
 #pragma unroll
-                            for (int c = 0; c < 3; ++c) out[5 + c] = ldgf(H.sky + (p / H.S) * 4 + c);
+                            for (int c = 0; c < 3; ++c) out[5 + c] = ldgf(H.sky + (int64_t)((int)p / H.S) * 4 + c);
                         } else {
                             for (int c = 0; c < H.NO; ++c)
                                 if (c != 3 && c != 4) out[c] = 0.f;

@@ -145,6 +145,7 @@ int32_t heads_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, 
     SPN_ARG(a.mode == 1 || (k.Ffeat16 >= 0 && k.FQ16 >= 0 && k.Fs2_16 >= 0 && k.Fs3_16 >= 0 && (a.C == 0 || k.Fsem16 >= 0)),
             "heads_bf16: weights not packed for the fused heads");
     if (a.P == 0) return SPNERF_OK;
+    SPN_ARG(a.P < (1ll << 31) / HW, "heads_bf16: too many points (%lld)", (long long)a.P);
     const int ntiles = (int)((a.P + TM - 1) / TM);
     HeadsFusedArgs ad = a;
     ad.nt = (g_trunk_nt >> 1) & 1;

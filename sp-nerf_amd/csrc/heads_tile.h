@@ -168,8 +168,8 @@ __device__ __forceinline__ void heads_tile(GA& g, KA& k, char* smem, float* ost,
     // the tile's rays' sun rows of Q into LDS when they are few (one ray per tile at 128
     // samples per ray): the Q epilogue then reads LDS instead of an L2 round trip per row (read
     // after the barriers that follow the σ head)
-    const int64_t ray0 = p0 / g.S;
-    const int nray = (int)((std::min<int64_t>(p0 + TM, (int64_t)g.P) - 1) / g.S - ray0) + 1;
+    const int64_t ray0 = (int)p0 / g.S;  // P < 2^31 / 512 (host checks): 32-bit divisions
+    const int nray = (int)((int)(std::min<int64_t>(p0 + TM, (int64_t)g.P) - 1) / g.S - ray0) + 1;
     const bool rq_lds = RQ && full && nray <= RQ_RAYS && !(g.dbg & 4);  // block-uniform (dbg 4: A/B)
     if (rq_lds)
         for (int i = tid; i < nray * 2 * HH; i += 512) srq[i] = g.rbQ[ray0 * (2 * HH) + i];
@@ -248,7 +248,7 @@ __device__ __forceinline__ void heads_tile(GA& g, KA& k, char* smem, float* ost,
             const int er32 = opaque(lane) & 31;
             int rrel[NJ];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) rrel[j] = (int)(std::min<int64_t>(p0 + 32 * j + er32, g.P - 1) / g.S - ray0);
+            for (int j = 0; j < NJ; ++j) rrel[j] = (int)std::min<int64_t>(p0 + 32 * j + er32, g.P - 1) / g.S - (int)ray0;
             // two instances of the epilogue (block-uniform choice): one select between the LDS
             // and the global row made hipcc emit a flat load, waited with vmcnt(0) lgkmcnt(0)
             // per 4 outputs
@@ -312,7 +312,7 @@ __device__ __forceinline__ void heads_tile(GA& g, KA& k, char* smem, float* ost,
             float t = 0.f;
             for (int v = 0; v < 8; ++v) t += part[(v * TM + tid) * 4];
             ost[tid * OST_LD + 4] = sigmoidf_(t + Pk[k.bs4]);
-            const float* sk = g.sky + (std::min<int64_t>(p0 + tid, g.P - 1) / g.S) * 4;
+            const float* sk = g.sky + (int64_t)((int)std::min<int64_t>(p0 + tid, g.P - 1) / g.S) * 4;
 #pragma unroll
             for (int c = 0; c < 3; ++c) ost[tid * OST_LD + 5 + c] = sk[c];
         }
@@ -586,7 +586,7 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 u32x2 cq[4];
-                const int64_t ray = (p0 + std::min(32 * j + er32, rlast)) / g.S;
+                const int64_t ray = ((int)p0 + std::min(32 * j + er32, rlast)) / g.S;
 #pragma unroll
                 for (int gq = 0; gq < 4; ++gq) {
                     const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
@@ -699,7 +699,7 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
         ost[r * OST_LD + 4] = sun;
         if (r < rows) g.hsave[(p0 + r) * 8 + 4] = sun;
         if (full) {
-            const float* sk = g.sky + (std::min<int64_t>(p0 + r, g.P - 1) / g.S) * 4;
+            const float* sk = g.sky + (int64_t)((int)std::min<int64_t>(p0 + r, g.P - 1) / g.S) * 4;
 #pragma unroll
             for (int c = 0; c < 3; ++c) ost[r * OST_LD + 5 + c] = sk[c];
         } else {

@@ -211,7 +211,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 const int64_t pr = std::min<int64_t>(p0 + row, g.P - 1);
                 float xv[8];
                 if (g.rays) {  // block-uniform: encode o + dir·z here (pe_value, as k_encode)
-                    const float* ray = g.rays + (pr / g.S) * g.rs;
+                    const float* ray = g.rays + (int64_t)((int)pr / g.S) * g.rs;
                     const float zz = g.z[pr];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) xv[e] = pe_value(ray, g.dir_off, zz, q * 8 + e, g.n_freq, g.K0);
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
 #pragma unroll
                             for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] + bv[e];
                             if constexpr (RB) {
-                                const f32x4 rv = ld4(rb + (std::min<int64_t>(p0 + row, g.P - 1) / g.S) * TW + f0);
+                                const f32x4 rv = ld4(rb + (int64_t)((int)std::min<int64_t>(p0 + row, g.P - 1) / g.S) * TW + f0);  // P < 2^31 / 512: 32-bit division
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) v[e] += rv[e];
                             }
