@@ -86,26 +86,34 @@ __global__ __launch_bounds__(512) void k_heads_train_bf16(HeadsFusedArgs g, Pack
                  : i < SB_S2 ? P[k.bQ + (i - SB_Q)] : i < SB_S3 ? P[k.bs2 + (i - SB_S2)] : P[k.bs3 + (i - SB_S3)];
     }
     __syncthreads();
-    for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < ntiles; tile += gridDim.x) {
+    // H_L rows of a tile into registers (the next tile's under the current tile's last phases)
+    u32x4 hv[16];
+    auto load_hl = [&](int64_t q0) {
+        const int t = opaque(tid);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int c = t + 512 * q, row = c >> 6, ch = c & 63;
+            hv[q] = *reinterpret_cast<const u32x4*>(g.HL + std::min<int64_t>(q0 + row, g.P - 1) * HW + ch * 8);
+        }
+    };
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    if (tile < ntiles) load_hl((int64_t)tile * TM);
+    for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TM;
+        {
+            const int t = opaque(tid);
 #pragma unroll
-        for (int q0 = 0; q0 < 16; q0 += 8) {
-            u32x4 v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int c = tid + 512 * (q0 + q), row = c >> 6, ch = c & 63;
-                v[q] = *reinterpret_cast<const u32x4*>(g.HL + std::min<int64_t>(p0 + row, g.P - 1) * HW + ch * 8);
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int c = tid + 512 * (q0 + q), row = c >> 6, ch = c & 63;
-                *reinterpret_cast<u32x4*>(smem + img_off(row, ch)) = v[q];
+            for (int q = 0; q < 16; ++q) {
+                const int c = t + 512 * q, row = c >> 6, ch = c & 63;
+                *reinterpret_cast<u32x4*>(smem + img_off(row, ch)) = hv[q];
             }
         }
         const int r = opaque(tid);
         if (r < TM) ost[r * OST_LD + 3] = softplusf_(g.hsave[std::min<int64_t>(p0 + r, g.P - 1) * 8]);
         __syncthreads();
-        heads_tile_train(g, k, smem, ost, part, sbias, p0);
+        const int next = tile + (int)gridDim.x;
+        // (past the last tile: this tile's rows again, never stored — no branch around the loads)
+        heads_tile_train(g, k, smem, ost, part, sbias, p0, [&] { load_hl((int64_t)std::min(next, ntiles - 1) * TM); });
         __syncthreads();  // the next tile restages the image
     }
 }

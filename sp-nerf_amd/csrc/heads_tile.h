@@ -378,11 +378,21 @@ __device__ __forceinline__ void image_out(const char* smem, __amdgpu_buffer_rsrc
     }
 }
 
-// layer_mm with drain(group) after each group of TPD k-steps (behind that group's refills); the
-// ring must be primed (layer_prime) by the caller
-template <int NA, typename Drain>
+// layer_prime / layer_mm with a ring of DEPTH k-steps (the 256-wide layers run 8 deep: half the
+// MFMAs per k-step of the 512-wide ones, the same register cost and time of cover), drain(group)
+// after each group of DEPTH k-steps (behind that group's refills); the ring must be primed
+// (layer_prime_n) by the caller
+template <int NA, int DEPTH>
+__device__ __forceinline__ void layer_prime_n(const bf16* __restrict__ wsrc, u32x4 (&ring)[DEPTH][NA]) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) ring[d][a] = ldg16(wsrc + (d * NA + a) * 512);
+}
+template <int NA, int DEPTH, typename Drain>
 __device__ __forceinline__ void layer_mm_d(const bf16* __restrict__ wsrc, int nks, const char* smem, int lane,
-                                           f32x16 (&acc)[NA][NJ], u32x4 (&ring)[TPD][NA], Drain&& drain) {
+                                           f32x16 (&acc)[NA][NJ], u32x4 (&ring)[DEPTH][NA], Drain&& drain) {
+    constexpr int TPD = DEPTH;
     const int r32 = lane & 31, h = lane >> 5, sw = r32 & 15;
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -469,9 +479,10 @@ constexpr int SB_G = 0, SB_Q = HW + HH, SB_S2 = SB_Q + 2 * HH, SB_S3 = SB_S2 + H
 // (g.dbg, profiling ablations of the -DSPN_ABLATIONS build, outputs invalid: 1 = no image
 // copy-outs, 2 = no register stores (D, semantic hidden), 8 = no sin / cos in the wide layers'
 // epilogues)
-template <typename GA, typename KA>
+template <typename GA, typename KA, typename Prefetch>
 __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float* ost, float* part, const float* sbias,
-                                                 int64_t p0) {
+                                                 int64_t p0, Prefetch&& prefetch) {
+    constexpr int D1 = 8;  // ring depth of the 256-wide layers (sem hidden, sun_v 2 / 3)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int dbg = g.dbg;
     const float* Pk = g.packed;
@@ -507,10 +518,10 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     // semantic hidden = sin(W_m1 H_L + b) → G[:, W..W+H) and DG; its logits' partials → part
     if (C > 0) {
         f32x16 acc[1][NJ];
-        u32x4 ring1[TPD][1];
-        layer_prime<1>(stream(k.Fsem16, HW / 16, 1), ring1);
-        layer_mm_d<1>(stream(k.Fsem16, HW / 16, 1), HW / 16, smem, lane, acc, ring1, nodrain);
-        layer_prime<2>(stream(k.Ffeat16, HW / 16, 2), ring2f);
+        u32x4 ring1[D1][1];
+        layer_prime_n<1, D1>(stream(k.Fsem16, HW / 16, 1), ring1);
+        layer_mm_d<1, D1>(stream(k.Fsem16, HW / 16, 1), HW / 16, smem, lane, acc, ring1, nodrain);
+        layer_prime_n<2, TPD>(stream(k.Ffeat16, HW / 16, 2), ring2f);
         const auto rsG = rsrc_r(g.G, g.ldG), rsD = rsrc_r(g.DG, g.ldG);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -542,14 +553,14 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
             __builtin_amdgcn_sched_barrier(0);
         }
     } else {
-        layer_prime<2>(stream(k.Ffeat16, HW / 16, 2), ring2f);
+        layer_prime_n<2, TPD>(stream(k.Ffeat16, HW / 16, 2), ring2f);
     }
     // feat = W_f H_L + b (linear) → the image (to G[:, 0..W) during Q's k-loop)
     u32x4 ring2q[TPD][2];  // Q's weights
     {
         f32x16 acc[2][NJ];
-        layer_mm_d<2>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc, ring2f, nodrain);
-        layer_prime<2>(stream(k.FQ16, HW / 16, 2), ring2q);
+        layer_mm_d<2, TPD>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc, ring2f, nodrain);
+        layer_prime_n<2, TPD>(stream(k.FQ16, HW / 16, 2), ring2q);
         __syncthreads();  // every wave is done reading H_L
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -568,14 +579,14 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     }
     // [sun1 | rgb1] = sin(W_Q feat + b + per-ray sun rows) → the image and DQ; feat leaves for G
     // in 8 slices behind Q's k-step groups (the solar pass keeps sun1: waves 0..3's features)
-    u32x4 ring1s2[TPD][1];  // sun_v 2's weights
+    u32x4 ring1s2[D1][1];  // sun_v 2's weights
     u32x4 afr[HH / 16 / 8];  // albedo's narrow A fragments
     {
         f32x16 acc[2][NJ];
         const auto rsF = rsrc(g.G, g.ldG);
-        layer_mm_d<2>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2q,
-                      [&](int grp) { image_out<64, 2>(smem, rsF, g.ldG, tid, 2 * grp); });
-        layer_prime<1>(stream(k.Fs2_16, HH / 16, 1), ring1s2);
+        layer_mm_d<2, TPD>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2q,
+                           [&](int grp) { image_out<64, 2>(smem, rsF, g.ldG, tid, 2 * grp); });
+        layer_prime_n<1, D1>(stream(k.Fs2_16, HH / 16, 1), ring1s2);
         if (full) narrow_load<HH / 16 / 8>(P16 + k.Fnar16 + narrow_off(1), lane, w, afr);
         __syncthreads();  // every wave is done reading feat (its copy-out included)
         const auto rsD = rsrc_r(g.DQ, g.ldQ);
@@ -628,17 +639,17 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
         }
     }
     // sun_v 2 on image columns 0..255 → the image and DS2; Q leaves for HBM behind its k-step groups
-    u32x4 ring1s3[TPD][1];
+    u32x4 ring1s3[D1][1];
     {
         f32x16 acc[1][NJ];
         const auto rsQ = rsrc(g.Q, g.ldQ);
         if (full)
-            layer_mm_d<1>(stream(k.Fs2_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s2,
-                          [&](int grp) { image_out<64, 4>(smem, rsQ, g.ldQ, tid, 4 * grp); });
+            layer_mm_d<1, D1>(stream(k.Fs2_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s2,
+                              [&](int grp) { image_out<64, 8>(smem, rsQ, g.ldQ, tid, 8 * grp); });
         else
-            layer_mm_d<1>(stream(k.Fs2_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s2,
-                          [&](int grp) { image_out<32, 2>(smem, rsQ, g.ldQ, tid, 2 * grp); });
-        layer_prime<1>(stream(k.Fs3_16, HH / 16, 1), ring1s3);
+            layer_mm_d<1, D1>(stream(k.Fs2_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s2,
+                              [&](int grp) { image_out<32, 4>(smem, rsQ, g.ldQ, tid, 4 * grp); });
+        layer_prime_n<1, D1>(stream(k.Fs3_16, HH / 16, 1), ring1s3);
         __syncthreads();  // every wave is done reading sun1 (and rgb1: the albedo head; Q's copy-out)
         const auto rsD = rsrc_r(g.DS2, HH);
 #pragma unroll
@@ -664,8 +675,8 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     {
         f32x16 acc[1][NJ];
         const auto rsS2 = rsrc(g.S2, HH);
-        layer_mm_d<1>(stream(k.Fs3_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s3,
-                      [&](int grp) { image_out<32, 2>(smem, rsS2, HH, tid, 2 * grp); });
+        layer_mm_d<1, D1>(stream(k.Fs3_16, HH / 16, 1), HH / 16, smem, lane, acc, ring1s3,
+                          [&](int grp) { image_out<32, 4>(smem, rsS2, HH, tid, 4 * grp); });
         narrow_load<HH / 16 / 8>(P16 + k.Fnar16 + narrow_off(2), lane, w, afs);
         __syncthreads();
         const auto rsD = rsrc_r(g.DS3, HH);
@@ -687,6 +698,8 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
         }
         __syncthreads();
     }
+    // the next tile's H_L rows start loading (into the caller's registers) under the last phases
+    prefetch();
     // the sun visibility (MFMA) on S3, then S3 to HBM and, for the main pass, the ray's sky colour
     narrow_run<HH / 16 / 8>(afs, 0, smem, lane, w, part);
     image_out<32, 8>(smem, rsrc(g.S3, HH), HH, tid, 0);
