@@ -75,6 +75,10 @@ struct TrunkGeo {
     static constexpr int BIAS_OFF = X0_OFF + TMt * 64 * 2;     // K0p <= 64
     static constexpr int LDS = BIAS_OFF + 2 * TW * 4;
     static constexpr int CPT = TMt * 64 / 512;                 // 16-B chunks of an image per thread
+    // the per-ray rows of a layer with them (layer 0, the skip layer) for the tile's first SRB_RAYS
+    // rays, staged by LDS-DMA at the layer's top (kernels without the fused heads: after LDS)
+    static constexpr int SRB_RAYS = 4;
+    static constexpr int SRB_BYTES = SRB_RAYS * TW * 4;
 };
 
 __device__ __forceinline__ int act_off(int row, int ch) { return row * 1024 + ((ch ^ (row & 15)) << 4); }
@@ -104,7 +108,9 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
     // (VAR 2048: the saving launches of the 128-point tiling as their own instance — the same code,
     // so rocprof tells the training launches from the inference ones by name)
     static_assert(!(VAR & 2048) || TMt == 128, "the 128-point training instance");
-    __shared__ __attribute__((aligned(16))) char smem[Geo::LDS + (HEADS ? hd::OST_BYTES : 0)];
+    constexpr bool SRB = !HEADS;  // per-ray rows staged in LDS (the fused heads' kernel has no room)
+    __shared__ __attribute__((aligned(16))) char smem[Geo::LDS + (HEADS ? hd::OST_BYTES : Geo::SRB_BYTES)];
+    float* srb = reinterpret_cast<float*>(smem + Geo::LDS);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     float* sbias = reinterpret_cast<float*>(smem + Geo::BIAS_OFF);
     char* sx0 = smem + Geo::X0_OFF;
@@ -196,6 +202,9 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
     if constexpr (!HEADS) prime(first, std::integral_constant<int, 0>{}, std::integral_constant<int, TPD>{});
+    // the next layer's bias, loaded behind a layer's k-loop (before its epilogue's stores, so the
+    // wait for it at the next layer's top does not wait for those stores as well)
+    float bpre = ka->bias[first][tid];
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TMt;
         const int st = opaque(tid);
@@ -278,7 +287,21 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             const bf16* wnxt = inext >= 0 ? wstream(inext) : wsrc;
             const int nkm = i == 0 ? nk0 : nmain;  // k-steps over the image
             float* sb = sbias + (i & 1) * TW;  // slot (i-1)&1 may still be read by the previous epilogue
-            sb[tid] = ka->bias[i][tid];
+            sb[tid] = bpre;
+            // this layer's per-ray rows (block-uniform): into LDS by DMA now, the oldest loads of
+            // the layer, so the k-loop's refill waits cover them and the epilogue reads LDS (a
+            // global load there was waited for with everything in flight: refills and copy-outs)
+            const float* rbl = i == 0 ? g.rb0 : (i == g.skip ? g.rb_skip : nullptr);
+            const int ray0 = (int)p0 / g.S, rayl = (int)(std::min<int64_t>(p0 + TMt, g.P) - 1) / g.S;
+            const bool srb_on = SRB && rbl && rayl - ray0 < Geo::SRB_RAYS;
+            if (srb_on) {
+                typedef __attribute__((address_space(3))) void* lds_ptr_t;
+                typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+                // wave w: row w / 2, floats 256·(w % 2) .. +255, 16 B per lane
+                const int rr = w >> 1;
+                const float* src = rbl + (int64_t)std::min(ray0 + rr, rayl) * TW + 256 * (w & 1) + 4 * opaque(lane);
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(srb + rr * TW + 256 * (w & 1)), 16, 0, 0);
+            }
             f32x16 acc[2][NJ];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -363,6 +386,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 }
             }
 
+            bpre = ka->bias[inext >= 0 ? inext : first][tid];
             __syncthreads();  // every wave is done reading the images of layer i
             bf16* Hs = ka->Hs[i];
             bf16* Ds = ka->Ds[i];
@@ -373,7 +397,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             // kpass 0: cos (or Z) into the image (TMt = 128 when saving: it leaves between two
             // barriers); 1: sin into the image; 2: sin into the image and cos (or Z) into the D image
             // kl0: layer 0 (SIREN w0 = 30 of fc_net.0; ×1 elsewhere, exact, so not multiplied)
-            auto epilogue = [&](auto kpass, auto kl0, auto krb) {
+            auto epilogue = [&](auto kpass, auto kl0, auto krb, auto klds) {
                 if constexpr (NOEPI) {  // keep the accumulators (and so the MFMAs) live
                     float t = 0.f;
 #pragma unroll
@@ -386,6 +410,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 constexpr int pass = decltype(kpass)::value;
                 constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
                 constexpr bool RB = decltype(krb)::value;  // per-ray rows (layer 0, the skip layer)
+                constexpr bool RBL = decltype(klds)::value;  // ... staged in LDS (srb)
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
@@ -400,7 +425,9 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
 #pragma unroll
                             for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] + bv[e];
                             if constexpr (RB) {
-                                const f32x4 rv = ld4(rb + (int64_t)((int)std::min<int64_t>(p0 + row, g.P - 1) / g.S) * TW + f0);  // P < 2^31 / 512: 32-bit division
+                                const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
+                                const f32x4 rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
+                                                     : ld4(rb + (int64_t)ray * TW + f0);
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) v[e] += rv[e];
                             }
@@ -435,13 +462,18 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             // block-uniform choices of compile-time instances: a load behind a runtime branch would
             // be waited for with vmcnt(0) — every refill and copy-out store in flight
             auto epi = [&](auto kpass) {
+                const std::false_type F{};
+                const std::true_type T{};
                 if (i == 0) {
-                    if (rb) epilogue(kpass, std::true_type{}, std::true_type{});
-                    else epilogue(kpass, std::true_type{}, std::false_type{});
+                    if (rb && srb_on) epilogue(kpass, T, T, T);
+                    else if (rb) epilogue(kpass, T, T, F);
+                    else epilogue(kpass, T, F, F);
+                } else if (rb && srb_on) {
+                    epilogue(kpass, F, T, T);
                 } else if (rb) {
-                    epilogue(kpass, std::false_type{}, std::true_type{});
+                    epilogue(kpass, F, T, F);
                 } else {
-                    epilogue(kpass, std::false_type{}, std::false_type{});
+                    epilogue(kpass, F, F, F);
                 }
             };
             // DREG: sin → the image as above, D = cos (×w0 at layer 0) straight from the registers
@@ -658,23 +690,27 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
     int tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;  // block-uniform
     prime(g.L - 1);
+    // a tile's dZ_{L-1} rows in registers: the next tile's load at the end of this tile's layer
+    // loop, before its last copy-out (the wait for them at the next tile's top does not wait for
+    // those stores as well, and their HBM latency runs under the copy-out)
+    u32x4 tv[CPT];
+    auto load_top = [&](int64_t q0) {
+        const int st = opaque(tid);
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const int c = st + 512 * q;
+            tv[q] = ldg16(g.dZtop + std::min<int64_t>(q0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
+        }
+    };
+    load_top((int64_t)tile * TMt);
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t p0 = (int64_t)tile * TMt;
         {
             const int st = opaque(tid);
 #pragma unroll
-            for (int q0 = 0; q0 < CPT; q0 += 8) {
-                u32x4 v[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int c = st + 512 * (q0 + q);
-                    v[q] = ldg16(g.dZtop + std::min<int64_t>(p0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
-                }
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int c = st + 512 * (q0 + q);
-                    *reinterpret_cast<u32x4*>(smem + act_off(c >> 6, c & 63)) = v[q];
-                }
+            for (int q = 0; q < CPT; ++q) {
+                const int c = st + 512 * q;
+                *reinterpret_cast<u32x4*>(smem + act_off(c >> 6, c & 63)) = tv[q];
             }
         }
         // this tile's D_{l} rows (rows past P: a clamped row), in registers until the k-loop of
@@ -823,6 +859,8 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
             }
             pend = DREG ? nullptr : ka->dZ[i - 1];
         }
+        // (past the last tile: this tile's rows again, never used — no branch around the loads)
+        load_top((int64_t)std::min(tile + (int)gridDim.x, ntiles - 1) * TMt);
         __syncthreads();  // dZ_0 is complete
 #pragma unroll
         for (int k = 0; k < 2; ++k)
