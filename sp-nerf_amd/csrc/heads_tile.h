@@ -468,6 +468,11 @@ __device__ __forceinline__ void narrow_run(const u32x4 (&af)[KPER], int kb, cons
     }
 }
 
+// ring depth of the training heads' 512-wide layers (8: 43 VGPRs spilled, main pass 1.69 against
+// 1.50 ms per 524 288 points)
+#ifndef SPN_HEADS_D2
+#define SPN_HEADS_D2 4
+#endif
 // the heads' biases staged once per launch (floats): G = [feat | sem hidden], Q, sun_v 2, sun_v 3
 constexpr int SB_G = 0, SB_Q = HW + HH, SB_S2 = SB_Q + 2 * HH, SB_S3 = SB_S2 + HH, SB_N = SB_S3 + HH;
 
@@ -483,6 +488,7 @@ template <typename GA, typename KA, typename Prefetch>
 __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float* ost, float* part, const float* sbias,
                                                  int64_t p0, Prefetch&& prefetch) {
     constexpr int D1 = 8;  // ring depth of the 256-wide layers (sem hidden, sun_v 2 / 3)
+    constexpr int D2 = SPN_HEADS_D2;  // ... of the 512-wide ones (feat, Q)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int dbg = g.dbg;
     const float* Pk = g.packed;
@@ -514,14 +520,14 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     auto nodrain = [](int) {};
     const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
 
-    u32x4 ring2f[TPD][2];  // feat's weights
+    u32x4 ring2f[D2][2];  // feat's weights
     // semantic hidden = sin(W_m1 H_L + b) → G[:, W..W+H) and DG; its logits' partials → part
     if (C > 0) {
         f32x16 acc[1][NJ];
         u32x4 ring1[D1][1];
         layer_prime_n<1, D1>(stream(k.Fsem16, HW / 16, 1), ring1);
         layer_mm_d<1, D1>(stream(k.Fsem16, HW / 16, 1), HW / 16, smem, lane, acc, ring1, nodrain);
-        layer_prime_n<2, TPD>(stream(k.Ffeat16, HW / 16, 2), ring2f);
+        layer_prime_n<2, D2>(stream(k.Ffeat16, HW / 16, 2), ring2f);
         const auto rsG = rsrc_r(g.G, g.ldG), rsD = rsrc_r(g.DG, g.ldG);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -553,14 +559,14 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
             __builtin_amdgcn_sched_barrier(0);
         }
     } else {
-        layer_prime_n<2, TPD>(stream(k.Ffeat16, HW / 16, 2), ring2f);
+        layer_prime_n<2, D2>(stream(k.Ffeat16, HW / 16, 2), ring2f);
     }
     // feat = W_f H_L + b (linear) → the image (to G[:, 0..W) during Q's k-loop)
-    u32x4 ring2q[TPD][2];  // Q's weights
+    u32x4 ring2q[D2][2];  // Q's weights
     {
         f32x16 acc[2][NJ];
-        layer_mm_d<2, TPD>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc, ring2f, nodrain);
-        layer_prime_n<2, TPD>(stream(k.FQ16, HW / 16, 2), ring2q);
+        layer_mm_d<2, D2>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc, ring2f, nodrain);
+        layer_prime_n<2, D2>(stream(k.FQ16, HW / 16, 2), ring2q);
         __syncthreads();  // every wave is done reading H_L
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -584,8 +590,11 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     {
         f32x16 acc[2][NJ];
         const auto rsF = rsrc(g.G, g.ldG);
-        layer_mm_d<2, TPD>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2q,
-                           [&](int grp) { image_out<64, 2>(smem, rsF, g.ldG, tid, 2 * grp); });
+        layer_mm_d<2, D2>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2q,
+                           [&](int grp) {
+                               constexpr int PER = 16 / (HW / 16 / D2);  // feat's 16 chunks per thread over Q's groups
+                               image_out<64, PER>(smem, rsF, g.ldG, tid, PER * grp);
+                           });
         layer_prime_n<1, D1>(stream(k.Fs2_16, HH / 16, 1), ring1s2);
         if (full) narrow_load<HH / 16 / 8>(P16 + k.Fnar16 + narrow_off(1), lane, w, afr);
         __syncthreads();  // every wave is done reading feat (its copy-out included)
