@@ -104,6 +104,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
     static_assert(!HEADS || (TMt == 128 && Geo::BIAS_OFF - Geo::X0_OFF >= hd::PART_BYTES &&
                              Geo::LDS + hd::OST_BYTES <= 160 * 1024), "the fused heads: 128-point tiles, LDS");
     constexpr bool NOMF = VAR & 16, NOSIN = VAR & 32, NOW = VAR & 64, NOB = VAR & 128, NOEPI = VAR & 256;
+    constexpr bool NOPE = VAR & 8192;  // ablation (outputs invalid): the inline encoding's math skipped
     constexpr bool DREG = Geo::DIMG && (VAR & 512);  // D from the registers (see epilogue_dreg)
     // (VAR 2048: the saving launches of the 128-point tiling as their own instance — the same code,
     // so rocprof tells the training launches from the inference ones by name)
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                     const float* ray = g.rays + (int64_t)((int)pr / g.S) * g.rs;
                     const float zz = g.z[pr];
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) xv[e] = pe_value(ray, g.dir_off, zz, q * 8 + e, g.n_freq, g.K0);
+                    for (int e = 0; e < 8; ++e) xv[e] = NOPE ? ray[e & 3] * zz : pe_value(ray, g.dir_off, zz, q * 8 + e, g.n_freq, g.K0);
                 } else {
                     const float* src = g.X0 + pr * g.K0p + q * 8;
                     const f32x4 v0 = ld4(src), v1 = ld4(src + 4);
@@ -997,6 +998,7 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     else if (tm == 128 && g_trunk_var == 128) hipLaunchKernelGGL((k_trunk_bf16<128, 128>), grid, block, 0, s, ad, ntiles);
     else if (tm == 128 && g_trunk_var == 256) hipLaunchKernelGGL((k_trunk_bf16<128, 256>), grid, block, 0, s, ad, ntiles);
     else if (tm == 128 && g_trunk_var == 464) hipLaunchKernelGGL((k_trunk_bf16<128, 464>), grid, block, 0, s, ad, ntiles);
+    else if (tm == 128 && save && g_trunk_var == 8192) hipLaunchKernelGGL((k_trunk_bf16<128, 2048 | 8192>), grid, block, 0, s, ad, ntiles);
     else done = false;
 #endif
     if (!done) {
