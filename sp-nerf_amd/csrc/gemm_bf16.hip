@@ -1610,6 +1610,26 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
             for (int e = 0; e < 8; ++e) bs[e] += f[e];
         }
     };
+    // the same sums split in two: the stage's rows read at its top (their latency runs with the
+    // fragment reads' and is covered by the same waits), added after its MFMAs — read and added in
+    // one place, each read was waited for on its own (lgkmcnt(0)) after the MFMAs: 8% of the kernel
+    // (tools/tn_lab mode 8).  Same rows, same order of additions: bitwise the same sums
+    auto bias_load = [&](int stg, u32x4 (&v)[TD_STEP / 16]) {
+        const char* sA = smem + stg * TD_STG + (ch >> 4) * HALF;
+#pragma unroll
+        for (int i = 0; i < TD_STEP / 16; ++i)
+            if (i == 0 || !bsplit) v[i] = *reinterpret_cast<const u32x4*>(sA + tn_off(lrow + 16 * i, ch & 15));
+    };
+    auto bias_add = [&](const u32x4 (&v)[TD_STEP / 16]) {
+#pragma unroll
+        for (int i = 0; i < TD_STEP / 16; ++i) {
+            if (i > 0 && bsplit) break;
+            float f[8];
+            unpack8(v[i], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bs[e] += f[e];
+        }
+    };
 
     // PF: fragments of one k-step (16 points) of stage stg into a register set; MFMAs from one
     struct Frag {
@@ -1744,8 +1764,13 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
             auto nxt = [&](int) { issue(min(st + 3, ns - 1), (st + 3) % TD_STAGES); };
             auto nxt1 = [&](int i) { issue1(min(st + 3, ns - 1), (st + 3) % TD_STAGES, i); };
             if constexpr (IP == 3) {
+                u32x4 bv[TD_STEP / 16];
+                if (do_bias) bias_load(st % TD_STAGES, bv);  // block-uniform
                 compute(st % TD_STAGES, nxt1);
                 ND_STAMP(7);
+                if (do_bias) bias_add(bv);
+                ND_STAMP(8);
+                continue;
             } else if constexpr (IP == 2) {
                 compute(st % TD_STAGES, nxt);
             } else if constexpr (IP == 1) {

@@ -195,8 +195,22 @@ int main(int argc, char** argv) {
     }
 #endif
     // profiling mode (argv[3]): one configuration only, for PMC passes — 1 DMA one-row, 2 quad
-    // one-row, 3 DMA, 4 quad, 5 prefetched one-row, 6 16x16x32 one-row, 7 16x16x32
+    // one-row, 3 DMA, 4 quad, 5 prefetched one-row, 6 16x16x32 one-row, 7 16x16x32; 8 / 9: the
+    // library kernel with / without the bias sums, alternating (what the bias rows cost)
     const int mode = argc > 3 ? atoi(argv[3]) : 0;
+    if (mode == 8) {
+        TN16Args t;
+        t.A = dA; t.lda = N; t.B = dB; t.ldb = K; t.K1 = K;
+        t.slab = slab; t.ld_slab = K; t.slab_stride = (int64_t)N * K;
+        t.P = P; t.N = N; t.K = K;
+        for (int r = 0; r < 3; ++r)
+            for (int b : {1, 0}) {
+                t.slab_b = b ? slab_b : nullptr;
+                const double u = timeit([&] { gemm_tn_bf16(t, splits, 0); });
+                printf("library DMA TN %s bias sums: %8.1f us  %7.1f TF/s\n", b ? "with" : "without", u, flop / u * 1e-6);
+            }
+        return 0;
+    }
     if (mode) {
         TN16Args t;
         t.A = dA; t.lda = (mode == 1 || mode == 2 || mode == 5 || mode == 6) ? 0 : N; t.B = dB; t.ldb = t.lda ? K : 0; t.K1 = K;
