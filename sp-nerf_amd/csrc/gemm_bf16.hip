@@ -1731,12 +1731,24 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
         fread(f0, 0, 0);
         for (int st = 0; st < ns; ++st) {
             const int stg = st % TD_STAGES;
+            // the stage's bias rows as asm reads issued before f1's fragments: the fragment wait
+            // below (at most f1's 12 reads outstanding) retires them too, and no compiler wait for
+            // them (which, counting in order, would have waited for f1's reads as well) remains
+            u32x4 bv[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+            if (do_bias) {  // block-uniform
+                const char* sA = smem + stg * TD_STG + (ch >> 4) * HALF;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (i > 0 && bsplit) break;
+                    const uint32_t addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(sA + tn_off(lrow + 16 * i, ch & 15));
+                    asm volatile("ds_read_b128 %0, %1" : "=v"(bv[i]) : "v"(addr) : "memory");
+                }
+            }
             fread(f1, stg, 1);
             fwait12(f0);
+            asm volatile("" : "+v"(bv[0]), "+v"(bv[1])::"memory");  // (after the wait that retired them)
             fmma(f0);
-            // (the bias rows' plain LDS reads: the compiler's own waits for them are conservative
-            // under in-order LDS counting, and the fragment waits count them as later reads)
-            if (do_bias) bias_rows(stg);
+            if (do_bias) bias_add(bv);
             // step st+1 landed (own DMAs: st+1, st+2 outstanding, st+3 not yet issued); the barrier
             // publishes it and retires every wave's reads of stage (st+3) % 4 = (st-1) % 4
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
