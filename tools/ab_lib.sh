@@ -13,6 +13,6 @@ for r in $(seq ${1:-2}); do
     timeout -k 10 200 python bench.py --global-batch 512 --no-cpu-baseline --no-secondary > gpurun_out/ab/c4_512_$lib.json 2>/dev/null || exit 1
     python -c "
 import json; a=json.load(open('gpurun_out/ab/c4_$lib.json')); b=json.load(open('gpurun_out/ab/c4_512_$lib.json'))
-k=a['kernels']; print('$lib', 'c4', round(a['ms_per_step'],3), 'c4@512', round(b['ms_per_step'],3), {n: round(k[n]['ms_per_step'],3) for n in ('trunk_bf16_train','heads_train','trunk_bwd_bf16','gemm_tn_bf16d') if n in k})"
+k=a['kernels']; print('$lib', 'c4', round(a['ms_per_step'],3), 'c4@512', round(b['ms_per_step'],3), {n: round(k[n]['ms_per_step'],3) for n in ('trunk_bf16_train','heads_train','trunk_bwd_bf16','gemm_tn_bf16d','gemm_nt_bf16d','gemm_nt_bf16d_dmul') if n in k})"
   done
 done
