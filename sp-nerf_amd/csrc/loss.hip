@@ -224,8 +224,9 @@ static LossArgs loss_args(int64_t n_rays, int32_t n_samples, int32_t n_classes, 
     return a;
 }
 
-// a block of 4 waves per 16 rays, at most 1024 blocks
-static int loss_blocks(int64_t n_rays) { return (int)std::min<int64_t>(std::max<int64_t>((n_rays + 15) / 16, 1), 1024); }
+// a block of 4 waves per 4 rays (a wave per ray: the per-ray terms are a chain of dependent
+// loads and wave sums, so 4 rays per wave took 18 us at any batch), at most 4096 blocks
+static int loss_blocks(int64_t n_rays) { return (int)std::min<int64_t>(std::max<int64_t>((n_rays + 3) / 4, 1), 4096); }
 
 extern "C" int64_t spnerf_render_loss_workspace_bytes(int64_t n_rays) {
     if (n_rays < 0) return -1;

@@ -22,6 +22,7 @@
 #include "gemm_f32.h"
 #include "mlp_layout.h"
 #include "trunk.h"
+#include "wave.h"
 
 namespace spn {
 
@@ -851,24 +852,38 @@ __global__ __launch_bounds__(256) void k_ray_tiles_sum(const float* __restrict__
 
 struct RayBwdArgs {
     const float* packed; PackedOffs k; Dims d;
-    const float *sky, *skyh, *dsky, *R0, *R4, *RQ;
+    const float *sky, *skyh, *R0, *R4, *RQ;
+    const float* d_out; int NO, S;   // the points' output gradients (sky columns 5..7)
     const int64_t* labels;
     float *skyd, *skydh, *gemb, *embr, *grad_t;
     int sem_on, beta_on, sky_on;
 };
 
 // Per-ray backward pieces: sky MLP pre-activation grads, the semantic-embedding input grad
-// and the time-embedding input grad.  One 256-thread block per ray.
+// and the time-embedding input grad.  One 256-thread block per ray.  The sky colour's gradient
+// is the sum of d_out's sky columns over the ray's samples (the sky is per ray, broadcast to every
+// sample: spnerf.py:244-249): wave c sums column c, its lanes strided over the samples (a separate
+// one-thread-per-column launch walked the 128 samples serially: 50 us per C4 step).
 __global__ __launch_bounds__(256) void k_ray_bwd(RayBwdArgs a) {
     const int64_t ray = blockIdx.x;
     const int tid = threadIdx.x;
     const Dims& d = a.d;
     const float* P = a.packed;
     if (a.sky_on) {
+        __shared__ float dsk[3];
+        if ((tid >> 6) < 3) {
+            const int c = tid >> 6, lane = tid & 63;
+            const float* q = a.d_out + ray * a.S * (int64_t)a.NO + 5 + c;
+            float v = 0.f;
+            for (int s = lane; s < a.S; s += 64) v += q[(int64_t)s * a.NO];
+            v = wave_sum(v);
+            if (lane == 0) dsk[c] = v;
+        }
+        __syncthreads();
         float dp[3];
         for (int c = 0; c < 3; ++c) {
             const float s = a.sky[ray * 4 + c];
-            dp[c] = a.dsky[ray * 4 + c] * (1.f - s) * s;
+            dp[c] = dsk[c] * (1.f - s) * s;
         }
         if (tid < 3) a.skyd[ray * 4 + tid] = dp[tid];
         for (int n = tid; n < d.H; n += blockDim.x) {
@@ -2335,14 +2350,8 @@ static int32_t mlp_backward(const Dims& d, const float* packed, const float* ray
     // 7. per-ray parameters: sun-direction columns, t columns, sky MLP, semantic embedding
     {
         const int sky_on = mode == 0;
-        if (sky_on) {
-            ProfScope prof("ray_rowsum", s, 0.0, 0.0);
-            hipLaunchKernelGGL(k_ray_rowsum<float>, dim3(1, (unsigned)n_rays), dim3(256), 0, s, d_out, d.NO, 5, 3, S,
-                               c.at(c.w.dsky), 4);
-            SPN_HIP(hipGetLastError());
-        }
-        RayBwdArgs a{packed, c.k, d, c.at(c.w.sky), c.at(c.w.skyh), c.at(c.w.dsky), c.at(c.w.R0), c.at(c.w.R4),
-                     c.at(c.w.RQ), labels, c.at(c.w.skyd), c.at(c.w.skydh), c.at(c.w.gemb), c.at(c.w.embr), grad_t,
+        RayBwdArgs a{packed, c.k, d, c.at(c.w.sky), c.at(c.w.skyh), c.at(c.w.R0), c.at(c.w.R4),
+                     c.at(c.w.RQ), d_out, (int)d.NO, (int)S, labels, c.at(c.w.skyd), c.at(c.w.skydh), c.at(c.w.gemb), c.at(c.w.embr), grad_t,
                      d.sem ? 1 : 0, (d.beta && mode == 0) ? 1 : 0, sky_on};
         {
             ProfScope prof("ray_terms", s, 0.0, 0.0);

@@ -261,7 +261,6 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         // per-64-point-tile column sums of dZ_0 / dZ_skip (tile_colsum order), summed per ray
         w.Rp0 = take((P + 63) / 64 * W);
         w.Rp4 = take((P + 63) / 64 * W);
-        w.dsky = take(B * 4);
         w.skyd = take(B * 4);
         w.skydh = take(B * H);
         w.gemb = take(B * (d.sd ? d.sd : 1));

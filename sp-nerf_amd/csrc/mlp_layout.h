@@ -87,7 +87,7 @@ struct WS {
     int64_t G, DG, Q, DQ, S2, DS2, S3, DS3, hsave;
     int64_t rb0, rb4, rbQ, skyh, sky;
     // backward
-    int64_t dZG, dZQ, dS3, dS2, dZa, dZb, dZc, hpre, slab, slab_b, RQ, R0, R4, Rp0, Rp4, dsky, skyd, skydh, gemb, embr, sk_slab, sk_slab_b;
+    int64_t dZG, dZQ, dS3, dS2, dZa, dZb, dZc, hpre, slab, slab_b, RQ, R0, R4, Rp0, Rp4, skyd, skydh, gemb, embr, sk_slab, sk_slab_b;
     int64_t sk_slab_n = 0, sk_slab_b_n = 0;  // their capacities (floats)
     int64_t slab_n = 0, slab_b_n = 0;        // the TN slabs' capacities (floats)
     int64_t total;

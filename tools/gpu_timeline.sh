@@ -1,5 +1,5 @@
 # rocprofv3 kernel trace of short C4 bench runs (graph mode) at the given global batches;
-# tools/timeline.py prints one step from each.
+# tools/timeline.py prints the last steps of each (busy, idle gaps, sequence).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
