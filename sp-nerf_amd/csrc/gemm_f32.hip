@@ -752,10 +752,18 @@ __device__ __forceinline__ void reduce_slab_row(const ReduceArgs& g, const int r
     const int n = g.row0 + r;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (c + 3 < g.ncols) {
-        // 4 splits' quads in flight per thread (the sums stay in split order)
+        // 16 (then 4) splits' quads in flight per thread, the sums in split order either way (a
+        // skinny reduction's 512-768 splits were 32 serial rounds of 4 loads: 15-30 us for a few MB)
         const float* src = g.slab + (int64_t)n * g.ld_slab + c;
         const int64_t st = g.slab_stride;
         int k = ty;
+        for (; k + 60 < g.splits; k += 64) {
+            f32x4 x[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) x[j] = ld4(src + (int64_t)(k + 4 * j) * st);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v += x[j];
+        }
         for (; k + 12 < g.splits; k += 16) {
             const f32x4 x0 = ld4(src + k * st), x1 = ld4(src + (k + 4) * st), x2 = ld4(src + (k + 8) * st),
                         x3 = ld4(src + (k + 12) * st);
@@ -772,8 +780,10 @@ __device__ __forceinline__ void reduce_slab_row(const ReduceArgs& g, const int r
             float a = 0.f;
             if (cc < g.ncols) {
                 const float* src = g.slab + (int64_t)n * g.ld_slab + cc;
+#pragma unroll 8
                 for (int k = ty; k < g.splits; k += 4) a += src[(int64_t)k * g.slab_stride];
             } else if (cc == g.ncols && g.dst_b) {
+#pragma unroll 8
                 for (int k = ty; k < g.splits; k += 4) a += g.slab_b[(int64_t)k * g.N + n];
             }
             v[e] = a;
