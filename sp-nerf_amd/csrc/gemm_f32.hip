@@ -993,9 +993,14 @@ int32_t gemm_nt(const NTArgs& a0, hipStream_t s, int variant) {
     return SPNERF_OK;
 }
 
+// rows per block of a skinny reduction: ≤ 768 chunks, multiples of 64 rows; from 2^16 rows on at
+// least 256 (a block's combine and slab writes cost as much as 128 rows' loads: the 512-ray
+// step's narrow-head reduction took twice the time per byte of the 4 096-ray one).  Any P' ≤ P
+// has at most min(ceil(P / 64), 768) chunks (mlp_layout's slab bound).
 int skinny_chunk(int64_t P) {
     int64_t c = (P + 767) / 768;
     c = (c + 63) / 64 * 64;
+    if (P >= 65536 && c < 256) c = 256;
     return (int)(c < 64 ? 64 : c);
 }
 

@@ -267,7 +267,8 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
         w.embr = take(B * (d.sd ? d.sd : 1));
         // skinny slabs: one point reduction at a time, or the per-ray batch (≤ kSkinnyMulti tasks of
         // ≤ 9 rows x max(W, H) columns each, mlp.hip SkinnyBatch)
-        const int64_t cP = (P + skinny_chunk(P) - 1) / skinny_chunk(P), cB = (B + skinny_chunk(B) - 1) / skinny_chunk(B);
+        // chunks of any row count up to P (resp. B): skinny_chunk's bound
+        const int64_t cP = std::min<int64_t>((P + 63) / 64, 768), cB = std::min<int64_t>((B + 63) / 64, 768);
         w.sk_slab_n = std::max(cP * 9 * W, cB * kSkinnyMulti * 9 * W);
         w.sk_slab_b_n = std::max(cP * 9, cB * kSkinnyMulti * 9);
         w.sk_slab = take(w.sk_slab_n);

@@ -134,6 +134,12 @@ __global__ __launch_bounds__(256) void k_guided(GuidedArgs a) {
     const bool active = ray < a.B;
     const int64_t rr = active ? ray : 0;
     WaveLds& L = lds[wv];
+    // each wave sorts in its own LDS slice: a wave barrier orders its LDS writes and reads (the
+    // block barriers made the four rays of a block wait for each other at every sort stage)
+    const auto wsync = [] {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    };
     const int S = a.S, N = S;
     // predicted-depth spread: std = sqrt(Σ (z - depth)^2 w)   (rendering.py:81)
     const float dep = a.depth[rr];
@@ -162,24 +168,24 @@ __global__ __launch_bounds__(256) void k_guided(GuidedArgs a) {
     float w[EPL];
     window_bins<EPL>(L, w, low, high, N, nr, fr, lane);
     build_cdf<EPL>(L, w, N - 1, lane, 1e-5f);
-    __syncthreads();
+    wsync();
     // 2N slots: [0,N) guided samples (sorted first, rendering.py:165), [N,2N) stratified
     int n2 = 1;
     while (n2 < 2 * N) n2 <<= 1;
     for (int e = lane; e < n2; e += 64)
         L.buf[e] = e < N ? invert_cdf(L, N - 1, dev_rng ? rng_uniform(rk, rr, e) : u[e], 1e-5f) : INFINITY;
-    __syncthreads();
+    wsync();
     int n1 = 1;
     while (n1 < N) n1 <<= 1;
     // sort the guided half (padded with +inf up to n1 ≤ n2)
     for (int e = lane + N; e < n1; e += 64) L.buf[e] = INFINITY;
-    __syncthreads();
-    wave_bitonic_sort(L.buf, n1, lane, [] { __syncthreads(); });
+    wsync();
+    wave_bitonic_sort(L.buf, n1, lane, wsync);
     if (active) {
         for (int e = lane; e < 2 * N; e += 64)
             a.z_unsort[ray * 2 * N + e] = e < N ? a.z[ray * N + e] : L.buf[e - N];
     }
-    __syncthreads();
+    wsync();
     // merge: [sorted guided | stratified | +inf pad] → full sort of n2 slots
     for (int e = lane; e < n2; e += 64) {
         float v = INFINITY;
@@ -187,8 +193,8 @@ __global__ __launch_bounds__(256) void k_guided(GuidedArgs a) {
         else if (e < 2 * N) v = a.z[rr * N + (e - N)];
         L.cdf[e & 255] = v;  // stage in cdf (free now)
     }
-    __syncthreads();
-    wave_bitonic_sort(L.cdf, n2, lane, [] { __syncthreads(); });
+    wsync();
+    wave_bitonic_sort(L.cdf, n2, lane, wsync);
     if (active)
         for (int e = lane; e < 2 * N; e += 64) a.z_sorted[ray * 2 * N + e] = L.cdf[e];
 }
