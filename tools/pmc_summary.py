@@ -1,6 +1,8 @@
 """Summarise tools/pmc_gemm*.sh output: one line of derived counters per (kernel, grid).
-    python tools/pmc_summary.py gpurun_out/pmc16"""
+    python tools/pmc_summary.py gpurun_out/pmc16
+PMC_MATCH (a regex, default "gemm|trunk") and PMC_MIN_GRID (default 100000) pick the kernels."""
 import collections
+import re
 import csv
 import glob
 import os
@@ -22,7 +24,8 @@ seen = set()
 for d in sorted(data):
     name, grid, dur = meta[d]
     short = name.split("(")[0].replace("void spn::", "").replace("spn::", "")
-    if not ("gemm" in short or "trunk" in short) or grid < 100000 or (short, grid) in seen:
+    if not re.search(os.environ.get("PMC_MATCH", "gemm|trunk"), short) or grid < int(os.environ.get("PMC_MIN_GRID", 100000)) \
+            or (short, grid) in seen:
         continue
     seen.add((short, grid))
     c = data[d]
