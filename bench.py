@@ -468,7 +468,7 @@ def grad_gates(errs, ratios):
 
 
 def psnr_seeds(seeds=(3, 4, 5, 6, 7, 8), steps: int = 1000, batch: int = 512, n_eval: int = 4096, dev="cuda:0",
-               checkpoints: int = 8):
+               checkpoints: int = 8, detail_path: str | None = None):
     """Paired multi-seed trained-PSNR statistics (BASELINE.json "PSNR vs ref", north star within
     0.05 dB): ``psnr_long`` once per seed (its own init, batches and on-device draws), three arms
     each (fp32 = the reference-pinned HIP path, bf16, fp32_control = fp32 from the init x (1 +
@@ -495,6 +495,9 @@ def psnr_seeds(seeds=(3, 4, 5, 6, 7, 8), steps: int = 1000, batch: int = 512, n_
                     "loss_spikes": r["loss_spikes"],
                     "loss_trace_every_10": r["loss_trace_every_10"],
                     "final_loss": {a: v[-1][1] for a, v in r["loss_curve"].items()}})
+        if detail_path:   # the full per-seed record (traces, floors) as a side file, rewritten per seed
+            with open(detail_path, "w") as f:
+                json.dump({"per_seed": per}, f)
         print(f"psnr_seeds: seed {sd} done ({time.perf_counter() - t0:.0f} s): " +
               " ".join(f"{k} {v:.3f}" for k, v in per[-1].items() if k.endswith("_db")), file=sys.stderr, flush=True)
 
@@ -543,6 +546,95 @@ def psnr_seeds(seeds=(3, 4, 5, 6, 7, 8), steps: int = 1000, batch: int = 512, n_
             "train_seconds": time.perf_counter() - t0,
             "setup": "bench.psnr_long per seed: C3 flags at img_downscale 4 on the JAX_269 cameras against the real "
                      "JAX_269 images (JAX_214 absent), trainer's loss sum, Adam lr 5e-4"}
+
+
+# The driver parses the ONE JSON line rank 0 prints; round 5's 68 KB line (per-seed loss traces
+# of the PSNR study) was not parsed at all.  Every line is held to this budget by construction
+# (finalize_line), and tests/test_bench_line.py / test_gpu_bench_lines.py check it.
+LINE_BUDGET = 8192
+
+
+def compact(v, sig: int = 5):
+    """``v`` with every float rounded to ``sig`` significant digits (dicts / lists recursively)."""
+    if isinstance(v, float):
+        if not math.isfinite(v) or v == 0.0:
+            return v
+        return float(f"{v:.{sig}g}")
+    if isinstance(v, dict):
+        return {k: compact(x, sig) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [compact(x, sig) for x in v]
+    return v
+
+
+def psnr_seeds_summary(r: dict) -> dict:
+    """The PSNR study's statistics for the bench line: per seed the final dB figures and the worst
+    gradient error, the across-seed means / SEs, the gates, the worst checkpoint (seed, step, error,
+    its two floors) and the spike list — no per-step traces or per-checkpoint arrays (those go to
+    the ``--psnr-detail`` side file)."""
+    w = r["worst_grad_checkpoint"]
+    keep = ("seed", "fp32_db", "bf16_db", "control_db", "delta_db", "control_delta_db", "infer_delta_db",
+            "max_grad_rel_err", "max_grad_err_over_batch_noise")
+    return {"n_seeds": r["n_seeds"], "steps": r["steps"], "batch_rays": r["batch_rays"],
+            "held_out_rays": r["held_out_rays"],
+            "per_seed": [{k: q[k] for k in keep} for q in r["per_seed"]],
+            "delta_bf16_minus_fp32_db": r["delta_bf16_minus_fp32_db"],
+            "delta_control_minus_fp32_db": r["delta_control_minus_fp32_db"],
+            "bf16_inference_at_fp32_trained_db": r["bf16_inference_at_fp32_trained_db"],
+            "gradient_gates": {k: {"value": g["value"], "pass": g["pass"]} for k, g in r["gradient_gates"].items()},
+            "worst_grad_checkpoint": {"seed": w["seed"], "step": w["step"], "grad_rel_err": w["grad_rel_err"],
+                                      "bf16_weights_floor": w["floors"]["bf16_weights"],
+                                      "other_batch_floor": w["floors"]["other_batch"]},
+            "seeds_ending_in_a_loss_spike": r["seeds_ending_in_a_loss_spike"],
+            "resolvable_0p05_db": r["resolvable_0p05_db"], "train_seconds": r["train_seconds"]}
+
+
+def _line_size(out) -> int:
+    return len(json.dumps(out))
+
+
+def finalize_line(out: dict, budget: int = LINE_BUDGET) -> dict:
+    """The record rank 0 prints, held to ``budget`` bytes of JSON: floats to 5 significant digits,
+    the PSNR study reduced to its summary, then — only while still over — the optional detail
+    trimmed in a fixed order (named in ``trimmed``).  The headline fields, ``roofline``,
+    ``cpu_baseline``, ``mlp_mfma_utilisation`` and the secondaries' values and rooflines are never
+    dropped."""
+    out = dict(out)
+    if "psnr_seeds" in out and "per_seed" in out["psnr_seeds"] and "grad_rel_err" in out["psnr_seeds"]["per_seed"][0]:
+        out["psnr_seeds"] = psnr_seeds_summary(out["psnr_seeds"])
+    out = compact(out)
+    trimmed = []
+
+    def over():
+        return _line_size(dict(out, trimmed=trimmed)) > budget
+
+    def strip_kernel_names(d):
+        if isinstance(d, dict) and "roofline" in d and isinstance(d["roofline"], dict):
+            d["roofline"] = {k: v for k, v in d["roofline"].items() if k not in ("traffic_source", "traffic_unit")}
+
+    steps = [
+        ("psnr_parity: figures only", lambda: out.__setitem__("psnr_parity", {
+            p: {k: v for k, v in r.items() if k in ("psnr_gpu_db", "psnr_cpu_reference_db", "delta_db", "steps",
+                                                   "batch_rays", "max_train_loss_rel_diff")}
+            for p, r in out["psnr_parity"].items()}) if "psnr_parity" in out else None),
+        ("kernels: top 8", lambda: out.__setitem__("kernels", dict(list(out["kernels"].items())[:8]))
+         if isinstance(out.get("kernels"), dict) else None),
+        ("rooflines_top3", lambda: out.pop("rooflines_top3", None)),
+        ("roofline traffic_source", lambda: [strip_kernel_names(d) for d in [out] + list(out.get("secondary", {}).values())]),
+        ("psnr_seeds: per_seed", lambda: out.get("psnr_seeds", {}).pop("per_seed", None)),
+        ("secondary workloads", lambda: [d.get("config", {}).pop("workload", None)
+                                         for d in out.get("secondary", {}).values()]),
+        ("kernels", lambda: out.pop("kernels", None)),
+        ("parity_note", lambda: out.pop("parity_note", None)),
+    ]
+    for name, fn in steps:
+        if not over():
+            break
+        fn()
+        trimmed.append(name)
+    if trimmed:
+        out["trimmed"] = trimmed
+    return out
 
 
 def ref_cpu_replay(draws):
@@ -841,9 +933,15 @@ def parse_args(argv=None):
     ap.add_argument("--torch-loss", action="store_true", help="the losses module (plain torch) instead of the fused loss kernels")
     ap.add_argument("--torch-gather", action="store_true", help="torch indexing per field instead of the one-launch batch gather")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--psnr-steps", type=int, default=1000,
-                    help="steps per seed of the paired bf16-vs-fp32 training PSNR study in the default line (0 = skip)")
+    ap.add_argument("--psnr-steps", type=int, default=0,
+                    help="steps per seed of the paired bf16-vs-fp32 training PSNR study (psnr_seeds; 0 = skip, the "
+                         "default: ~275 s for 6 seeds x 1000 steps, and it cannot resolve 0.05 dB — DESIGN.md §5)")
     ap.add_argument("--psnr-seeds", type=int, default=6, help="seeds of that study (psnr_seeds)")
+    ap.add_argument("--psnr-detail", default=None,
+                    help="write the PSNR study's full per-seed record (loss traces, floors) to this JSON file; the "
+                         "line carries its summary only")
+    ap.add_argument("--psnr-parity-steps", type=int, default=30,
+                    help="steps of the 30-step oracle-anchored psnr_parity legs (fp32, bf16; 0 = skip)")
     ap.add_argument("--cpu-batch", type=int, default=0,
                     help="rays per CPU-baseline step (default: the GPU step's batch, at most 512)")
     ap.add_argument("--full-image", action="store_true",
@@ -911,11 +1009,25 @@ def main():
         sec = run_inference(a, "c5", rank, world, dev, steps=10, warmup=3, secondary=True)
         out["secondary"]["c5"] = {k: sec[k] for k in keys + ("steps", "image_seconds_projected")}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(finalize_line(out)), flush=True)
     if world > 1:
         dist.barrier()
     if dist.is_initialized():
         dist.destroy_process_group()
+    report_children(rank)
+
+
+def report_children(rank: int) -> None:
+    """At exit, name this rank's child processes on stderr (the driver has seen one process left
+    at the end of the bench for several rounds: this says whether it is one of the bench's own)."""
+    try:
+        import psutil
+        kids = psutil.Process().children(recursive=True)
+        print(f"bench: rank {rank} child processes at exit: "
+              + (", ".join(f"{k.pid} {k.name()} {' '.join(k.cmdline()[:4])}" for k in kids) or "none"),
+              file=sys.stderr, flush=True)
+    except Exception as e:   # diagnosis only
+        print(f"bench: child-process report failed: {type(e).__name__}: {e}", file=sys.stderr)
 
 
 class TrainStep:
@@ -993,6 +1105,7 @@ class TrainStep:
         self.ar_timing = False
         self.in_graph = False     # the all-reduce is part of the captured graph
         self.graph = None
+        self.graph_packs = []     # packed-weight buffers the captured graph writes (kept with it)
         self.static_loss = None
         self.res = None           # the last render's outputs (the graph's static outputs after capture)
 
@@ -1129,7 +1242,43 @@ class TrainStep:
                 graph = None
                 torch.cuda.synchronize()
         self.graph = graph
+        # the packed-weight buffers this capture wrote into live exactly as long as the graph
+        self.graph_packs = self.model.release_graph_packs()
         return graph is not None
+
+    def exposed_collective_ms(self, reps: int = 5, wd=None):
+        """With the bucket all-reduces captured INTO the step graph, the exposed collective per
+        step cannot be timed by host events around it: it is the difference of paired replays
+        (each synchronized, medians of ``reps``) of the step graph with the buckets and of a second
+        capture of the same render + loss + backward without them.  None unless the collectives
+        are in the graph.  (Round 5 faulted here before the packed-weight buffers of the first
+        capture were kept with its graph: the second capture's empty_cache() released them and the
+        next replay wrote unmapped memory — DESIGN.md §7, tests/test_gpu_graph.py.)"""
+        if not self.in_graph or self.graph is None:
+            return None
+        import statistics
+        torch.cuda.synchronize()
+        self.opt.zero_grad(set_to_none=True)
+        plain = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(plain):
+            self.fwd_bwd()
+        plain_packs = self.model.release_graph_packs()   # kept exactly as long as `plain`
+        torch.cuda.synchronize()
+        t = {"with": [], "without": []}
+        for r in range(reps):
+            for key, g in (("with", self.graph), ("without", plain)):
+                if wd is not None:
+                    wd.beat(r, f"paired replay ({key} buckets)")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                g.replay()
+                e1.record()
+                e1.synchronize()
+                t[key].append(e0.elapsed_time(e1))
+        del plain, plain_packs
+        med = {k: statistics.median(v) for k, v in t.items()}
+        return {"exposed_ms": max(0.0, med["with"] - med["without"]), "replay_ms_with_buckets": med["with"],
+                "replay_ms_without": med["without"], "reps": reps}
 
     def probe(self) -> dict:
         """Watchdog diagnosis: the gradient marks an EAGER backward reached (the marks inside a
@@ -1139,12 +1288,16 @@ class TrainStep:
         if self.buckets is None:
             return {"marks": None}
         n = self.buckets.n_marks
-        done = [k for k in range(n) if _lib.grad_mark_query(k)]
-        return {"marks_completed": done, "n_marks": n}
+        dev = self.dev.index if self.dev.index is not None else 0
+        state = [_lib.grad_mark_query(dev, k) for k in range(n)]
+        return {"marks_completed": [k for k in range(n) if state[k]],
+                "marks_pending": [k for k in range(n) if state[k] is False],
+                "marks_never_recorded": [k for k in range(n) if state[k] is None], "n_marks": n, "device": dev}
 
     def close(self):
         from spnerf_amd import set_random_source
         self.graph = None
+        self.graph_packs = []
         self.res = None
         set_random_source(None)
         if self.buckets is not None:
@@ -1225,6 +1378,12 @@ def run_train(a, config, rank, world, dev, secondary=False):
         if ts.in_graph and ts.ar_events:
             allreduce_ms = sum(e0.elapsed_time(e1) for e0, e1 in ts.ar_events) / len(ts.ar_events)
     _lib.prof_enable(False)
+    allreduce_eager_ms = allreduce_ms
+    # graph mode with the collectives captured: the exposed all-reduce from paired replays of the
+    # graph with and without the buckets (the eager-step figure is kept beside it)
+    paired = ts.exposed_collective_ms(wd=wd) if (ts.in_graph and a.graph) else None
+    if paired is not None:
+        allreduce_ms = paired["exposed_ms"]
     wd.close()
 
     kernels = kernel_table(prof_steps)
@@ -1256,9 +1415,12 @@ def run_train(a, config, rank, world, dev, secondary=False):
         "rooflines_top3": top_rooflines(config, B, 3),
         "mlp_mfma_utilisation": gemm_totals(prof_steps),
         "allreduce_ms_per_step": allreduce_ms,
+        "allreduce_ms_eager_steps": allreduce_eager_ms if paired is not None else None,
+        "allreduce_exposed_paired_replays": paired,
         "allreduce": (None if (world == 1 and not ts.rehearse) else
                       f"{len(buckets.buckets)} buckets behind the backward's gradient marks, inside the HIP graph "
-                      "(exposed ms timed over the profiled eager steps: the same buckets behind the same marks)"
+                      "(exposed ms = paired replays of the graph with / without the buckets; the same buckets "
+                      "timed over the profiled eager steps in allreduce_ms_eager_steps)"
                       if ts.in_graph else
                       f"{len(buckets.buckets)} buckets after each graph replay (exposed ms above)"
                       if (buckets is not None and a.graph) else
@@ -1278,12 +1440,15 @@ def run_train(a, config, rank, world, dev, secondary=False):
         out["parity_note"] = PARITY_NOTE_BF16
     ts.close()
     del ts
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and not secondary:
+    if rank == 0 and world == 1 and not secondary and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds, a.cpu_batch or min(B, 512))
         if config in ("c2", "c4"):
-            out["psnr_parity"] = {p: psnr_parity(dev=dev, precision=p) for p in ("fp32", "bf16")}
+            if a.psnr_parity_steps > 0:
+                out["psnr_parity"] = {p: psnr_parity(steps=a.psnr_parity_steps, dev=dev, precision=p)
+                                      for p in ("fp32", "bf16")}
             if a.psnr_steps > 0 and c["precision"] == "bf16":
-                out["psnr_seeds"] = psnr_seeds(seeds=tuple(range(3, 3 + a.psnr_seeds)), steps=a.psnr_steps, dev=dev)
+                out["psnr_seeds"] = psnr_seeds(seeds=tuple(range(3, 3 + a.psnr_seeds)), steps=a.psnr_steps, dev=dev,
+                                               detail_path=a.psnr_detail)
     return out
 
 

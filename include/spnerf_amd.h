@@ -257,10 +257,12 @@ int32_t spnerf_gather_rows(const int64_t* idx, int64_t n, int32_t nfields, const
 int32_t spnerf_grad_marks(const spnerf_model_cfg* cfg, int32_t* mark_of_param, int32_t n_params);
 int32_t spnerf_grad_marks_arm(int32_t on);
 int32_t spnerf_grad_mark_wait(int32_t mark, void* stream);
-/* 1 when the latest record of `mark` has completed on the device, 0 while it is pending (a
- * never-recorded mark reads as completed); a hung step's diagnosis (bench.py's step watchdog)
- * reports the marks an eager backward reached.  Replays of a captured graph do not record them. */
-int32_t spnerf_grad_mark_query(int32_t mark);
+/* Device `device`'s mark `mark`: 1 when its latest record has completed, 0 while it is pending,
+ * 2 when it was never recorded (or the device's mark events do not exist yet: a query never
+ * creates them).  Safe from any host thread — the device is named, not taken from the calling
+ * thread — so a hung step's diagnosis (bench.py's step watchdog thread) reports the marks an eager
+ * backward on that rank's GPU reached.  Replays of a captured graph do not record them. */
+int32_t spnerf_grad_mark_query(int32_t device, int32_t mark);
 
 /* ---- in-library kernel timing (HIP events on the launch stream) ------------------------- */
 int32_t spnerf_prof_enable(int32_t on);

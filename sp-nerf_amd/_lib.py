@@ -100,7 +100,7 @@ SIGNATURES = {
     "spnerf_grad_marks": (c_int32, [POINTER(ModelCfg), POINTER(c_int32), c_int32]),
     "spnerf_grad_marks_arm": (c_int32, [c_int32]),
     "spnerf_grad_mark_wait": (c_int32, [c_int32, c_void_p]),
-    "spnerf_grad_mark_query": (c_int32, [c_int32]),
+    "spnerf_grad_mark_query": (c_int32, [c_int32, c_int32]),
 }
 
 _lib = None
@@ -201,12 +201,13 @@ def grad_marks_arm(on: bool) -> None:
     check(lib().spnerf_grad_marks_arm(1 if on else 0), "grad_marks_arm")
 
 
-def grad_mark_query(mark: int) -> bool:
-    """Has the latest record of gradient mark ``mark`` completed? (spnerf_grad_mark_query)"""
-    r = lib().spnerf_grad_mark_query(int(mark))
+def grad_mark_query(device: int, mark: int):
+    """Device ``device``'s gradient mark ``mark`` (spnerf_grad_mark_query): True when its latest
+    record has completed, False while pending, None when it was never recorded on that device."""
+    r = lib().spnerf_grad_mark_query(int(device), int(mark))
     if r < 0:
         check(r, "grad_mark_query")
-    return r == 1
+    return None if r == 2 else r == 1
 
 
 def grad_mark_wait(mark: int, stream) -> None:

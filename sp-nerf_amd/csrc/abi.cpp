@@ -104,7 +104,7 @@ using namespace spn;
 
 extern "C" const char* spnerf_last_error(void) { return g_err; }
 
-extern "C" int32_t spnerf_abi_version(void) { return 1; }
+extern "C" int32_t spnerf_abi_version(void) { return 2; }
 
 extern "C" int32_t spnerf_prof_enable(int32_t on) {
     std::lock_guard<std::mutex> lk(g_mu);

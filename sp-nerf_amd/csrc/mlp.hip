@@ -12,6 +12,7 @@
 //    Q = feat·[sun hidden 1; rgb hidden; beta hidden]^T;
 //  * N ≤ C-wide output heads (σ, rgb, sun, β, semantic logits) are per-point dot products.
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <cstring>
 #include <deque>
@@ -359,22 +360,35 @@ Side* side_stream() {
 // then be captured into the same graph (dp.GradBuckets).
 struct Marks {
     hipEvent_t ev[64] = {};
-    bool ok = false;
+    std::atomic<bool> ok{false};
+    std::atomic<uint64_t> recorded{0};   // bit k: mark k recorded at least once since the events were made
 };
 Marks g_marks[64];
+std::mutex g_marks_mu;                   // creation only (a watchdog thread may query concurrently)
 int g_marks_armed = 0;
 int g_marks_flags = hipEventDisableTiming;  // option "grad_marks_flags": hipEventCreateWithFlags flags (before the first arm)
 
-static Marks* marks_of_device() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+// The mark events of device `dev`, created on first use when `create` (on that device: the
+// calling thread's current device is the caller's, e.g. the rank's own GPU); nullptr when they do
+// not exist and `create` is false — a query from another thread never creates them.
+static Marks* marks_of(int dev, bool create) {
+    if (dev < 0 || dev >= 64) return nullptr;
     Marks& m = g_marks[dev];
-    if (!m.ok) {
+    if (m.ok.load(std::memory_order_acquire)) return &m;
+    if (!create) return nullptr;
+    std::lock_guard<std::mutex> lock(g_marks_mu);
+    if (!m.ok.load(std::memory_order_relaxed)) {
         for (auto& e : m.ev)
             if (hipEventCreateWithFlags(&e, (unsigned)g_marks_flags) != hipSuccess) return nullptr;
-        m.ok = true;
+        m.ok.store(true, std::memory_order_release);
     }
     return &m;
+}
+
+static Marks* marks_of_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    return marks_of(dev, true);
 }
 
 int g_tile_rowsum = 1;  // 1 = per-ray dZ sums by 64-point tiles (fused into the dX chain); 0 = k_ray_rowsum16
@@ -387,6 +401,7 @@ static int32_t grad_mark(int k, hipStream_t s) {
     // captured (a wait on it from another stream of the same capture joins that stream to the
     // graph); this HIP runtime refuses external event-record nodes (hipEventRecordExternal)
     SPN_HIP(hipEventRecord(m->ev[k], s));
+    m->recorded.fetch_or(uint64_t(1) << k, std::memory_order_relaxed);
     return SPNERF_OK;
 }
 
@@ -2524,10 +2539,15 @@ extern "C" int32_t spnerf_grad_mark_wait(int32_t mark, void* stream) {
     return SPNERF_OK;
 }
 
-extern "C" int32_t spnerf_grad_mark_query(int32_t mark) {
-    Marks* m = marks_of_device();
-    SPN_ARG(m && mark >= 0 && mark < 64, "spnerf_grad_mark_query: bad mark");
+extern "C" int32_t spnerf_grad_mark_query(int32_t device, int32_t mark) {
+    SPN_ARG(device >= 0 && device < 64 && mark >= 0 && mark < 64, "spnerf_grad_mark_query: bad device or mark");
+    Marks* m = marks_of(device, false);
+    if (!m || !(m->recorded.load(std::memory_order_relaxed) & (uint64_t(1) << mark))) return 2;   // never recorded
+    int cur = -1;
+    SPN_HIP(hipGetDevice(&cur));
+    if (cur != device) SPN_HIP(hipSetDevice(device));
     const hipError_t e = hipEventQuery(m->ev[mark]);
+    if (cur != device) SPN_HIP(hipSetDevice(cur));
     if (e == hipSuccess) return 1;
     if (e == hipErrorNotReady) return 0;
     SPN_HIP(e);

@@ -211,6 +211,19 @@ class SPNeRF(torch.nn.Module):
                    "pack_params")
         return buf
 
+    def release_graph_packs(self) -> list:
+        """Hand over the packed-weight buffers captured into HIP graphs so far (see
+        ``WeightPack.done``): the caller keeps them exactly as long as the graph(s) it captured
+        (bench.TrainStep stores them beside its graph and drops both together).  Every replay writes
+        the re-packed weights into these buffers, so they must outlive the graph: a buffer the
+        capture took from the free list was allocated OUTSIDE the graph's private pool, and once
+        unreferenced the caching allocator may hand it to eager tensors or, at the next
+        ``torch.cuda.graph`` capture (whose ``__enter__`` calls ``torch.cuda.empty_cache()``),
+        return its segment to the driver — a replay then writes unmapped memory (round 5's
+        illegal-address fault)."""
+        packs, self._graph_packs = self._graph_packs, []
+        return packs
+
     def release_packed(self, buf: torch.Tensor) -> None:
         """Return a buffer from ``packed_weights(own=True)`` once its backward has run."""
         if buf is not None and buf is not self._packed and len(self._pack_pool) < 4:
@@ -336,8 +349,9 @@ class WeightPack:
             else:
                 # ... and it must stay ALLOCATED for the graph's lifetime: a buffer taken from the
                 # free list was allocated outside the capture, so with its last reference gone
-                # the caching allocator would hand its memory to later eager tensors while every
-                # replay still writes the packed weights into it
+                # the caching allocator would hand its memory to later eager tensors, or release
+                # it to the driver at the next capture's empty_cache(), while every replay still
+                # writes the packed weights into it (SPNeRF.release_graph_packs)
                 self.model._graph_packs.append(self.buf)
             self.buf = None
 

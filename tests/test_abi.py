@@ -25,7 +25,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert sorted(_lib.SIGNATURES) == syms, "ctypes signature table out of sync with the header"
-    assert L.spnerf_abi_version() == 1
+    assert L.spnerf_abi_version() == 2
 
 
 def cfg_of(d: ModelDims):

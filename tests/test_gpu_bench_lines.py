@@ -67,8 +67,9 @@ def test_c5_row_sharded_image_equals_single_process(tmp_path):
     assert np.array_equal(got, ref), float(np.abs(got - ref).max())
 
 
-def _bench(tag, *args, timeout=110):
-    """bench.py as a child process; its stdout / stderr kept under gpurun_out/ for diagnosis."""
+def _bench(tag, *args, timeout=110, budget=True):
+    """bench.py as a child process; its stdout / stderr kept under gpurun_out/ for diagnosis.  The
+    printed line must fit the driver's parse budget (bench.LINE_BUDGET)."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", SPNERF_STEP_DEADLINE="90")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
@@ -79,15 +80,30 @@ def _bench(tag, *args, timeout=110):
     with open(os.path.join(out, f"bench_{tag}.err"), "w") as f:
         f.write(p.stderr)
     assert p.returncode == 0, p.stderr[-3000:]
-    return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
+    if budget:
+        sys.path.insert(0, ROOT)
+        import bench
+        assert len(line) <= bench.LINE_BUDGET, len(line)
+    return json.loads(line)
 
 
 def test_bench_default_line_carries_c5_secondary():
-    """The default line's path at a small batch (C4 + the C2 and C5 secondaries, no CPU leg):
-    the C5 secondary carries its roofline and MLP MFMA utilisation."""
+    """The default line's path at a small batch with EVERY leg on (C4, the C2 and C5 secondaries,
+    a short CPU baseline, the psnr_parity legs and a one-seed PSNR study with its side file): the
+    line fits the parse budget and carries roofline, cpu_baseline, the study's summary and the C5
+    secondary with its roofline and MLP MFMA utilisation."""
+    detail = os.path.join(ROOT, "gpurun_out", "psnr_detail_test.json")
     d = _bench("secondary", "--global-batch", "512", "--steps", "3", "--warmup", "2", "--prof-steps", "1",
-               "--no-cpu-baseline", "--psnr-steps", "0")
+               "--cpu-seconds", "1", "--cpu-batch", "32", "--psnr-parity-steps", "3", "--psnr-steps", "20",
+               "--psnr-seeds", "1", "--psnr-detail", detail, timeout=300)
     assert d["finite"] and d["n_gpus"] == 1 and d["allreduce"] is None
+    assert d["roofline"]["frac"] > 0 and d["cpu_baseline"]["value"] > 0
+    assert set(d["psnr_parity"]) == {"fp32", "bf16"}
+    ps = d["psnr_seeds"]
+    assert ps["n_seeds"] == 1 and "worst_grad_checkpoint" in ps and "gradient_gates" in ps
+    with open(detail) as f:
+        assert "loss_trace_every_10" in json.load(f)["per_seed"][0]
     c5 = d["secondary"]["c5"]
     assert c5["value"] > 0 and c5["roofline"]["frac"] > 0 and c5["mlp_mfma_utilisation"]["frac"] > 0.2
     assert d["secondary"]["c2"]["value"] > 0
@@ -95,10 +111,15 @@ def test_bench_default_line_carries_c5_secondary():
 
 def test_bench_line_rehearsed_collective():
     """bench.py at N=1 with --rehearse-collective: a one-rank RCCL group, the bucket all-reduces
-    captured into the step graph and replayed, the exposed collective timed over the profiled eager
-    steps (allreduce_ms_per_step is a number, not null)."""
+    captured into the step graph and replayed; then the profiled eager steps (eager collectives),
+    a SECOND capture without the buckets and paired replays of both graphs — round 5's faulting
+    sequence, safe since the captured packed-weight buffers live with their graphs.  The exposed
+    collective comes from the paired replays (a number, not null), the eager-step figure beside it."""
     d = _bench("rehearse", "--rehearse-collective", "--no-secondary", "--global-batch", "512", "--steps", "3",
                "--warmup", "2", "--prof-steps", "2", "--no-cpu-baseline")
     assert d["finite"] and d["n_gpus"] == 1
     assert "inside the HIP graph" in d["allreduce"], d["allreduce"]
     assert isinstance(d["allreduce_ms_per_step"], float) and d["allreduce_ms_per_step"] >= 0.0
+    pr = d["allreduce_exposed_paired_replays"]
+    assert pr is not None and pr["replay_ms_with_buckets"] > 0 and pr["replay_ms_without"] > 0
+    assert isinstance(d["allreduce_ms_eager_steps"], float)

@@ -190,16 +190,57 @@ def test_trunk_with_fused_heads_bit_identical(sem, B, S, th):
                                     sc_lambda=0.0, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
     model = make_model(ModelDims(width=512, sem=sem), 9, "bf16")
     outs = []
+    if th == 1 and not _lib.has_option("trunk2"):
+        pytest.skip("trunk_heads 1 rides on the two-workgroup trunk k_trunk2_bf16 (ablation build only)")
     try:
         for t in (th, 0):
             _lib.set_option("trunk_heads", t)
-            _lib.set_option("trunk2", 3 if t == 1 else 0)   # trunk_heads 1 rides on the two-workgroup trunk
+            if th == 1:
+                _lib.set_option("trunk2", 3 if t == 1 else 0)
             with torch.no_grad(), random_source(FixedU(u)):
                 outs.append(spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels if sem else None,
                                                    mode="test"))
     finally:
         _lib.set_option("trunk_heads", 2)
-        _lib.set_option("trunk2", 0)
+        if th == 1:
+            _lib.set_option("trunk2", 0)
     for k in outs[1]:
         assert torch.isfinite(outs[0][k]).all(), k
         assert torch.equal(outs[0][k], outs[1][k]), (k, float((outs[0][k] - outs[1][k]).abs().max()))
+
+
+@pytest.mark.parametrize("sem", [True, False])
+def test_fused_inference_kernel_vs_layer_by_layer_gemms(sem):
+    """The product C5 kernel (k_trunk_bf16<128, 4096>: trunk + heads in one launch, the default)
+    against the product library's layer-by-layer path (fused_trunk 0, trunk_heads 0: layer 0 on
+    the hi/lo-plane k_gemm_nt_bf16 after k_encode, layers 1..7 one bf16 GEMM each with the sine
+    epilogue, then the heads kernel) on 3 000 rays x 128 samples: the same bf16 rounding points,
+    other kernels and tilings.  Bound: norm-relative 2e-3 per output (the bf16 ulp is 2^-9 = 2e-3
+    of one activation; the fp32 accumulation orders differ), and the maximum difference printed."""
+    from spnerf_amd import _lib
+    from oracle.weights import ModelDims
+    g = torch.Generator(device="cpu").manual_seed(13)
+    B, S = 3000, 128
+    rays = torch.tensor(gu.synthetic_rays(B, 27), device=DEV)
+    u = torch.rand(B, S, generator=g).to(DEV)
+    labels = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    args = gu.args_of({"args": dict(n_samples=S, n_importance=0, model="sp-nerf", beta=False, guidedsample=False,
+                                    sc_lambda=0.0, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+    model = make_model(ModelDims(width=512, sem=sem), 10, "bf16")
+    outs = []
+    try:
+        for fused in (1, 0):
+            _lib.set_option("fused_trunk", fused)
+            _lib.set_option("trunk_heads", 2 if fused else 0)
+            with torch.no_grad(), random_source(FixedU(u)):
+                outs.append(spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels if sem else None,
+                                                   mode="test"))
+    finally:
+        _lib.set_option("fused_trunk", 1)
+        _lib.set_option("trunk_heads", 2)
+    for k in outs[1]:
+        a, b = outs[0][k].cpu().numpy(), outs[1][k].cpu().numpy()
+        assert np.isfinite(a).all() and np.isfinite(b).all(), k
+        e = gu.rel_err(a, b)
+        print(k, f"norm-rel {e:.2e} max-abs {float(np.abs(a - b).max()):.2e} bitwise {np.array_equal(a, b)}")
+        assert e < 2e-3, (k, e)

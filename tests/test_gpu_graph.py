@@ -158,3 +158,97 @@ def test_forward_sees_fused_optimizer_updates():
     ref = fresh(xyz, input_s=lab)
     assert torch.equal(out, ref)
     print("fused Adam bumped versions:", versions != [p._version for p in m.parameters()])
+
+
+def _allocated(addr: int) -> bool:
+    """Is device address ``addr`` inside a block the caching allocator has handed out?"""
+    for seg in torch.cuda.memory_snapshot():
+        a = seg["address"]
+        for blk in seg["blocks"]:
+            if a <= addr < a + blk["size"]:
+                return blk["state"] == "active_allocated"
+            a += blk["size"]
+    return False
+
+
+class _Drop(list):
+    """A _graph_packs that forgets what it is given (round 5's code before the fix)."""
+
+    def append(self, x):
+        pass
+
+
+@pytest.mark.parametrize("keep", [True, False], ids=["fixed", "round5"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_pooled_pack_outlives_capture(precision, keep):
+    """Round 5's illegal-address fault (bench.py's paired replays), step by step:
+    an eager step returns its packed-weight buffer to the model's free list; the capture takes
+    that buffer (allocated OUTSIDE the graph's private pool); a SECOND capture follows, whose
+    torch.cuda.graph.__enter__ calls torch.cuda.empty_cache(); eager tensors of the buffer's size
+    are allocated.  Fixed (the buffer kept with the graph, SPNeRF.release_graph_packs): it stays
+    allocated, no eager tensor overlaps it, and replays of the first graph equal eager steps bit
+    for bit with the eager tensors untouched.  round5 (the buffer not kept): after the second
+    capture its address is no longer allocated — what a replay would have written through; that
+    arm never replays."""
+    torch.manual_seed(0)
+    B = 128
+    args = gu.args_of({"args": dict(n_samples=64, n_importance=0, model="sp-nerf", beta=False, guidedsample=True,
+                                    sc_lambda=0.1, margin=1e-4, stdscale=1.0, chunk=5120, noise_std=0.0)})
+    rays = torch.tensor(gu_rays(B, 7), device=DEV)
+    g = torch.Generator().manual_seed(4)
+    valid = (torch.rand(B, generator=g) < 0.68).long().to(DEV)
+    depths = torch.stack([rays[:, 7] * 0.5, torch.rand(B, generator=g).to(DEV)], 1)
+    tstd = torch.full((B,), 0.01, device=DEV)
+    sems = torch.randint(0, 3, (B,), generator=g).to(DEV)
+    rgbs = torch.rand(B, 3, generator=g).to(DEV)
+    m = spnerf_amd.SPNeRF(num_sem_classes=3, layers=8, feat=128, mapping=True, sem=True, precision=precision).to(DEV)
+    m_ref = copy.deepcopy(m)
+    if not keep:
+        m._graph_packs = _Drop()
+    src = StaticRandom(5)
+    sl, dl, ce = SNerfLoss(lambda_sc=0.1), DepthLoss(1.0, usealldepth=False), SemanticLoss(1.0)
+
+    def fwd_bwd(model):
+        src.reset()
+        res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=sems, mode="train", valid_depth=valid,
+                                     target_depths=depths, target_std=tstd)
+        loss = sl(res, rgbs)[0] + dl(res, depths[:, 0], depths[:, 1], valid, tstd)[0] + ce(res, sems)[0]
+        loss.backward()
+        return loss
+
+    with random_source(src):
+        fwd_bwd(m)                                   # eager: its own pack goes back to the free list
+        assert len(m._pack_pool) == 1
+        addr, nbytes = m._pack_pool[0].data_ptr(), 4 * m._pack_pool[0].numel()
+        m.zero_grad(set_to_none=True)
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            loss_g = fwd_bwd(m)
+        assert not m._pack_pool                      # the capture took the pooled buffer
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2):                   # __enter__: synchronize + empty_cache
+            fwd_bwd(m)
+        torch.cuda.synchronize()
+        if not keep:
+            assert not _allocated(addr), "the captured pack survived without being kept"
+            del g1, g2
+            return
+        junk = [torch.full((nbytes // 4,), 7.0, device=DEV) for _ in range(4)]
+        packs = m.release_graph_packs()
+        assert any(p.data_ptr() == addr for p in packs) and _allocated(addr)
+        for j in junk:
+            assert j.data_ptr() + nbytes <= addr or addr + nbytes <= j.data_ptr()
+        for it in range(2):
+            m_ref.zero_grad(set_to_none=True)
+            loss_e = fwd_bwd(m_ref)
+            g1.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(loss_e, loss_g), (it, float(loss_e), float(loss_g))
+            for (n, pe), (_, pg) in zip(m_ref.named_parameters(), m.named_parameters()):
+                assert torch.equal(pe.grad, pg.grad), (it, n)
+            assert all(bool((j == 7.0).all()) for j in junk)
+            with torch.no_grad():
+                for pe, pg in zip(m_ref.parameters(), m.parameters()):
+                    pe.mul_(0.97).add_(0.001)
+                    pg.mul_(0.97).add_(0.001)
+        del g1, g2, packs
