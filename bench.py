@@ -654,7 +654,7 @@ def measured_traffic(config, rays_per_rank, kernel_class):
     FETCH_SIZE / WRITE_SIZE passes, bytes = 2*FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md's
     gfx950 correction.  None when no profile of that (config, rays per rank) is committed (PMC
     counters cannot be read from inside the bench process, hence the profile file)."""
-    for rnd in ("r05", "r04"):
+    for rnd in ("r06", "r05", "r04"):
         rel = f"profiles/{rnd}/traffic_{config}_rays{rays_per_rank}.json"
         try:
             with open(os.path.join(ROOT, rel)) as f:

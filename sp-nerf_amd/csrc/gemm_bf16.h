@@ -100,7 +100,13 @@ int32_t gemm_tn_bf16(const TN16Args& a, int splits, hipStream_t s);
 // GEMM has 4 tiles, so alone it fills the CUs with 64 splits and writes 64 MB of partial slabs;
 // n of them together need 1/n of the splits each (n x fewer slab bytes, one launch, one tail).
 constexpr int kTnGroup = 10;
-constexpr int kTnGroupRounds = 4;  // most blocks per CU a group launch may take (option tn_group_rounds)
+// most blocks per CU a group launch may take: the product's automatic choice is at most 2; the
+// ablation build's option tn_group_rounds reaches 4 (and sizes the slab reservation for it)
+#ifdef SPN_ABLATIONS
+constexpr int kTnGroupRounds = 4;
+#else
+constexpr int kTnGroupRounds = 2;
+#endif
 struct TN16Group {
     TN16Args g[kTnGroup];
     int start[kTnGroup + 1];  // GEMM i's blocks: [start[i], start[i + 1])

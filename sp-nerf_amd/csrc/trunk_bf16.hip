@@ -908,7 +908,10 @@ int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double
 }
 
 bool trunk_bf16_supported(int W, int L, int skip, int K0p) {
-    return W == TW && L >= 2 && L <= kTrunkMaxL && K0p <= 64 && K0p % 16 == 0 && skip < L;
+    // skip == 1 is refused: layers 0 and 1 would both stage per-ray rows into srb, and layer 1's
+    // DMA is issued at its top with no barrier after layer 0's epilogue, which still reads srb
+    // (those shapes run layer by layer; the reference's skips=[4] is unaffected)
+    return W == TW && L >= 2 && L <= kTrunkMaxL && K0p <= 64 && K0p % 16 == 0 && skip < L && skip != 1;
 }
 
 // 128-point tiles for training too: C4 26.16 / 26.07 -> 25.41 / 25.43 ms, C4@512 3.789 -> 3.656 ms
