@@ -214,9 +214,9 @@ def test_fused_inference_kernel_vs_layer_by_layer_gemms(sem):
     """The product C5 kernel (k_trunk_bf16<128, 4096>: trunk + heads in one launch, the default)
     against the product library's layer-by-layer path (fused_trunk 0, trunk_heads 0: layer 0 on
     the hi/lo-plane k_gemm_nt_bf16 after k_encode, layers 1..7 one bf16 GEMM each with the sine
-    epilogue, then the heads kernel) on 3 000 rays x 128 samples: the same bf16 rounding points,
-    other kernels and tilings.  Bound: norm-relative 2e-3 per output (the bf16 ulp is 2^-9 = 2e-3
-    of one activation; the fp32 accumulation orders differ), and the maximum difference printed."""
+    epilogue, then the heads kernel) on 3 000 rays x 128 samples: other kernels and tilings over
+    the same bf16 rounding points, the same k order and the same epilogue arithmetic, so every
+    output is bit-identical (measured so on MI355X, profiles/r06/gpu_suite.txt)."""
     from spnerf_amd import _lib
     from oracle.weights import ModelDims
     g = torch.Generator(device="cpu").manual_seed(13)
@@ -243,4 +243,4 @@ def test_fused_inference_kernel_vs_layer_by_layer_gemms(sem):
         assert np.isfinite(a).all() and np.isfinite(b).all(), k
         e = gu.rel_err(a, b)
         print(k, f"norm-rel {e:.2e} max-abs {float(np.abs(a - b).max()):.2e} bitwise {np.array_equal(a, b)}")
-        assert e < 2e-3, (k, e)
+        assert np.array_equal(a, b), (k, e)
