@@ -1378,6 +1378,13 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
 // only when every split holds whole 32-point steps (P % 32 == 0).  Bias sums are read back from
 // the landed stage (k0 == 0 blocks only).
 constexpr int TD_STEP = 32, TD_STAGES = 4, TD_STG = 4 * TD_STEP * 256;  // bytes per stage
+#ifndef SPN_TN_ADDR
+// 1: the IP 3 main loop reads its fragments at 12 lane offsets computed once per block, one
+// v_add per offset per stage and the k-step as the ds_read immediate (the same reads, MFMAs and
+// order: bit-identical); 0: every read's address from tn_off per k-step (≈ 48 VALU per stage
+// beside 16 MFMAs: the SIMD's issue port, not the MFMA pipe, was the kernel's limit)
+#define SPN_TN_ADDR 1
+#endif
 // IP: where a step issues the next DMA step: 0 = before its MFMAs, 1 = after them, 2 = between
 // its two k-halves (default, option tn_bf16_ip: a wave stalled on the DMA issue then has MFMAs
 // in flight; 393 -> 365 us on 524 288 x 512 x 512, C4 TN 7.18 -> 6.81 ms/step)
@@ -1393,7 +1400,12 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
     __shared__ __attribute__((aligned(16))) char smem[TD_STAGES * TD_STG];  // [stage][A0|A1|B0|B1]
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
     typedef __attribute__((address_space(1))) void* gbl_ptr_t;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+#if SPN_TN_ADDR
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: DMA destinations in SGPRs
+#else
+    const int wid = tid >> 6;
+#endif
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
     int gi = 0;
     while (gi + 1 < G.n && wg >= G.start[gi + 1]) ++gi;
@@ -1454,12 +1466,30 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
         }
     }
     const int64_t P1 = g.P1;  // (a local: no scalar loads from the argument inside the loops)
+#if SPN_TN_ADDR
+    // the row strides and segment offsets are wave-uniform (ld: readfirstlane'd segment choice):
+    // a step's byte offset is scalar arithmetic and each DMA address one 64-bit VALU add
+    int ldu[4];
+    int64_t dlu[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ldu[i] = __builtin_amdgcn_readfirstlane(ld[i]);
+        const uint64_t d = (uint64_t)dl[i];
+        dlu[i] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(d >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)d));
+    }
+#endif
     // one of the lane's 4 DMA instructions (IP 3 spreads them over a step's MFMAs)
     auto issue1 = [&](int st, int stg, int i) {
         const int64_t p0 = p_beg + (int64_t)TD_STEP * st;
         const bool sg2 = p0 >= P1;
         const int q = wid + 8 * i;
+#if SPN_TN_ADDR
+        const int64_t boff = p0 * ldu[i] * (int64_t)sizeof(bf16) + (sg2 ? dlu[i] : 0);
+        const char* a = reinterpret_cast<const char*>(src[i]) + boff;
+#else
         const char* a = reinterpret_cast<const char*>(src[i] + p0 * ld[i]) + (sg2 ? dl[i] : 0);
+#endif
         __builtin_amdgcn_global_load_lds((gbl_ptr_t)a, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
     };
     auto issue = [&](int st, int stg) {
@@ -1544,6 +1574,74 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
             }
         }
     };
+#if SPN_TN_ADDR
+    // lane offsets (bytes from smem) of the 12 fragment reads of k-step 0 of stage 0: A fragments
+    // i lo / hi, then B fragments j lo / hi.  Rows 16·ks + 8h + q4 (+ 4 for hi): k-step 1 adds 16
+    // rows = 4096 bytes, and tn_off's swizzle reads only row bits 0..3, which 16·ks leaves alone
+    uint32_t fo[12];
+    {
+        const uint32_t sbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+        const int cb = (wb & 1) * 64;
+        auto off = [&](int half, int r0, int col) {
+            return sbase + (uint32_t)(half * HALF + tn_off(r0 + q4, (col >> 3) + (pp >> 1)) + 8 * (pp & 1));
+        };
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            fo[2 * i] = off(wa, 8 * h, 32 * i + 16 * grp);
+            fo[2 * i + 1] = off(wa, 8 * h + 4, 32 * i + 16 * grp);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            fo[8 + 2 * j] = off(2 + (wb >> 1), 8 * h, cb + 32 * j + 16 * grp);
+            fo[8 + 2 * j + 1] = off(2 + (wb >> 1), 8 * h + 4, cb + 32 * j + 16 * grp);
+        }
+    }
+    // the compute() schedule of IP 3 on those offsets: va = fo + the stage's byte offset (12 VALU
+    // per stage), k-step ks as the instruction's immediate offset
+    auto compute_fo = [&](int stg, auto&& mid) {
+        const uint32_t so = (uint32_t)(stg * TD_STG);
+        uint32_t va[12];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) va[r] = fo[r] + so;
+        auto kst = [&](auto kks) {
+            constexpr int ks = decltype(kks)::value;
+            s16x4 al[4], ah[4], bl[2], bh[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(bl[j]) : "v"(va[8 + 2 * j]), "i"(4096 * ks) : "memory");
+                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(bh[j]) : "v"(va[9 + 2 * j]), "i"(4096 * ks) : "memory");
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(al[i]) : "v"(va[2 * i]), "i"(4096 * ks) : "memory");
+                asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(ah[i]) : "v"(va[2 * i + 1]), "i"(4096 * ks) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(al[0]), "+v"(al[1]), "+v"(al[2]), "+v"(al[3]), "+v"(ah[0]), "+v"(ah[1]),
+                           "+v"(ah[2]), "+v"(ah[3]), "+v"(bl[0]), "+v"(bl[1]), "+v"(bh[0]), "+v"(bh[1])
+                         :
+                         : "memory");
+            bf16x8 a[4], b[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = join(bl[j], bh[j]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = join(al[i], ah[i]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+                if (i & 1) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    mid(2 * ks + (i >> 1));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        };
+        kst(std::integral_constant<int, 0>{});
+        kst(std::integral_constant<int, 1>{});
+    };
+#endif
     // one 16-point k-step of stage stg (IP 4's shifted schedule)
     auto kstep = [&](int stg, int ks) {
         const char* sA = smem + stg * TD_STG + wa * HALF;
@@ -1778,7 +1876,11 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
             if constexpr (IP == 3) {
                 u32x4 bv[TD_STEP / 16];
                 if (do_bias) bias_load(st % TD_STAGES, bv);  // block-uniform
+#if SPN_TN_ADDR
+                compute_fo(st % TD_STAGES, nxt1);
+#else
                 compute(st % TD_STAGES, nxt1);
+#endif
                 ND_STAMP(7);
                 if (do_bias) bias_add(bv);
                 ND_STAMP(8);
