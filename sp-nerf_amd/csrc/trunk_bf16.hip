@@ -113,6 +113,11 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
     __shared__ __attribute__((aligned(16))) char smem[Geo::LDS + (HEADS ? hd::OST_BYTES : Geo::SRB_BYTES)];
     float* srb = reinterpret_cast<float*>(smem + Geo::LDS);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
+    // product: the H copy-outs non-temporal (g_trunk_nt's default, bit 1; the fused-heads launch
+    // copies nothing out and passes 0), the register-D stores not (bit 2)
+    constexpr int kNtDefault = (VAR & 4096) ? 0 : 1;
+    const int gnt = kTrunkAbl ? g.nt : kNtDefault;
+    const int gdbg = kTrunkAbl ? g.dbg : 0;
     float* sbias = reinterpret_cast<float*>(smem + Geo::BIAS_OFF);
     char* sx0 = smem + Geo::X0_OFF;
     const int x0ch = g.K0p >> 3;
@@ -149,7 +154,8 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
         constexpr int n = decltype(kn)::value;
         const int ct = opaque(tid);
         const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + p0 * TW, 0, rows * TW * 2, 0x00020000);
+        // (dst nullptr: an empty resource, every store dropped — no branch around the stores)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + p0 * TW, 0, dst ? rows * TW * 2 : 0, 0x00020000);
         u32x4 v[n];
 #pragma unroll
         for (int q = 0; q < n; ++q) {
@@ -161,12 +167,12 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             const int c = ct + 512 * (q0 + q);
 #if SPN_TRUNK_BUFSTORE
             const int off = ((c >> 6) * TW + (c & 63) * 8) * 2;
-            if (g.nt & 1) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // block-uniform: glc slc
+            if (gnt & 1) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // block-uniform: glc slc
             else __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 0);
 #else  // A/B build: the guarded stores
             if (p0 + (c >> 6) < g.P) {
                 u32x4* o = reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8);
-                if (g.nt & 1) __builtin_nontemporal_store(v[q], o);
+                if (gnt & 1) __builtin_nontemporal_store(v[q], o);
                 else *o = v[q];
             }
 #endif
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
 
     // a whole image, 4 chunks per thread at a time (the accumulators may still be live)
     auto copy_all = [&](const char* img, bf16* dst, int64_t p0) {
-        if (g.dbg & 1) return;
+        if (gdbg & 1) return;
 #pragma unroll
         for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(img, dst, p0, q0, std::integral_constant<int, 4>{});
     };
@@ -360,8 +366,14 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 // drain the previous layer's outputs: CPT / (nmain / TPD) chunks per thread
                 constexpr int per = CPT / (nmain / TPD);
                 static_assert(per * (nmain / TPD) == CPT && per >= 1, "copy slices");
-                if (hpend && !(g.dbg & 9)) copy_out(smem, hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
-                if (Geo::DIMG && dpend && !(g.dbg & 1)) copy_out(smem + IMG, dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+#if SPN_TRUNK_BUFSTORE
+                // (hpend / dpend nullptr on a tile's first layer: empty resources, no branch)
+                copy_out(smem, (gdbg & 9) ? nullptr : hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                if (Geo::DIMG) copy_out(smem + IMG, (gdbg & 1) ? nullptr : dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+#else
+                if (hpend && !(gdbg & 9)) copy_out(smem, hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                if (Geo::DIMG && dpend && !(gdbg & 1)) copy_out(smem + IMG, dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+#endif
             }
             // the x0 columns of the skip layer's input [h | x0] (nks == nmain elsewhere)
 #pragma unroll 1
@@ -498,7 +510,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
                 // (dbg 1, no copy-outs: an empty range drops every store — no branch around them)
                 const __amdgpu_buffer_rsrc_t dr =
-                    __builtin_amdgcn_make_buffer_rsrc(Ds + p0 * TW, 0, (g.dbg & 5) ? 0 : rows * TW * 2, 0x00020000);
+                    __builtin_amdgcn_make_buffer_rsrc(Ds + p0 * TW, 0, (gdbg & 5) ? 0 : rows * TW * 2, 0x00020000);
                 // act_off(32j + er32, 8w + 4a + gq) + 8eh without per-piece index math: the row's
                 // swizzle (row & 15 = er32 & 15) only touches the chunk's low 4 bits
                 char* lbase = smem + er32 * 1024 + 256 * (w >> 1) + 8 * eh;
@@ -563,7 +575,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                             // (option trunk_nt bit 4: glc slc — measured 3.50-3.57 against 2.92 ms per
                             // 524 288 points: without L2 write-combining the 32-B row pieces reach HBM
                             // as partial lines.  H non-temporal, bit 1: 2.88 against 2.92, not default)
-                            if (g.nt & 2)  // block-uniform
+                            if (gnt & 2)  // block-uniform
                                 __builtin_amdgcn_raw_buffer_store_b128(u32x4{cq[k][0], cq[k][1], cq[k + 1][0], cq[k + 1][1]},
                                     dr, ((32 * j + er32) * TW + fb) * 2, 0, 3);
                             else
@@ -640,6 +652,8 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
     __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 8 * TW * 4];  // + the column-sum partials
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     const int sw = r32 & 15;
+    const int gnt = kTrunkAbl ? g.nt : 0;    // product: trunk_bwd_nt 0
+    const int gdbg = kTrunkAbl ? g.dbg : 0;
     typedef const __attribute__((address_space(4))) TrunkBwdArgs* KArgs;
     const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
 
@@ -653,9 +667,18 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
             ring[d][1] = ldg16(src + d * kTrunkKStride + 512);
         }
     };
+    // the tile's rows of a [P][512] bf16 tensor as a buffer resource: rows past P are dropped by
+    // the hardware (stores) — no branch around the stores, whose conservative vmcnt accounting
+    // made later weight-refill waits wait for them too (as in the forward's copy-outs)
+    // (base nullptr: an empty resource — every access dropped, no branch)
+    auto tile_rsrc = [&](const bf16* base, int64_t p0) {
+        const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(base) + p0 * TW, 0, base ? rows * TW * 2 : 0, 0x00020000);
+    };
     auto copy_out = [&](bf16* dst, int64_t p0, int q0, auto kn) {
         constexpr int n = decltype(kn)::value;
         const int ct = opaque(tid);
+        const __amdgpu_buffer_rsrc_t rs = tile_rsrc(dst, p0);
         u32x4 v[n];
 #pragma unroll
         for (int q = 0; q < n; ++q) {
@@ -665,12 +688,16 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
 #pragma unroll
         for (int q = 0; q < n; ++q) {
             const int c = ct + 512 * (q0 + q);
-            if (p0 + (c >> 6) < g.P) {
-                u32x4* o = reinterpret_cast<u32x4*>(dst + (p0 + (c >> 6)) * TW + (c & 63) * 8);
-                if (g.nt & 1) __builtin_nontemporal_store(v[q], o);  // block-uniform (option trunk_bwd_nt)
-                else *o = v[q];
-            }
+            const int off = ((c >> 6) * TW + (c & 63) * 8) * 2;
+            if (gnt & 1) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // (ablation build only)
+            else __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 0);
         }
+    };
+    // 16 B of row min(p0 + row, P - 1) (rows past P read a clamped row, as before) through a buffer
+    // resource over the tile's rows: 32-bit offsets, no 64-bit address per load
+    auto tile_load = [&](const __amdgpu_buffer_rsrc_t& rs, int rows, int row, int ch) -> u32x4 {
+        const int off = (std::min(row, rows - 1) * TW + ch * 8) * 2;
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
     };
     // per-tile column sums of the image (dZ_l, complete: called after a barrier, by every thread)
     // into dst[512]; the partials sit beyond the two images
@@ -697,10 +724,12 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
     u32x4 tv[CPT];
     auto load_top = [&](int64_t q0) {
         const int st = opaque(tid);
+        const int rows = (int)std::min<int64_t>(TMt, g.P - q0);
+        const __amdgpu_buffer_rsrc_t rs = tile_rsrc(g.dZtop, q0);
 #pragma unroll
         for (int q = 0; q < CPT; ++q) {
             const int c = st + 512 * q;
-            tv[q] = ldg16(g.dZtop + std::min<int64_t>(q0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
+            tv[q] = tile_load(rs, rows, c >> 6, c & 63);
         }
     };
     load_top((int64_t)tile * TMt);
@@ -719,15 +748,18 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
         // vmcnt retires in order, so the weight refills issued after them are only usable once
         // the D rows are in — the epilogue plus TPD k-steps cover that HBM latency
         u32x4 dv[CPT];
+        const int trows = (int)std::min<int64_t>(TMt, g.P - p0);
         auto load_d = [&](int l) {
             const int st = opaque(tid);
-            const bf16* dsrc = ka->D[l];
-            if (g.dbg & 2) return;
+            if (gdbg & 2) return;
+            const __amdgpu_buffer_rsrc_t rs = tile_rsrc(ka->D[l], p0);
 #pragma unroll
             for (int q = 0; q < CPT; ++q) {
                 const int c = st + 512 * q;
-                const u32x4* src = reinterpret_cast<const u32x4*>(dsrc + std::min<int64_t>(p0 + (c >> 6), g.P - 1) * TW + (c & 63) * 8);
-                dv[q] = (g.nt & 2) ? __builtin_nontemporal_load(src) : *src;  // block-uniform
+                if (gnt & 2)  // (ablation build only) non-temporal
+                    dv[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (std::min(c >> 6, trows - 1) * TW + (c & 63) * 8) * 2, 0, 3);
+                else
+                    dv[q] = tile_load(rs, trows, c >> 6, c & 63);
             }
         };
         load_d(g.L - 2);
@@ -788,7 +820,8 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
                 }
                 constexpr int per = CPT / (nks / TPD);
                 static_assert(per * (nks / TPD) == CPT && per >= 1, "copy slices");
-                if (pend && !(g.dbg & 1)) copy_out(pend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                // (pend nullptr on a tile's first layer: the stores are dropped, no branch around them)
+                copy_out(gdbg & 1 ? nullptr : pend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
             }
             {
                 const int st = opaque(tid);
@@ -805,7 +838,7 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
                 const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
                 // (dbg 1, no copy-outs: an empty range drops every store)
                 const __amdgpu_buffer_rsrc_t dr =
-                    __builtin_amdgcn_make_buffer_rsrc(ka->dZ[i - 1] + p0 * TW, 0, (g.dbg & 1) ? 0 : rows * TW * 2, 0x00020000);
+                    __builtin_amdgcn_make_buffer_rsrc(ka->dZ[i - 1] + p0 * TW, 0, (gdbg & 1) ? 0 : rows * TW * 2, 0x00020000);
 #pragma unroll
                 for (int a = 0; a < 2; ++a) {
 #pragma unroll
