@@ -37,6 +37,9 @@
 #ifndef SPN_BIAS_HOIST
 #define SPN_BIAS_HOIST 1  // register-D epilogue: the biases of a feature tile read once for both point tiles
 #endif
+#ifndef SPN_TRUNK_EPI_PK
+#define SPN_TRUNK_EPI_PK 1  // the 128-point epilogue's bias adds as packed pairs (0: scalar, A/B builds)
+#endif
 #ifndef SPN_TRUNK_BUFSTORE
 #define SPN_TRUNK_BUFSTORE 1  // copy-outs through buffer descriptors (0: guarded stores, A/B builds)
 #endif
@@ -410,6 +413,10 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             // kpass 0: cos (or Z) into the image (TMt = 128 when saving: it leaves between two
             // barriers); 1: sin into the image; 2: sin into the image and cos (or Z) into the D image
             // kl0: layer 0 (SIREN w0 = 30 of fc_net.0; ×1 elsewhere, exact, so not multiplied)
+            // On 128-point tiles the element arithmetic r = (acc + b [+ row]) [· w0] · 1/2π runs per
+            // pair (the bias adds as v_pk_add_f32; the same roundings per element as fast_sin /
+            // fast_cos: bit-identical).  (Handing r from the cos pass to the sin pass through the
+            // accumulators would save that pass's add / mul, but made the saving kernel spill.)
             auto epilogue = [&](auto kpass, auto kl0, auto krb, auto klds) {
                 if constexpr (NOEPI) {  // keep the accumulators (and so the MFMAs) live
                     float t = 0.f;
@@ -424,6 +431,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
                 constexpr bool RB = decltype(krb)::value;  // per-ray rows (layer 0, the skip layer)
                 constexpr bool RBL = decltype(klds)::value;  // ... staged in LDS (srb)
+                constexpr bool PK = !Geo::DIMG;  // 128-point tiles (zr is false there)
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
@@ -434,29 +442,70 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
 #pragma unroll
                         for (int j = 0; j < NJ; ++j) {
                             const int row = 32 * j + er32;
-                            float v[4];
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] + bv[e];
-                            if constexpr (RB) {
-                                const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
-                                const f32x4 rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
-                                                     : ld4(rb + (int64_t)ray * TW + f0);
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) v[e] += rv[e];
-                            }
                             const int o = act_off(row, f0 >> 3) + 8 * eh;
                             float y[4], c[4];
+                            if constexpr (PK) {
+                                f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
+                                if constexpr (RB) {
+                                    const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
+                                    rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
+                                             : ld4(rb + (int64_t)ray * TW + f0);
+                                }
+                                // one pair at a time (fewer live temporaries)
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) {
-                                const float z = zr ? zr16(v[e]) : v[e];
-                                const float x = w0 == 1.f ? z : w0 * z;
-                                if (pass == 2) {
-                                    fast_sincos(x, &y[e], &c[e]);
-                                    c[e] = zr ? z : (w0 == 1.f ? c[e] : w0 * c[e]);
-                                } else if (pass == 1) {
-                                    y[e] = NOSIN ? x : fast_sin(x);
-                                } else {
-                                    y[e] = zr ? z : (w0 == 1.f ? fast_cos(x) : w0 * fast_cos(x));
+                                for (int q = 0; q < 2; ++q) {
+                                    const int e = 2 * q;
+                                    f32x2 r2;
+                                    {
+#if SPN_TRUNK_EPI_PK
+                                        f32x2 v2 = f32x2{acc[a][j][4 * gq + e], acc[a][j][4 * gq + e + 1]} + f32x2{bv[e], bv[e + 1]};
+                                        if constexpr (RB) v2 += f32x2{rv[e], rv[e + 1]};
+                                        const f32x2 x2 = w0 == 1.f ? v2 : v2 * f32x2{w0, w0};
+                                        r2 = x2 * f32x2{0.15915494309189535f, 0.15915494309189535f};
+#else
+#pragma unroll
+                                        for (int u = 0; u < 2; ++u) {
+                                            float v = acc[a][j][4 * gq + e + u] + bv[e + u];
+                                            if constexpr (RB) v += rv[e + u];
+                                            r2[u] = revs(w0 == 1.f ? v : w0 * v);
+                                        }
+#endif
+                                    }
+#pragma unroll
+                                    for (int u = 0; u < 2; ++u) {
+                                        if (pass == 2) {
+                                            y[e + u] = __builtin_amdgcn_sinf(r2[u]);
+                                            c[e + u] = w0 == 1.f ? __builtin_amdgcn_cosf(r2[u]) : w0 * __builtin_amdgcn_cosf(r2[u]);
+                                        } else if (pass == 1) {
+                                            y[e + u] = NOSIN ? r2[u] : __builtin_amdgcn_sinf(r2[u]);
+                                        } else {
+                                            y[e + u] = w0 == 1.f ? __builtin_amdgcn_cosf(r2[u]) : w0 * __builtin_amdgcn_cosf(r2[u]);
+                                        }
+                                    }
+                                }
+                            } else {
+                                float v[4];
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] + bv[e];
+                                if constexpr (RB) {
+                                    const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
+                                    const f32x4 rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
+                                                         : ld4(rb + (int64_t)ray * TW + f0);
+#pragma unroll
+                                    for (int e = 0; e < 4; ++e) v[e] += rv[e];
+                                }
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) {
+                                    const float z = zr ? zr16(v[e]) : v[e];
+                                    const float x = w0 == 1.f ? z : w0 * z;
+                                    if (pass == 2) {
+                                        fast_sincos(x, &y[e], &c[e]);
+                                        c[e] = zr ? z : (w0 == 1.f ? c[e] : w0 * c[e]);
+                                    } else if (pass == 1) {
+                                        y[e] = NOSIN ? x : fast_sin(x);
+                                    } else {
+                                        y[e] = zr ? z : (w0 == 1.f ? fast_cos(x) : w0 * fast_cos(x));
+                                    }
                                 }
                             }
                             // Z (zr: into the D image, or into the image by pass 0) is stored as fp16
