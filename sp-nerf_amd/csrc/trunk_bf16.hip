@@ -113,6 +113,7 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
     // so rocprof tells the training launches from the inference ones by name)
     static_assert(!(VAR & 2048) || TMt == 128, "the 128-point training instance");
     constexpr bool SRB = !HEADS;  // per-ray rows staged in LDS (the fused heads' kernel has no room)
+    constexpr bool SAVING = (VAR & 2048) != 0;  // the 128-point training instance (every layer saved)
     __shared__ __attribute__((aligned(16))) char smem[Geo::LDS + (HEADS ? hd::OST_BYTES : Geo::SRB_BYTES)];
     float* srb = reinterpret_cast<float*>(smem + Geo::LDS);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
@@ -370,9 +371,15 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 constexpr int per = CPT / (nmain / TPD);
                 static_assert(per * (nmain / TPD) == CPT && per >= 1, "copy slices");
 #if SPN_TRUNK_BUFSTORE
-                // (hpend / dpend nullptr on a tile's first layer: empty resources, no branch)
-                copy_out(smem, (gdbg & 9) ? nullptr : hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
-                if (Geo::DIMG) copy_out(smem + IMG, (gdbg & 1) ? nullptr : dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                if constexpr (SAVING) {
+                    // (hpend nullptr on a tile's first layer: an empty resource, no branch around the
+                    // stores).  Only the saving instance: elsewhere hpend is null on every layer and
+                    // the branch skips the copy entirely (inference: no LDS reads, no dropped stores)
+                    copy_out(smem, (gdbg & 9) ? nullptr : hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                } else {
+                    if (hpend && !(gdbg & 9)) copy_out(smem, hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                    if (Geo::DIMG && dpend && !(gdbg & 1)) copy_out(smem + IMG, dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
+                }
 #else
                 if (hpend && !(gdbg & 9)) copy_out(smem, hpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
                 if (Geo::DIMG && dpend && !(gdbg & 1)) copy_out(smem + IMG, dpend, p0, (ks0 / TPD) * per, std::integral_constant<int, per>{});
@@ -413,10 +420,6 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             // kpass 0: cos (or Z) into the image (TMt = 128 when saving: it leaves between two
             // barriers); 1: sin into the image; 2: sin into the image and cos (or Z) into the D image
             // kl0: layer 0 (SIREN w0 = 30 of fc_net.0; ×1 elsewhere, exact, so not multiplied)
-            // On 128-point tiles the element arithmetic r = (acc + b [+ row]) [· w0] · 1/2π runs per
-            // pair (the bias adds as v_pk_add_f32; the same roundings per element as fast_sin /
-            // fast_cos: bit-identical).  (Handing r from the cos pass to the sin pass through the
-            // accumulators would save that pass's add / mul, but made the saving kernel spill.)
             auto epilogue = [&](auto kpass, auto kl0, auto krb, auto klds) {
                 if constexpr (NOEPI) {  // keep the accumulators (and so the MFMAs) live
                     float t = 0.f;
@@ -431,7 +434,72 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
                 constexpr bool RB = decltype(krb)::value;  // per-ray rows (layer 0, the skip layer)
                 constexpr bool RBL = decltype(klds)::value;  // ... staged in LDS (srb)
-                constexpr bool PK = !Geo::DIMG;  // 128-point tiles (zr is false there)
+                const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                        const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + f0);
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) {
+                            const int row = 32 * j + er32;
+                            float v[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] + bv[e];
+                            if constexpr (RB) {
+                                const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
+                                const f32x4 rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
+                                                     : ld4(rb + (int64_t)ray * TW + f0);
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) v[e] += rv[e];
+                            }
+                            const int o = act_off(row, f0 >> 3) + 8 * eh;
+                            float y[4], c[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const float z = zr ? zr16(v[e]) : v[e];
+                                const float x = w0 == 1.f ? z : w0 * z;
+                                if (pass == 2) {
+                                    fast_sincos(x, &y[e], &c[e]);
+                                    c[e] = zr ? z : (w0 == 1.f ? c[e] : w0 * c[e]);
+                                } else if (pass == 1) {
+                                    y[e] = NOSIN ? x : fast_sin(x);
+                                } else {
+                                    y[e] = zr ? z : (w0 == 1.f ? fast_cos(x) : w0 * fast_cos(x));
+                                }
+                            }
+                            // Z (zr: into the D image, or into the image by pass 0) is stored as fp16
+                            if (pass == 0 && zr)
+                                *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2_f16(y[0], y[1]), pack2_f16(y[2], y[3])};
+                            else
+                                *reinterpret_cast<u32x2*>(smem + o) = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                            if (pass == 2) {
+                                if (zr) *reinterpret_cast<u32x2*>(smem + IMG + o) = u32x2{pack2_f16(c[0], c[1]), pack2_f16(c[2], c[3])};
+                                else *reinterpret_cast<u32x2*>(smem + IMG + o) = u32x2{pack2(c[0], c[1]), pack2(c[2], c[3])};
+                            }
+                        }
+                        __builtin_amdgcn_sched_barrier(0);  // bound the live range of hoisted loads
+                    }
+            };
+            // The saving 128-point instance: the element arithmetic r = (acc + b [+ row]) [· w0] · 1/2π runs per
+            // pair (the bias adds as v_pk_add_f32; the same roundings per element as fast_sin /
+            // fast_cos: bit-identical).  (Handing r from the cos pass to the sin pass through the
+            // accumulators would save that pass's add / mul, but made the saving kernel spill.)
+            auto epilogue_pk = [&](auto kpass, auto kl0, auto krb, auto klds) {
+                if constexpr (NOEPI) {  // keep the accumulators (and so the MFMAs) live
+                    float t = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) t += acc[a][j][0];
+                    if (t == 1234.5f) *reinterpret_cast<float*>(smem + 4 * tid) = t;
+                    return;
+                }
+                constexpr int pass = decltype(kpass)::value;
+                constexpr float w0 = decltype(kl0)::value ? 30.f : 1.f;
+                constexpr bool RB = decltype(krb)::value;  // per-ray rows (layer 0, the skip layer)
+                constexpr bool RBL = decltype(klds)::value;  // ... staged in LDS (srb)
                 const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
@@ -444,67 +512,41 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                             const int row = 32 * j + er32;
                             const int o = act_off(row, f0 >> 3) + 8 * eh;
                             float y[4], c[4];
-                            if constexpr (PK) {
-                                f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
-                                if constexpr (RB) {
-                                    const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
-                                    rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
-                                             : ld4(rb + (int64_t)ray * TW + f0);
-                                }
-                                // one pair at a time (fewer live temporaries)
+                            f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
+                            if constexpr (RB) {
+                                const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
+                                rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
+                                         : ld4(rb + (int64_t)ray * TW + f0);
+                            }
+                            // one pair at a time (fewer live temporaries)
 #pragma unroll
-                                for (int q = 0; q < 2; ++q) {
-                                    const int e = 2 * q;
-                                    f32x2 r2;
-                                    {
+                            for (int q = 0; q < 2; ++q) {
+                                const int e = 2 * q;
+                                f32x2 r2;
+                                {
 #if SPN_TRUNK_EPI_PK
-                                        f32x2 v2 = f32x2{acc[a][j][4 * gq + e], acc[a][j][4 * gq + e + 1]} + f32x2{bv[e], bv[e + 1]};
-                                        if constexpr (RB) v2 += f32x2{rv[e], rv[e + 1]};
-                                        const f32x2 x2 = w0 == 1.f ? v2 : v2 * f32x2{w0, w0};
-                                        r2 = x2 * f32x2{0.15915494309189535f, 0.15915494309189535f};
+                                    f32x2 v2 = f32x2{acc[a][j][4 * gq + e], acc[a][j][4 * gq + e + 1]} + f32x2{bv[e], bv[e + 1]};
+                                    if constexpr (RB) v2 += f32x2{rv[e], rv[e + 1]};
+                                    const f32x2 x2 = w0 == 1.f ? v2 : v2 * f32x2{w0, w0};
+                                    r2 = x2 * f32x2{0.15915494309189535f, 0.15915494309189535f};
 #else
 #pragma unroll
-                                        for (int u = 0; u < 2; ++u) {
-                                            float v = acc[a][j][4 * gq + e + u] + bv[e + u];
-                                            if constexpr (RB) v += rv[e + u];
-                                            r2[u] = revs(w0 == 1.f ? v : w0 * v);
-                                        }
-#endif
-                                    }
-#pragma unroll
                                     for (int u = 0; u < 2; ++u) {
-                                        if (pass == 2) {
-                                            y[e + u] = __builtin_amdgcn_sinf(r2[u]);
-                                            c[e + u] = w0 == 1.f ? __builtin_amdgcn_cosf(r2[u]) : w0 * __builtin_amdgcn_cosf(r2[u]);
-                                        } else if (pass == 1) {
-                                            y[e + u] = NOSIN ? r2[u] : __builtin_amdgcn_sinf(r2[u]);
-                                        } else {
-                                            y[e + u] = w0 == 1.f ? __builtin_amdgcn_cosf(r2[u]) : w0 * __builtin_amdgcn_cosf(r2[u]);
-                                        }
+                                        float v = acc[a][j][4 * gq + e + u] + bv[e + u];
+                                        if constexpr (RB) v += rv[e + u];
+                                        r2[u] = revs(w0 == 1.f ? v : w0 * v);
                                     }
-                                }
-                            } else {
-                                float v[4];
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * gq + e] + bv[e];
-                                if constexpr (RB) {
-                                    const int ray = (int)std::min<int64_t>(p0 + row, g.P - 1) / g.S;  // P < 2^31 / 512
-                                    const f32x4 rv = RBL ? *reinterpret_cast<const f32x4*>(srb + (ray - ray0) * TW + f0)
-                                                         : ld4(rb + (int64_t)ray * TW + f0);
-#pragma unroll
-                                    for (int e = 0; e < 4; ++e) v[e] += rv[e];
+#endif
                                 }
 #pragma unroll
-                                for (int e = 0; e < 4; ++e) {
-                                    const float z = zr ? zr16(v[e]) : v[e];
-                                    const float x = w0 == 1.f ? z : w0 * z;
+                                for (int u = 0; u < 2; ++u) {
                                     if (pass == 2) {
-                                        fast_sincos(x, &y[e], &c[e]);
-                                        c[e] = zr ? z : (w0 == 1.f ? c[e] : w0 * c[e]);
+                                        y[e + u] = __builtin_amdgcn_sinf(r2[u]);
+                                        c[e + u] = w0 == 1.f ? __builtin_amdgcn_cosf(r2[u]) : w0 * __builtin_amdgcn_cosf(r2[u]);
                                     } else if (pass == 1) {
-                                        y[e] = NOSIN ? x : fast_sin(x);
+                                        y[e + u] = NOSIN ? r2[u] : __builtin_amdgcn_sinf(r2[u]);
                                     } else {
-                                        y[e] = zr ? z : (w0 == 1.f ? fast_cos(x) : w0 * fast_cos(x));
+                                        y[e + u] = w0 == 1.f ? __builtin_amdgcn_cosf(r2[u]) : w0 * __builtin_amdgcn_cosf(r2[u]);
                                     }
                                 }
                             }
@@ -526,16 +568,20 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             auto epi = [&](auto kpass) {
                 const std::false_type F{};
                 const std::true_type T{};
+                auto ep = [&](auto l0, auto rbk, auto lds) {
+                    if constexpr (SAVING) epilogue_pk(kpass, l0, rbk, lds);
+                    else epilogue(kpass, l0, rbk, lds);
+                };
                 if (i == 0) {
-                    if (rb && srb_on) epilogue(kpass, T, T, T);
-                    else if (rb) epilogue(kpass, T, T, F);
-                    else epilogue(kpass, T, F, F);
+                    if (rb && srb_on) ep(T, T, T);
+                    else if (rb) ep(T, T, F);
+                    else ep(T, F, F);
                 } else if (rb && srb_on) {
-                    epilogue(kpass, F, T, T);
+                    ep(F, T, T);
                 } else if (rb) {
-                    epilogue(kpass, F, T, F);
+                    ep(F, T, F);
                 } else {
-                    epilogue(kpass, F, F, F);
+                    ep(F, F, F);
                 }
             };
             // DREG: sin → the image as above, D = cos (×w0 at layer 0) straight from the registers
