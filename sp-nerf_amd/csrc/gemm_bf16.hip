@@ -461,6 +461,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void k_gemm_nt_bf16w(NT16Args g, in
 // Same k order as k_gemm_nt_bf16w (16-wide k blocks in increasing k): bit-identical outputs.
 // K and K1 must be multiples of 32 (host-checked).
 constexpr int ND_K = 32, ND_STAGES = 4, ND_STG = 512 * 64;
+#ifndef SPN_NT_ADDR
+#define SPN_NT_ADDR 1  // DMA sources as a uniform base + 32-bit lane offset (0: 64-bit per-lane pointers, A/B builds)
+#endif
 #ifndef SPN_NT16_NT
 // the DMA NT GEMM's C / Dout stores non-temporal (glc slc; A/B builds): C4 26.20 / 26.19 -> 26.13 /
 // 26.11 ms, C4@512 level (tools/gpu_r3x.sh) — within the box's spread, so off
@@ -541,9 +544,18 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             const int q = wid + 8 * i;
             const int row = 16 * q + (el >> 2);
             const int c8 = ((el & 3) ^ ((row >> 2) & 3)) * 8;
+#if SPN_NT_ADDR
+            // a wave-uniform 64-bit base and a 32-bit per-lane byte offset (P·K < 2^31 / 2 is host-
+            // checked): the saddr + voffset form, no 64-bit VALU address per DMA
+            const char* base = i < 2 ? reinterpret_cast<const char*>(pa) : reinterpret_cast<const char*>(g.B + k0);
+            const uint32_t off = i < 2 ? (uint32_t)(min(bm + row, g.M - 1) * lda + c8) * 2u
+                                       : (uint32_t)(min(bn + row - 256, g.N - 1) * g.ldb + c8) * 2u;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(base + off), (lds_ptr_t)(smem + stg * ND_STG + q * 1024), 16, 0, 0);
+#else
             const bf16* src = i < 2 ? pa + (int64_t)min(bm + row, g.M - 1) * lda + c8
                                     : g.B + (int64_t)min(bn + row - 256, g.N - 1) * g.ldb + k0 + c8;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(smem + stg * ND_STG + q * 1024), 16, 0, 0);
+#endif
         }
         if (i == 3 && ++is_k == nk) {
             is_k = 0;
@@ -2720,6 +2732,8 @@ int32_t gemm_nt_bf16(const NT16Args& a, hipStream_t s, int variant) {
             "gemm_nt_bf16: a split K1=%d must be a multiple of %d with A2 set", a.K1, HK);
     SPN_ARG(a.lda % 8 == 0 && a.ldb % 8 == 0 && a.ldc % 8 == 0 && (a.K1 == a.K || a.lda2 % 8 == 0),
             "gemm_nt_bf16: leading dims must be multiples of 8");
+    SPN_ARG((int64_t)a.M * std::max(a.lda, a.K1 == a.K ? 0 : a.lda2) < (1ll << 31) && (int64_t)a.N * a.ldb < (1ll << 31),
+            "gemm_nt_bf16: operands past 2^31 elements (32-bit DMA offsets)");
     SPN_ARG(!a.Dout || a.ld_dout % 8 == 0, "gemm_nt_bf16: ld_dout");
     SPN_ARG(!a.Dmul || a.ld_dmul % 8 == 0, "gemm_nt_bf16: ld_dmul");
     SPN_ARG(a.rowbias == nullptr || (a.rows_per_ray > 0 && a.ld_rb % 4 == 0), "gemm_nt_bf16: rowbias");
