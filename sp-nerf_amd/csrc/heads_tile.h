@@ -170,7 +170,7 @@ __device__ __forceinline__ void heads_tile(GA& g, KA& k, char* smem, float* ost,
     // after the barriers that follow the σ head)
     const int64_t ray0 = (int)p0 / g.S;  // P < 2^31 / 512 (host checks): 32-bit divisions
     const int nray = (int)((int)(std::min<int64_t>(p0 + TM, (int64_t)g.P) - 1) / g.S - ray0) + 1;
-    const bool rq_lds = RQ && full && nray <= RQ_RAYS && !(g.dbg & 4);  // block-uniform (dbg 4: A/B)
+    const bool rq_lds = RQ && full && nray <= RQ_RAYS && !((kTrunkAbl ? g.dbg : 0) & 4);  // block-uniform (dbg 4: A/B)
     if (rq_lds)
         for (int i = tid; i < nray * 2 * HH; i += 512) srq[i] = g.rbQ[ray0 * (2 * HH) + i];
     // σ on MFMA (narrow_mm), the 8 waves' partials summed in wave order
@@ -378,6 +378,9 @@ __device__ __forceinline__ void image_out(const char* smem, __amdgpu_buffer_rsrc
     }
 }
 
+#ifndef SPN_HEADS_ZC
+#define SPN_HEADS_ZC 0  // 1: layer_mm_d k-step 0 with the MFMA C = 0 (no accumulator zeroing) — spills 172 B, heads 2.56 -> 3.0 ms per C4 step
+#endif
 // layer_prime / layer_mm with a ring of DEPTH k-steps (the 256-wide layers run 8 deep: half the
 // MFMAs per k-step of the 512-wide ones, the same register cost and time of cover), drain(group)
 // after each group of DEPTH k-steps (behind that group's refills); the ring must be primed
@@ -394,43 +397,56 @@ __device__ __forceinline__ void layer_mm_d(const bf16* __restrict__ wsrc, int nk
                                            f32x16 (&acc)[NA][NJ], u32x4 (&ring)[DEPTH][NA], Drain&& drain) {
     constexpr int TPD = DEPTH;
     const int r32 = lane & 31, h = lane >> 5, sw = r32 & 15;
+    const char* brow = smem + r32 * 1024;
+    bf16x8 bc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
+    // one k-step; k-step 0 (kfirst) takes the accumulators' C operand as the inline constant 0
+    // instead of zeroed registers (no v_mov per accumulator register per layer; the same sums)
+    auto kstep = [&](int ks, int d, auto kfirst) {
+        constexpr bool FIRST = decltype(kfirst)::value;
+        const int offn = ((2 * (ks + 1) + h) ^ sw) << 4;
+        bf16x8 bn[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int a = 0; a < NA; ++a)
+                acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ring[d][a]), bc[j],
+                                                                  FIRST ? f32x16{} : acc[a][j], 0, 0, 0);
+        const int kn = min(ks + TPD, nks - 1);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) ring[d][a] = ldg16(wsrc + (kn * NA + a) * 512);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, NA, 0);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bc[j] = bn[j];
+    };
+#if SPN_HEADS_ZC
+    // the first group peeled (k-step 0 with C = 0), then groups TPD.. as before
+    kstep(0, 0, std::true_type{});
+#pragma unroll
+    for (int d = 1; d < TPD; ++d) kstep(d, d, std::false_type{});
+    drain(0);
+    constexpr int kfirst = TPD;
+#else
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][j][r] = 0.f;
-    const char* brow = smem + r32 * 1024;
-    bf16x8 bc[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bc[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + ((h ^ sw) << 4));
+    constexpr int kfirst = 0;
+#endif
 #pragma unroll 1
-    for (int ks0 = 0; ks0 < nks; ks0 += TPD) {
+    for (int ks0 = kfirst; ks0 < nks; ks0 += TPD) {
 #pragma unroll
-        for (int d = 0; d < TPD; ++d) {
-            const int ks = ks0 + d;
-            const int offn = ((2 * (ks + 1) + h) ^ sw) << 4;
-            bf16x8 bn[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(brow + j * 32768 + offn);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-#pragma unroll
-                for (int a = 0; a < NA; ++a)
-                    acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ring[d][a]), bc[j],
-                                                                      acc[a][j], 0, 0, 0);
-            const int kn = min(ks + TPD, nks - 1);
-#pragma unroll
-            for (int a = 0; a < NA; ++a) ring[d][a] = ldg16(wsrc + (kn * NA + a) * 512);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, NA, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x020, NA, 0);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) bc[j] = bn[j];
-        }
+        for (int d = 0; d < TPD; ++d) kstep(ks0 + d, d, std::false_type{});
         drain(ks0 / TPD);
     }
 }
@@ -490,7 +506,9 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     constexpr int D1 = 8;  // ring depth of the 256-wide layers (sem hidden, sun_v 2 / 3)
     constexpr int D2 = SPN_HEADS_D2;  // ... of the 512-wide ones (feat, Q)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int dbg = g.dbg;
+    // (product build: 0 — a runtime flag here made every sine epilogue compute sin, cos AND the
+    // ablation's alternative, then select per element: two v_cndmask per element)
+    const int dbg = kTrunkAbl ? g.dbg : 0;
     const float* Pk = g.packed;
     const bf16* P16 = reinterpret_cast<const bf16*>(g.packed);
     const bool full = g.mode == 0;
