@@ -44,6 +44,13 @@ int num_cus();
 // for kLayoutCus (a pure function of the model dimensions, whatever device is current), and a
 // launch never uses more splits than that (split_cus: the device's CUs, capped at kLayoutCus)
 constexpr int kLayoutCus = 256;
+// Profiling-ablation arguments of the kernels (dbg, nt) vary only in a -DSPN_ABLATIONS build; the
+// product build folds them to their defaults, so no runtime flag branches a hot loop
+#ifdef SPN_ABLATIONS
+constexpr bool kAblBuild = true;
+#else
+constexpr bool kAblBuild = false;
+#endif
 inline int split_cus() {
     const int n = num_cus();
     return n < kLayoutCus ? n : kLayoutCus;

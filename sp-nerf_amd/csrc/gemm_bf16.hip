@@ -520,6 +520,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
     typedef __attribute__((address_space(1))) void* gbl_ptr_t;
     constexpr int MI = 4, NJ = 2;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int gdbg = kAblBuild ? g.dbg : 0;  // (product: no ablation branch in the k-loop)
     const int nN = (g.N + 255) / 256;
     const int G = gridDim.x;
     int t = xcd_remap(blockIdx.x, G);
@@ -539,7 +540,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
         const bf16* pa = seg2 ? g.A2 + (k0 - g.K1) : g.A + k0;
         const int lda = seg2 ? g.lda2 : g.lda;
         const int el = opaque(lane);
-        const int ni = (g.dbg & 16) ? 2 : 4;  // ablation: A only
+        const int ni = (gdbg & 16) ? 2 : 4;  // ablation: A only
         if (i < ni) {
             const int q = wid + 8 * i;
             const int row = 16 * q + (el >> 2);
@@ -682,8 +683,8 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             // wrong); the barrier publishes every wave's DMAs and retires the reads of stage
             // (gs + 3) % 4 (step gs - 1, or the previous epilogue's staging)
             ND_STAMP(0);
-            if (g.dbg & 16) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else if (!(g.dbg & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            if (gdbg & 16) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (!(gdbg & 4)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             ND_STAMP(1);
             __builtin_amdgcn_s_barrier();
             ND_STAMP(2);
@@ -697,11 +698,11 @@ __global__ __launch_bounds__(512) void k_gemm_nt_bf16d(NT16Args g, int ntiles) {
             } else {
                 issue((gs + 3) % ND_STAGES);
                 ND_STAMP(3);
-                if (!(g.dbg & 1)) compute(gs % ND_STAGES, [](int) {});
+                if (!(gdbg & 1)) compute(gs % ND_STAGES, [](int) {});
             }
         }
         ND_STAMP(4);
-        if (g.dbg & 2) {
+        if (gdbg & 2) {
             if (tn >= ntiles) break;
             t = tn;
             continue;

@@ -10,11 +10,7 @@ constexpr int kTrunkMaxL = 16;
 // vary only in a -DSPN_ABLATIONS build; the product build folds them to the product defaults, so
 // no store or copy-out sits behind a runtime branch (a branch around a store made hipcc's later
 // vmcnt waits conservative: they then waited for the stores as well)
-#ifdef SPN_ABLATIONS
-constexpr bool kTrunkAbl = true;
-#else
-constexpr bool kTrunkAbl = false;
-#endif
+constexpr bool kTrunkAbl = kAblBuild;
 
 // fc_net layers 1 .. L-1 over P points: H1 (layer-0 output, [P][512] bf16) in, the output of
 // layer i to Hs[i] and its derivative cos(z) (with zround: Z itself) to Ds[i] where non-null
