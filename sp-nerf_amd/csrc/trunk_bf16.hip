@@ -40,6 +40,9 @@
 #ifndef SPN_TRUNK_EPI_PK
 #define SPN_TRUNK_EPI_PK 1  // the 128-point epilogue's bias adds as packed pairs (0: scalar, A/B builds)
 #endif
+#ifndef SPN_TRUNK_DCOLS
+#define SPN_TRUNK_DCOLS 1  // saving 128-point tiles: each wave copies out its own D columns (0: between barriers)
+#endif
 #ifndef SPN_TRUNK_BUFSTORE
 #define SPN_TRUNK_BUFSTORE 1  // copy-outs through buffer descriptors (0: guarded stores, A/B builds)
 #endif
@@ -188,6 +191,31 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
         if (gdbg & 1) return;
 #pragma unroll
         for (int q0 = 0; q0 < CPT; q0 += 4) copy_out(img, dst, p0, q0, std::integral_constant<int, 4>{});
+    };
+
+    // wave w's own feature columns [64w, 64w + 64) of the image (the chunks its epilogue wrote) to
+    // HBM rows p0 + row: lane l takes chunk 8w + (l & 7) of rows 8q + (l >> 3), so 8 lanes store
+    // one row's whole 128-B line; 4 chunks per lane at a time (the accumulators are still live)
+    auto copy_cols = [&](bf16* dst, int64_t p0) {
+        if (gdbg & 1) return;
+        const int l = opaque(lane);
+        const int rows = (int)std::min<int64_t>(TMt, g.P - p0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + p0 * TW, 0, rows * TW * 2, 0x00020000);
+        const int ch = 8 * w + (l & 7), r0 = l >> 3;
+        asm volatile("" ::: "memory");  // the epilogue's image writes (other lanes' chunks) stay before
+#pragma unroll
+        for (int q0 = 0; q0 < TMt / 8; q0 += 4) {
+            u32x4 v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(smem + act_off(8 * (q0 + q) + r0, ch));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int off = ((8 * (q0 + q) + r0) * TW + ch * 8) * 2;
+                if (gnt & 1) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // block-uniform: glc slc
+                else __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 0);
+            }
+        }
+        asm volatile("" ::: "memory");  // ... and the next pass's writes after
     };
 
     // σ pre-activation of the tile's points from the last layer's image (TrunkArgs::sig_hsave):
@@ -702,9 +730,18 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
             } else {
                 if (Ds) {  // block-uniform
                     epi(std::integral_constant<int, 0>{});
-                    __syncthreads();
-                    copy_all(smem, Ds, p0);
-                    __syncthreads();  // the sin pass overwrites the image
+#if SPN_TRUNK_DCOLS
+                    if constexpr (SAVING) {
+                        // each wave copies out the columns it wrote itself: no barriers (one wave's
+                        // LDS accesses run in order), whole 128-B lines per 8 lanes
+                        copy_cols(Ds, p0);
+                    } else
+#endif
+                    {
+                        __syncthreads();
+                        copy_all(smem, Ds, p0);
+                        __syncthreads();  // the sin pass overwrites the image
+                    }
                 }
                 epi(std::integral_constant<int, 1>{});
                 if (last) {
@@ -747,7 +784,7 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
     __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 8 * TW * 4];  // + the column-sum partials
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     const int sw = r32 & 15;
-    const int gnt = kTrunkAbl ? g.nt : 0;    // product: trunk_bwd_nt 0
+    const int gnt = kTrunkAbl ? g.nt : 2;    // product: trunk_bwd_nt 2 (non-temporal D loads)
     const int gdbg = kTrunkAbl ? g.dbg : 0;
     typedef const __attribute__((address_space(4))) TrunkBwdArgs* KArgs;
     const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
@@ -851,7 +888,7 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
 #pragma unroll
             for (int q = 0; q < CPT; ++q) {
                 const int c = st + 512 * q;
-                if (gnt & 2)  // (ablation build only) non-temporal
+                if (gnt & 2)  // non-temporal (glc slc): the product's; 0 only in ablation builds
                     dv[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (std::min(c >> 6, trows - 1) * TW + (c & 63) * 8) * 2, 0, 3);
                 else
                     dv[q] = tile_load(rs, trows, c >> 6, c & 63);
@@ -1007,9 +1044,12 @@ int g_fused_bwd = 1;
 // 5.05-5.10 -> 5.25-5.27 ms per step, C4@512 4.42 -> 4.47 ms): unlike the forward's sin/cos, the
 // x D epilogue is too short to cover the stores, which then hold up the next k-loop's refills
 int g_trunk_bwd_dreg = 0;
-// dX chain: 1 = non-temporal dZ copy-outs, 2 = non-temporal D loads — level either way (C4 26.27 /
-// 26.27 / 26.22 / 26.23 ms for 0 / 1 / 2 / 3, C4@512 4.09 / 4.08 / 4.09 / 4.10: tools/gpu_r3w.sh)
-int g_trunk_bwd_nt = 0;
+// dX chain: 1 = non-temporal dZ copy-outs, 2 = non-temporal D loads.  Round 3 (the kernel then): level
+// either way (C4 26.27 / 26.27 / 26.22 / 26.23 ms for 0 / 1 / 2 / 3, tools/gpu_r3w.sh).  Round 6 (32-bit
+// buffer loads, branch-free copy-outs): 2 is the default — dX chain 5.17 / 5.18 -> 4.96 / 4.99 ms per C4
+// step, the same HBM bytes (PMC FETCH_SIZE 5.235 GB per launch either way; without D loads 1.48 GB:
+// D is read exactly once, the rest over dZ_top is weight re-fetch; tools/dx_probe.sh)
+int g_trunk_bwd_nt = 2;
 
 int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes) {
     SPN_ARG(a.P >= 0 && a.L >= 2 && a.L <= kTrunkMaxL, "trunk_bwd_bf16: bad sizes (P=%lld L=%d)", (long long)a.P, a.L);

@@ -11,9 +11,6 @@ import os
 import re
 import sys
 
-src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_bench"
-dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r03"
-RUNS = sys.argv[3:] or ["c4:4096", "c5:32768"]
 # rocprof kernel name → the library's profiling class (one class per kernel function)
 CLASSES = [(r"k_gemm_nt_bf16d<true", "gemm_nt_bf16d_dmul"), (r"k_gemm_nt_bf16d<", "gemm_nt_bf16d"),
            (r"k_gemm_nt_bf16w", "gemm_nt_bf16w"), (r"k_gemm_nt_bf16<", "gemm_nt_bf16"),
@@ -35,35 +32,43 @@ def class_of(name):
     return None
 
 
-for run in RUNS:
-    cfg, rays = run.split(":")
-    tag = f"{cfg}_rays{rays}"
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        for f in glob.glob(os.path.join(src, f"{tag}_{ctr}", "**", "*counter_collection.csv"), recursive=True):
-            per = collections.defaultdict(float)
-            names = {}
-            for r in csv.DictReader(open(f)):
-                d = int(r["Dispatch_Id"])
-                per[d] += float(r["Counter_Value"])
-                names[d] = r["Kernel_Name"]
-            for d, v in per.items():
-                cls = class_of(names[d])
-                if cls:
-                    acc[cls][ctr].append(v)
-    out = {}
-    for cls, c in acc.items():
-        if not c.get("FETCH_SIZE") or not c.get("WRITE_SIZE"):
-            continue
-        fetch = 2 * 1024 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
-        write = 1024 * sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
-        out[cls] = {"launches": len(c["FETCH_SIZE"]), "hbm_read_bytes_per_launch": fetch,
-                    "hbm_write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
-                    "rays_per_rank": int(rays),
-                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over `bench.py --config "
-                              f"{cfg} --global-batch {rays} --eager --steps 2 --warmup 1`; bytes = 2*FETCH_SIZE + "
-                              "WRITE_SIZE (KiB, gfx950 correction, MI355X_MICROARCH.md HBM)"}
-    if out:
-        os.makedirs(dst, exist_ok=True)
-        json.dump(out, open(os.path.join(dst, f"traffic_{tag}.json"), "w"), indent=1)
-        print(tag, {k: round(v["hbm_bytes_per_launch"] / 1e6, 1) for k, v in out.items()}, "MB/launch")
+def main():
+    src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_bench"
+    dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r03"
+    RUNS = sys.argv[3:] or ["c4:4096", "c5:32768"]
+    for run in RUNS:
+        cfg, rays = run.split(":")
+        tag = f"{cfg}_rays{rays}"
+        acc = collections.defaultdict(lambda: collections.defaultdict(list))
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            for f in glob.glob(os.path.join(src, f"{tag}_{ctr}", "**", "*counter_collection.csv"), recursive=True):
+                per = collections.defaultdict(float)
+                names = {}
+                for r in csv.DictReader(open(f)):
+                    d = int(r["Dispatch_Id"])
+                    per[d] += float(r["Counter_Value"])
+                    names[d] = r["Kernel_Name"]
+                for d, v in per.items():
+                    cls = class_of(names[d])
+                    if cls:
+                        acc[cls][ctr].append(v)
+        out = {}
+        for cls, c in acc.items():
+            if not c.get("FETCH_SIZE") or not c.get("WRITE_SIZE"):
+                continue
+            fetch = 2 * 1024 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"])
+            write = 1024 * sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
+            out[cls] = {"launches": len(c["FETCH_SIZE"]), "hbm_read_bytes_per_launch": fetch,
+                        "hbm_write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
+                        "rays_per_rank": int(rays),
+                        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over `bench.py --config "
+                                  f"{cfg} --global-batch {rays} --eager --steps 2 --warmup 1`; bytes = 2*FETCH_SIZE + "
+                                  "WRITE_SIZE (KiB, gfx950 correction, MI355X_MICROARCH.md HBM)"}
+        if out:
+            os.makedirs(dst, exist_ok=True)
+            json.dump(out, open(os.path.join(dst, f"traffic_{tag}.json"), "w"), indent=1)
+            print(tag, {k: round(v["hbm_bytes_per_launch"] / 1e6, 1) for k, v in out.items()}, "MB/launch")
+
+
+if __name__ == "__main__":
+    main()
