@@ -378,6 +378,30 @@ __device__ __forceinline__ void image_out(const char* smem, __amdgpu_buffer_rsrc
     }
 }
 
+#ifndef SPN_HEADS_DCOLS
+#define SPN_HEADS_DCOLS 1  // the wide layers' D (cos) through the wave's own image columns (0: register stores)
+#endif
+// rows 32j .. 32j + 31 of this wave's own image columns [fb, fb + 32·NA) (written by this wave
+// only, after the barrier that ends every wave's reads of the image) to a descriptor (ld
+// elements): 4·NA lanes store one row's whole 64·NA-byte piece (the register stores of
+// store_rows16 write 32 B per row and instruction).  One wave's LDS accesses run in order; the
+// memory clobbers keep the compiler from moving the epilogue's image writes across the reads.
+template <int NA>
+__device__ __forceinline__ void cols_out(const char* smem, __amdgpu_buffer_rsrc_t rs, int ld, int fb, int j, int lane_) {
+    constexpr int LPR = 4 * NA;    // lanes per row (16 B each)
+    constexpr int RPI = 64 / LPR;  // rows per instruction
+    constexpr int N = 32 / RPI;    // instructions
+    const int l = opaque(lane_);
+    const int ch = (fb >> 3) + l % LPR, r0 = 32 * j + l / LPR;
+    asm volatile("" ::: "memory");
+    u32x4 v[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = *reinterpret_cast<const u32x4*>(smem + img_off(r0 + RPI * q, ch));
+#pragma unroll
+    for (int q = 0; q < N; ++q) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, ((r0 + RPI * q) * ld + 8 * ch) * 2, 0, 0);
+    asm volatile("" ::: "memory");
+}
+
 #ifndef SPN_HEADS_ZC
 #define SPN_HEADS_ZC 0  // 1: layer_mm_d k-step 0 with the MFMA C = 0 (no accumulator zeroing) — spills 172 B, heads 2.56 -> 3.0 ms per C4 step
 #endif
@@ -619,6 +643,37 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
         const auto rsD = rsrc_r(g.DQ, g.ldQ);
         const bool dq = full || w < 4;  // wave-uniform
         const int rlast = (int)(g.P - 1 - p0);  // P < 2^31 / 512 (host check)
+#if SPN_HEADS_DCOLS
+        // per point tile j: cos into the wave's own image columns, those rows out to DQ, then sin
+        // over them (the sines wait in registers)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            u32x2 yq[2][4];
+            const int64_t ray = ((int)p0 + std::min(32 * j + er32, rlast)) / g.S;
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                    const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_Q + f0);
+                    const f32x4 rv = ld4(g.rbQ + ray * (2 * HH) + f0);
+                    float y[4], cs[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) sincos((acc[a][j][4 * gq + e] + bv[e]) + rv[e], &y[e], &cs[e]);
+                    put4(32 * j + er32, f0, cs);
+                    yq[a][gq] = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                }
+            if (dq) cols_out<2>(smem, rsD, g.ldQ, 64 * w, j, lane);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                    *reinterpret_cast<u32x2*>(smem + img_off(32 * j + er32, f0 >> 3) + 8 * ((f0 >> 2) & 1)) = yq[a][gq];
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#else
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -639,6 +694,7 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
                 if (dq) store_rows16(rsD, g.ldQ, 64 * w + 32 * a, 32 * j + er32, eh, cq);
                 __builtin_amdgcn_sched_barrier(0);
             }
+#endif
         __syncthreads();
     }
     if (full) {
@@ -689,10 +745,24 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
                 float y[4], cs[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) sincos(acc[0][j][4 * gq + e] + bv[e], &y[e], &cs[e]);
+#if SPN_HEADS_DCOLS  // cos through the own columns, then sin over them (cq holds the sines)
+                put4(32 * j + er32, f0, cs);
+                cq[gq] = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+#else
                 put4(32 * j + er32, f0, y);
                 cq[gq] = u32x2{pack2(cs[0], cs[1]), pack2(cs[2], cs[3])};
+#endif
             }
+#if SPN_HEADS_DCOLS
+            cols_out<1>(smem, rsD, HH, 32 * w, j, lane);
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 32 * w + 8 * gq + 4 * eh;
+                *reinterpret_cast<u32x2*>(smem + img_off(32 * j + er32, f0 >> 3) + 8 * ((f0 >> 2) & 1)) = cq[gq];
+            }
+#else
             store_rows16(rsD, HH, 32 * w, 32 * j + er32, eh, cq);
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
@@ -717,10 +787,24 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
                 float y[4], cs[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) sincos(acc[0][j][4 * gq + e] + bv[e], &y[e], &cs[e]);
+#if SPN_HEADS_DCOLS  // cos through the own columns, then sin over them (cq holds the sines)
+                put4(32 * j + er32, f0, cs);
+                cq[gq] = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+#else
                 put4(32 * j + er32, f0, y);
                 cq[gq] = u32x2{pack2(cs[0], cs[1]), pack2(cs[2], cs[3])};
+#endif
             }
+#if SPN_HEADS_DCOLS
+            cols_out<1>(smem, rsD, HH, 32 * w, j, lane);
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 32 * w + 8 * gq + 4 * eh;
+                *reinterpret_cast<u32x2*>(smem + img_off(32 * j + er32, f0 >> 3) + 8 * ((f0 >> 2) & 1)) = cq[gq];
+            }
+#else
             store_rows16(rsD, HH, 32 * w, 32 * j + er32, eh, cq);
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();

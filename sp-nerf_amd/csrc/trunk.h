@@ -103,7 +103,7 @@ struct TrunkBwdArgs {
     int64_t P = 0;
     int L = 0;
     int dbg = 0;  // g_trunk_dbg (profiling ablations, outputs invalid): 1 = no dZ copy-outs, 2 = no D loads
-    int nt = 2;   // g_trunk_bwd_nt: 1 = non-temporal dZ copy-outs, 2 = non-temporal D loads (the default)
+    int nt = 3;   // g_trunk_bwd_nt: 1 = non-temporal dZ copy-outs, 2 = non-temporal D loads (3: the default)
     // per-tile column sums of dZ_l for l = rs_layer[k] (-1: none) into Rsum[k][tile][512]: the
     // per-ray sums of layer 0's and the skip layer's dZ (semantic columns) from the LDS image
     // instead of a re-read of dZ (k_ray_rowsum16).  Needs P % 64 == 0; the order is tile_colsum's

@@ -784,7 +784,7 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
     __shared__ __attribute__((aligned(16))) char smem[2 * IMG + 8 * TW * 4];  // + the column-sum partials
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r32 = lane & 31, h = lane >> 5;
     const int sw = r32 & 15;
-    const int gnt = kTrunkAbl ? g.nt : 2;    // product: trunk_bwd_nt 2 (non-temporal D loads)
+    const int gnt = kTrunkAbl ? g.nt : 3;    // product: trunk_bwd_nt 3 (non-temporal D loads and dZ stores)
     const int gdbg = kTrunkAbl ? g.dbg : 0;
     typedef const __attribute__((address_space(4))) TrunkBwdArgs* KArgs;
     const KArgs ka = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
@@ -821,7 +821,7 @@ __global__ __launch_bounds__(512) void k_trunk_bwd_bf16(TrunkBwdArgs g, int ntil
         for (int q = 0; q < n; ++q) {
             const int c = ct + 512 * (q0 + q);
             const int off = ((c >> 6) * TW + (c & 63) * 8) * 2;
-            if (gnt & 1) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // (ablation build only)
+            if (gnt & 1) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 3);  // the product's (glc slc)
             else __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, off, 0, 0);
         }
     };
@@ -1048,8 +1048,10 @@ int g_trunk_bwd_dreg = 0;
 // either way (C4 26.27 / 26.27 / 26.22 / 26.23 ms for 0 / 1 / 2 / 3, tools/gpu_r3w.sh).  Round 6 (32-bit
 // buffer loads, branch-free copy-outs): 2 is the default — dX chain 5.17 / 5.18 -> 4.96 / 4.99 ms per C4
 // step, the same HBM bytes (PMC FETCH_SIZE 5.235 GB per launch either way; without D loads 1.48 GB:
-// D is read exactly once, the rest over dZ_top is weight re-fetch; tools/dx_probe.sh)
-int g_trunk_bwd_nt = 2;
+// D is read exactly once, the rest over dZ_top is weight re-fetch; tools/dx_probe.sh); 3 (the dZ
+// copy-outs — whole 1-KB rows — non-temporal too) is the default since: dX chain 5.06 / 5.01 -> 4.97 /
+// 4.97 ms, C4 24.15 / 24.18 -> 24.05 / 24.07 (ablation build, pairs in one call)
+int g_trunk_bwd_nt = 3;
 
 int32_t trunk_bwd_bf16(const TrunkBwdArgs& a, hipStream_t s, double flop, double bytes) {
     SPN_ARG(a.P >= 0 && a.L >= 2 && a.L <= kTrunkMaxL, "trunk_bwd_bf16: bad sizes (P=%lld L=%d)", (long long)a.P, a.L);
