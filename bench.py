@@ -1082,6 +1082,7 @@ class TrainStep:
         # Batch indices live in static buffers so that the captured step reads each new batch.
         # (this rank's rows are a view of the global batch: one copy per step)
         self.gidx_s = torch.empty(B * world, dtype=torch.int64, device=dev)
+        self.one = torch.ones((), device=dev)
         self.idx_s = self.gidx_s[rank * B:(rank + 1) * B]
         # this rank's rows of every per-ray field in one launch, into static buffers
         self.gather = None if getattr(a, "torch_gather", False) else dp.BatchGather(self.R, B)
@@ -1135,7 +1136,7 @@ class TrainStep:
         if self.floss is not None:   # the trainer's loss sum (main.py:143-174) in two kernels
             loss, _ = self.floss(res, bt["rgbs"], depths, valid, dstd, sem,
                                  labels_global=R["sems"][gidx] if (world > 1 and sem is not None) else None, world=world)
-            loss.backward()
+            loss.backward(self.one)   # d loss / d loss = 1 from a static tensor (no fill launch per step)
             return loss.detach()
         loss, _ = self.sloss(res, bt["rgbs"])
         if self.dloss is not None:

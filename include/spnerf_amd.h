@@ -243,6 +243,13 @@ int32_t spnerf_adam_step(int32_t n, void* const* params, const void* const* grad
 int32_t spnerf_gather_rows(const int64_t* idx, int64_t n, int32_t nfields, const void* const* src,
                            const int64_t* src_rows, const int32_t* row_bytes, void* const* dst, void* stream);
 
+/* ---- a render's random-state step (the on-device Philox state of spnerf_rng above): state[1] += 1,
+ * then snap[0..1] = state[0..1], in one launch on `stream` — the render's kernels (and its
+ * backward's) read the snapshot, so a later render advancing the state changes none of its draws.
+ * Replaces the torch in-place add and clone of the host binding (rng.py PhiloxRandom.begin_render):
+ * one launch instead of two per training step.  state and snap: device int64[2]. */
+int32_t spnerf_rng_begin(int64_t* state, int64_t* snap, void* stream);
+
 /* ---- gradient readiness marks for data parallelism (no reference counterpart: the reference
  *      trains on one GPU, main.py:322-337).  A backward passes n_marks = layers + 2 points after
  *      which groups of parameter gradients are final: mark 0 after the output heads', mark

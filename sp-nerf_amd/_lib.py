@@ -91,6 +91,7 @@ SIGNATURES = {
                                    POINTER(c_int64), c_double, c_double, c_double, c_double, c_int32, c_void_p]),
     "spnerf_gather_rows": (c_int32, [c_void_p, c_int64, c_int32, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int32),
                                      POINTER(c_void_p), c_void_p]),
+    "spnerf_rng_begin": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "spnerf_prof_enable": (c_int32, [c_int32]),
     "spnerf_prof_reset": (c_int32, []),
     "spnerf_prof_read": (c_int32, [c_char_p, POINTER(c_int64), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),

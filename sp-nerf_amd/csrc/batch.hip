@@ -37,9 +37,24 @@ __global__ __launch_bounds__(256) void k_gather_rows(GatherArgs g) {
     g.dst[f][row * wpr + w] = (r < 0 || r >= g.src_rows[f]) ? 0xFFFFFFFFu : g.src[f][r * wpr + w];
 }
 
+// one thread: the render's step advanced and snapshotted (spnerf_rng_begin)
+__global__ void k_rng_begin(int64_t* state, int64_t* snap) {
+    const int64_t step = state[1] + 1;
+    state[1] = step;
+    snap[0] = state[0];
+    snap[1] = step;
+}
+
 }  // namespace spn
 
 using namespace spn;
+
+extern "C" int32_t spnerf_rng_begin(int64_t* state, int64_t* snap, void* stream) {
+    SPN_ARG(state && snap && state != snap, "rng_begin: null or aliased state / snapshot");
+    hipLaunchKernelGGL(k_rng_begin, dim3(1), dim3(1), 0, (hipStream_t)stream, state, snap);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
 
 extern "C" int32_t spnerf_gather_rows(const int64_t* idx, int64_t n, int32_t nfields, const void* const* src,
                                       const int64_t* src_rows, const int32_t* row_bytes, void* const* dst,

@@ -362,6 +362,9 @@ __device__ __forceinline__ void store_rows16(__amdgpu_buffer_rsrc_t rs, int ld, 
 
 // chunks [q0, q0 + N) (per thread) of image columns [0, 8·NCH) to the rows of a descriptor (ld
 // elements): chunk c = tid + 512·q, consecutive lanes on consecutive 16-B pieces of a row
+#ifndef SPN_HEADS_NT
+#define SPN_HEADS_NT 3  // training heads' stores non-temporal (glc slc): 1 = image copy-outs (whole rows), 2 = the D columns
+#endif
 template <int NCH, int N>
 __device__ __forceinline__ void image_out(const char* smem, __amdgpu_buffer_rsrc_t rs, int ld, int tid_, int q0) {
     const int tid = opaque(tid_);  // per-thread offsets computed here, not hoisted across the tile loop
@@ -374,7 +377,7 @@ __device__ __forceinline__ void image_out(const char* smem, __amdgpu_buffer_rsrc
 #pragma unroll
     for (int q = 0; q < N; ++q) {
         const int c = tid + 512 * (q0 + q);
-        __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, ((c / NCH) * ld + 8 * (c % NCH)) * 2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, ((c / NCH) * ld + 8 * (c % NCH)) * 2, 0, (SPN_HEADS_NT & 1) ? 3 : 0);
     }
 }
 
@@ -398,7 +401,8 @@ __device__ __forceinline__ void cols_out(const char* smem, __amdgpu_buffer_rsrc_
 #pragma unroll
     for (int q = 0; q < N; ++q) v[q] = *reinterpret_cast<const u32x4*>(smem + img_off(r0 + RPI * q, ch));
 #pragma unroll
-    for (int q = 0; q < N; ++q) __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, ((r0 + RPI * q) * ld + 8 * ch) * 2, 0, 0);
+    for (int q = 0; q < N; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(v[q], rs, ((r0 + RPI * q) * ld + 8 * ch) * 2, 0, (SPN_HEADS_NT & 2) ? 3 : 0);
     asm volatile("" ::: "memory");
 }
 

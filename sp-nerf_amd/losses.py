@@ -197,12 +197,16 @@ class _RenderLoss(torch.autograd.Function):
         ctx.save_for_backward(rgb, sun_sc, depth, logits, out)
         terms = out[1:6]
         ctx.mark_non_differentiable(terms)
+        # the terms take no gradient: not materialised as zeros (one fill launch per step)
+        ctx.set_materialize_grads(False)
         return out[0], terms
 
     @staticmethod
     def backward(ctx, g_loss, g_terms):
         from . import _lib
         rgb, sun_sc, depth, logits, out = ctx.saved_tensors
+        if g_loss is None:
+            return None, None, None, None, None
         cfg = ctx.cfg
         B, S, C = cfg["B"], cfg["S"], cfg["C"]
         g = g_loss.contiguous().reshape(1)

@@ -90,9 +90,12 @@ class PhiloxRandom:
         elif self._state.device != torch.device(device):
             # moved with its DEVICE step: graph replays advance that one, not the host mirror
             self._state = self._state.to(device)
-        self._state[1:].add_(1)
+        # state[1] += 1 and the snapshot in one launch (spnerf_rng_begin)
+        from . import _lib
+        self._snap = torch.empty(2, dtype=torch.int64, device=self._state.device)
+        _lib.check(_lib.lib().spnerf_rng_begin(_lib.ptr(self._state), _lib.ptr(self._snap), _lib.stream_of(self._state)),
+                   "rng_begin")
         self._host_step += 1
-        self._snap = self._state.clone()
         self._slot = 0
 
     def reset_step(self, step: int = -1) -> None:

@@ -61,3 +61,31 @@ def test_gather_rows_poisons_out_of_range_indices():
             assert torch.isnan(out[k][bad]).all(), k
         else:
             assert (out[k][bad] == -1).all(), k
+
+
+def test_rng_begin_advances_and_snapshots():
+    """spnerf_rng_begin (PhiloxRandom.begin_render's one launch): the device step advances by one
+    per render, the snapshot holds {seed, step} and keeps it while a later render advances the
+    state; the host mirror follows; inside a captured graph every replay advances the step."""
+    from spnerf_amd import PhiloxRandom
+    r = PhiloxRandom(seed=11)
+    r.begin_render(DEV)
+    s0 = r._snap
+    assert r._state.tolist() == [11, 0] and s0.tolist() == [11, 0]
+    r.begin_render(DEV)
+    assert r._state.tolist() == [11, 1] and r._snap.tolist() == [11, 1] and s0.tolist() == [11, 0]
+    assert r.sync_host_step() == 1
+    r.reset_step(41)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        r.begin_render(DEV)       # warm-up (eager): step 42
+    torch.cuda.current_stream().wait_stream(side)
+    with torch.cuda.graph(g):
+        r.begin_render(DEV)       # captured: each replay advances the device step
+        snap = r._snap
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert r._state.tolist() == [11, 45] and snap.tolist() == [11, 45]
