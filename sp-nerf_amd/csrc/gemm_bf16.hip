@@ -465,9 +465,10 @@ constexpr int ND_K = 32, ND_STAGES = 4, ND_STG = 512 * 64;
 #define SPN_NT_ADDR 1  // DMA sources as a uniform base + 32-bit lane offset (0: 64-bit per-lane pointers, A/B builds)
 #endif
 #ifndef SPN_NT16_NT
-// the DMA NT GEMM's C / Dout stores non-temporal (glc slc; A/B builds): C4 26.20 / 26.19 -> 26.13 /
-// 26.11 ms, C4@512 level (tools/gpu_r3x.sh) — within the box's spread, so off
-#define SPN_NT16_NT 0
+// the DMA NT GEMM's C / Dout stores non-temporal (glc slc; whole 128-B row pieces): round 3, C4 26.20 /
+// 26.19 -> 26.13 / 26.11 ms (off then: within the spread); round 6, C4 23.66 / 23.69 -> 23.58 /
+// 23.63 ms, C4@512 3.390 / 3.394 -> 3.374 / 3.390 (tools/ab_libs.sh, one call): on
+#define SPN_NT16_NT 1
 #endif
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 #ifdef ND_STAMPS
@@ -1391,6 +1392,12 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16w(TN16Args g) {
 // only when every split holds whole 32-point steps (P % 32 == 0).  Bias sums are read back from
 // the landed stage (k0 == 0 blocks only).
 constexpr int TD_STEP = 32, TD_STAGES = 4, TD_STG = 4 * TD_STEP * 256;  // bytes per stage
+#ifndef SPN_TN_NT
+// the weight-gradient GEMM's DMA loads non-temporal (glc slc; A/B builds): slower — TN 5.88 -> 6.07 ms
+// per C4 step, PMC reads 4.59 -> 6.12 GB per launch (the two tiles that share operand rows then
+// fetch them twice)
+#define SPN_TN_NT 0
+#endif
 #ifndef SPN_TN_ADDR
 // 1: the IP 3 main loop reads its fragments at 12 lane offsets computed once per block, one
 // v_add per offset per stage and the k-step as the ds_read immediate (the same reads, MFMAs and
@@ -1503,7 +1510,7 @@ __global__ __launch_bounds__(512) void k_gemm_tn_bf16d(TN16Group G) {
 #else
         const char* a = reinterpret_cast<const char*>(src[i] + p0 * ld[i]) + (sg2 ? dl[i] : 0);
 #endif
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)a, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)a, (lds_ptr_t)(smem + stg * TD_STG + q * 1024), 16, 0, SPN_TN_NT ? 3 : 0);
     };
     auto issue = [&](int st, int stg) {
 #pragma unroll
