@@ -74,6 +74,7 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
 // the trunk's tile loop spilled (64-bit values reloaded from scratch behind the copy-out stores)
 // and the main pass took 5.78 ms against 2.78 + 1.72 ms for the two launches.
 static_assert(SB_N * 4 <= RQ_BYTES, "the training heads' biases in the RQ area");
+template <bool RQ1>
 __global__ __launch_bounds__(512) void k_heads_train_bf16(HeadsFusedArgs g, PackedOffs k, int ntiles) {
     __shared__ __attribute__((aligned(16))) char smem[LDS];
     const int tid = threadIdx.x;
@@ -110,10 +111,11 @@ __global__ __launch_bounds__(512) void k_heads_train_bf16(HeadsFusedArgs g, Pack
         }
         const int r = opaque(tid);
         if (r < TM) ost[r * OST_LD + 3] = softplusf_(g.hsave[std::min<int64_t>(p0 + r, g.P - 1) * 8]);
+        if constexpr (RQ1) stage_rows_ost(g, k, ost, p0, tid);
         __syncthreads();
         const int next = tile + (int)gridDim.x;
         // (past the last tile: this tile's rows again, never stored — no branch around the loads)
-        heads_tile_train(g, k, smem, ost, part, sbias, p0, [&] { load_hl((int64_t)std::min(next, ntiles - 1) * TM); });
+        heads_tile_train<RQ1>(g, k, smem, ost, part, sbias, p0, [&] { load_hl((int64_t)std::min(next, ntiles - 1) * TM); });
         __syncthreads();  // the next tile restages the image
     }
 }
@@ -137,7 +139,11 @@ int32_t heads_train_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream
     ad.dbg = 0;
 #endif
     ProfScope prof("heads_train", s, flop, bytes);
-    hipLaunchKernelGGL(k_heads_train_bf16, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, k, ntiles);
+    // every 128-point tile within one ray (S a multiple of 128): the Q epilogue's per-ray rows from LDS
+    if (SPN_HEADS_RQ_OST && a.S % TM == 0)
+        hipLaunchKernelGGL(k_heads_train_bf16<true>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, k, ntiles);
+    else
+        hipLaunchKernelGGL(k_heads_train_bf16<false>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, k, ntiles);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -406,6 +406,12 @@ __device__ __forceinline__ void cols_out(const char* smem, __amdgpu_buffer_rsrc_
     asm volatile("" ::: "memory");
 }
 
+#ifndef SPN_HEADS_RQ_OST
+#define SPN_HEADS_RQ_OST 1  // training heads: when every tile lies within one ray, its Q rows from LDS (ost)
+#endif
+#ifndef SPN_HEADS_WM_OST
+#define SPN_HEADS_WM_OST 1  // ... and the semantic logits' weights W_m2 from ost too
+#endif
 #ifndef SPN_HEADS_ZC
 #define SPN_HEADS_ZC 0  // 1: layer_mm_d k-step 0 with the MFMA C = 0 (no accumulator zeroing) — spills 172 B, heads 2.56 -> 3.0 ms per C4 step
 #endif
@@ -528,7 +534,25 @@ constexpr int SB_G = 0, SB_Q = HW + HH, SB_S2 = SB_Q + 2 * HH, SB_S3 = SB_S2 + H
 // (g.dbg, profiling ablations of the -DSPN_ABLATIONS build, outputs invalid: 1 = no image
 // copy-outs, 2 = no register stores (D, semantic hidden), 8 = no sin / cos in the wide layers'
 // epilogues)
-template <typename GA, typename KA, typename Prefetch>
+// The training heads' per-tile staging in ost (the caller's, before the barrier that precedes
+// heads_tile_train<true>; every tile within one ray): the ray's Q rows rbQ[ray][0..512) in columns
+// 8..15 of rows 0..63 and (SPN_HEADS_WM_OST) the semantic logits' weights W_m2 [C][HH], C <= 3:
+// entries q < 512 in columns 4..7 (rows q / 4), the rest in columns 8..15 of rows 64 + (q - 512) / 8
+// — every f32x4 the epilogues read is one aligned piece of a row.  Columns 0..2 and 4..15 are free
+// until the semantic logits and the outputs are written, after the Q epilogue.
+template <typename GA, typename KA>
+__device__ __forceinline__ void stage_rows_ost(GA& g, KA& k, float* ost, int64_t p0, int tid_) {
+    const int f = opaque(tid_);  // 512 threads: the 2·HH floats of the row
+    ost[(f >> 3) * OST_LD + 8 + (f & 7)] = g.rbQ[(int64_t)((int)p0 / g.S) * (2 * HH) + f];
+    if constexpr (SPN_HEADS_WM_OST) {
+        if (g.mode == 0)  // block-uniform (the solar pass has no semantic head)
+            for (int q = f; q < g.C * HH; q += 512)
+                ost[q < 512 ? (q >> 2) * OST_LD + 4 + (q & 3) : (64 + ((q - 512) >> 3)) * OST_LD + 8 + ((q - 512) & 7)] =
+                    g.packed[k.Wm2 + q];
+    }
+}
+
+template <bool RQ1, typename GA, typename KA, typename Prefetch>
 __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float* ost, float* part, const float* sbias,
                                                  int64_t p0, Prefetch&& prefetch) {
     constexpr int D1 = 8;  // ring depth of the 256-wide layers (sem hidden, sun_v 2 / 3)
@@ -565,6 +589,9 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     };
     auto nodrain = [](int) {};
     const int el = opaque(lane), er32 = el & 31, eh = el >> 5;
+    // RQ1 (every tile within one ray: S a multiple of TM, the launch's choice): the tile's ray's Q
+    // rows (and W_m2) were staged in ost by the caller before its barrier (stage_rows_ost)
+    static_assert(!RQ1 || (OST_LD >= 16 && 2 * HH == 512), "the Q row staging: 512 floats in ost columns 8..15");
 
     u32x4 ring2f[D2][2];  // feat's weights
     // semantic hidden = sin(W_m1 H_L + b) → G[:, W..W+H) and DG; its logits' partials → part
@@ -591,7 +618,14 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
                 const f32x4 yb = raw_f32(yq[gq]);  // the stored (bf16) values feed the logits
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const f32x4 wm = c < C ? ld4(Pk + k.Wm2 + c * HH + f0) : f32x4{0.f, 0.f, 0.f, 0.f};
+                    f32x4 wm = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (c < C) {
+                        if constexpr (RQ1 && SPN_HEADS_WM_OST)  // staged in ost (see the top of the tile)
+                            wm = *reinterpret_cast<const f32x4*>(
+                                ost + (c < 2 ? (c * 64 + 8 * w + 2 * gq + eh) * OST_LD + 4 : (64 + 4 * w + gq) * OST_LD + 8 + 4 * eh));
+                        else
+                            wm = ld4(Pk + k.Wm2 + c * HH + f0);
+                    }
                     sacc[c] += (yb[0] * wm[0] + yb[1] * wm[1]) + (yb[2] * wm[2] + yb[3] * wm[3]);
                 }
             }
@@ -649,34 +683,42 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
         const int rlast = (int)(g.P - 1 - p0);  // P < 2^31 / 512 (host check)
 #if SPN_HEADS_DCOLS
         // per point tile j: cos into the wave's own image columns, those rows out to DQ, then sin
-        // over them (the sines wait in registers)
+        // over them (the sines wait in registers).  KOST: the tile's one ray's row of rbQ staged in
+        // ost (no global load per feature group, whose wait would also wait for the D stores)
+        auto qepi = [&](auto kost) {
+            constexpr bool KOST = decltype(kost)::value;
+            const float* rqb = ost + 8 * w * OST_LD + 8 + 4 * eh;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            u32x2 yq[2][4];
-            const int64_t ray = ((int)p0 + std::min(32 * j + er32, rlast)) / g.S;
+            for (int j = 0; j < NJ; ++j) {
+                u32x2 yq[2][4];
+                const int64_t ray = ((int)p0 + std::min(32 * j + er32, rlast)) / g.S;
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+                for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
-                    const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_Q + f0);
-                    const f32x4 rv = ld4(g.rbQ + ray * (2 * HH) + f0);
-                    float y[4], cs[4];
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                        const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_Q + f0);
+                        // (f0 >> 3 = 8w + 4a + gq, f0 & 7 = 4·eh: one lane base, the group as an immediate)
+                        const f32x4 rv = KOST ? *reinterpret_cast<const f32x4*>(rqb + (4 * a + gq) * OST_LD)
+                                              : ld4(g.rbQ + ray * (2 * HH) + f0);
+                        float y[4], cs[4];
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) sincos((acc[a][j][4 * gq + e] + bv[e]) + rv[e], &y[e], &cs[e]);
-                    put4(32 * j + er32, f0, cs);
-                    yq[a][gq] = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
-                }
-            if (dq) cols_out<2>(smem, rsD, g.ldQ, 64 * w, j, lane);
+                        for (int e = 0; e < 4; ++e) sincos((acc[a][j][4 * gq + e] + bv[e]) + rv[e], &y[e], &cs[e]);
+                        put4(32 * j + er32, f0, cs);
+                        yq[a][gq] = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                    }
+                if (dq) cols_out<2>(smem, rsD, g.ldQ, 64 * w, j, lane);
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+                for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
-                    *reinterpret_cast<u32x2*>(smem + img_off(32 * j + er32, f0 >> 3) + 8 * ((f0 >> 2) & 1)) = yq[a][gq];
-                }
-            __builtin_amdgcn_sched_barrier(0);
-        }
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const int f0 = 64 * w + 32 * a + 8 * gq + 4 * eh;
+                        *reinterpret_cast<u32x2*>(smem + img_off(32 * j + er32, f0 >> 3) + 8 * ((f0 >> 2) & 1)) = yq[a][gq];
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        qepi(std::integral_constant<bool, RQ1>{});
 #else
 #pragma unroll
         for (int a = 0; a < 2; ++a)
