@@ -956,6 +956,9 @@ def parse_args(argv=None):
     ap.add_argument("--global-batch", type=int, default=0, help="override the config's global batch (rays per step)")
     ap.add_argument("--no-defer-wgrad", action="store_true",
                     help="one trunk weight-gradient GEMM per pass instead of one over the main + solar passes")
+    ap.add_argument("--no-reuse-pass1", action="store_true",
+                    help="evaluate the guided pass's stratified points twice, as the reference does (pass 1, then "
+                         "again in the sorted union) instead of once (rendering.REUSE_PASS1)")
     ap.add_argument("--flat-allreduce", action="store_true",
                     help="one all-reduce of the flat gradient after the backward instead of overlapped buckets")
     ap.add_argument("--no-graph-allreduce", action="store_true",
@@ -1056,6 +1059,7 @@ class TrainStep:
                                        sem=c["sem"], precision=c["precision"]).to(dev)
         self.model.use_flat_grads()   # backward adds into one flat buffer: the .grads are its views (one all-reduce)
         self.model.defer_trunk_wgrad = not a.no_defer_wgrad
+        spnerf_amd.rendering.REUSE_PASS1 = not a.no_reuse_pass1
         self.params = list(self.model.parameters())
         if a.torch_adam:
             self.opt = torch.optim.Adam(self.params, lr=5e-4, fused=True)

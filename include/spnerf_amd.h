@@ -94,6 +94,18 @@ int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed,
                            int64_t n_rays, int32_t n_samples, const float* z,
                            const int64_t* labels, const float* t_emb, int32_t flags,
                            void* workspace, float* out, void* stream);
+/* spnerf_mlp_forward over rays [ray_begin, ray_begin + n_rays) of a workspace laid out for
+ * n_rays_total rays (spnerf_mlp_workspace_bytes(cfg, n_rays_total, n_samples, flags)): rays, z,
+ * labels, t_emb and out are the window's own rows.  Windows filled at different times make ONE
+ * saving forward whose backward runs over all n_rays_total rays — render_rays' guided main pass
+ * (rendering.py:159-170) evaluates its stratified half in pass 1 (window 0, whose sigma feeds
+ * the guided windows) and only the guided half afterwards (window 1, the rays repeated), instead
+ * of evaluating the stratified points twice.  ray_begin * n_samples must be even. */
+int32_t spnerf_mlp_forward_window(const spnerf_model_cfg* cfg, const void* packed,
+                                  const float* rays, int32_t ray_stride, int32_t dir_offset,
+                                  int64_t n_rays_total, int64_t ray_begin, int64_t n_rays, int32_t n_samples,
+                                  const float* z, const int64_t* labels, const float* t_emb, int32_t flags,
+                                  void* workspace, float* out, void* stream);
 /* Gradients of sum(d_out * out) w.r.t. every parameter, written (overwritten, or added with
  * SPNERF_MLP_ACCUMULATE in `flags`) into `grad_flat` (canonical order, torch shapes,
  * contiguous) and w.r.t. t_emb (n_rays, t_dim, overwritten).  The workspace of a SAVE forward
@@ -187,6 +199,15 @@ int32_t spnerf_sample_3sigma(int64_t n_rays, int32_t n, const float* low, const 
                              const float* clamp_nf, const float* u, float* out, void* stream);
 /* row-wise ascending sort of (n_rays, n) floats, n <= 256 (torch.sort(-1) values) */
 int32_t spnerf_sort_rows(int64_t n_rays, int32_t n, const float* in, float* out, void* stream);
+/* rendering.py:165-168: the main pass's rows in the sorted depth order, gathered from two segments
+ * of MLP rows — s1 per ray (pass 1's stratified samples, rows [0, n_rays*s1)) then s2 per ray (the
+ * guided samples, rows [n_rays*s1, n_rays*(s1+s2))) — by the ranks of z_unsort = [z | sorted z_2]
+ * (n_rays, s1+s2), the reference's z_vals_unsort.  out_sorted (n_rays*(s1+s2), n_out).  The
+ * backward scatters the sorted rows' gradients d_sorted back into the segments' rows d_seg. */
+int32_t spnerf_merge_samples(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* out_seg,
+                             int32_t n_out, float* out_sorted, void* stream);
+int32_t spnerf_merge_samples_backward(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort,
+                                      const float* d_sorted, int32_t n_out, float* d_seg, void* stream);
 
 /* ---- RPC camera rays: get_rays + normalize_rays + get_sun_dirs (datasets/satellite_scene.py:21-68,
  *      :415-425, :449-473; modules/utils.py:59-100).  rpc = 90 host doubles: row/col/lat/lon/alt

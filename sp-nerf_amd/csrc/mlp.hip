@@ -1702,8 +1702,11 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
 
 static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays, int rs, int dir_off,
                            int64_t n_rays, int S, const float* z, const int64_t* labels, const float* temb, int flags,
-                           float* ws, float* out, hipStream_t s) {
-    Ctx c{d, packed_layout(d), ws_layout(d, n_rays, S, flags), packed, ws, S};
+                           float* ws, float* out, hipStream_t s, int64_t n_total = -1, int64_t r0 = 0) {
+    // n_total >= 0: rays [r0, r0 + n_rays) of a workspace laid out for n_total rays (forward_window)
+    Ctx c{d, packed_layout(d),
+          n_total < 0 ? ws_layout(d, n_rays, S, flags) : ws_window(d, ws_layout(d, n_total, S, flags), r0, n_rays, S),
+          packed, ws, S};
     const bool save = flags & SPNERF_MLP_SAVE;
     const int mode = (flags & SPNERF_MLP_SIGMA_ONLY) ? 1 : ((flags & SPNERF_MLP_SUN_ONLY) ? 2 : 0);
     const int64_t P = n_rays * S;
@@ -2604,6 +2607,24 @@ extern "C" int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* p
     SPN_ARG(dir_offset == 3 || dir_offset == 8, "mlp_forward: dir_offset must be 3 (view) or 8 (sun)");
     return mlp_forward(d, (const float*)packed, rays, ray_stride, dir_offset, n_rays, n_samples, z, labels, t_emb, flags,
                        (float*)workspace, out, (hipStream_t)stream);
+}
+
+extern "C" int32_t spnerf_mlp_forward_window(const spnerf_model_cfg* cfg, const void* packed, const float* rays,
+                                             int32_t ray_stride, int32_t dir_offset, int64_t n_rays_total,
+                                             int64_t ray_begin, int64_t n_rays, int32_t n_samples, const float* z,
+                                             const int64_t* labels, const float* t_emb, int32_t flags, void* workspace,
+                                             float* out, void* stream) {
+    Dims d;
+    SPN_TRY(make_dims(cfg, &d));
+    SPN_ARG(packed && rays && z && workspace && out, "mlp_forward_window: NULL pointer");
+    SPN_ARG(n_rays >= 0 && n_samples > 0 && ray_stride >= 11, "mlp_forward_window: bad sizes");
+    SPN_ARG(ray_begin >= 0 && n_rays_total >= ray_begin + n_rays, "mlp_forward_window: rays [%lld, %lld) outside %lld",
+            (long long)ray_begin, (long long)(ray_begin + n_rays), (long long)n_rays_total);
+    SPN_ARG((ray_begin * n_samples) % 2 == 0, "mlp_forward_window: the window must start at an even point");
+    SPN_ARG(n_rays_total * n_samples < (1ll << 31) / std::max(d.NQ, d.NG), "mlp_forward_window: too many points");
+    SPN_ARG(dir_offset == 3 || dir_offset == 8, "mlp_forward_window: dir_offset must be 3 (view) or 8 (sun)");
+    return mlp_forward(d, (const float*)packed, rays, ray_stride, dir_offset, n_rays, n_samples, z, labels, t_emb, flags,
+                       (float*)workspace, out, (hipStream_t)stream, n_rays_total, ray_begin);
 }
 
 extern "C" int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed, const float* rays,

@@ -278,4 +278,38 @@ WS ws_layout(const Dims& d, int64_t n_rays, int32_t S, int32_t flags) {
     return w;
 }
 
+WS ws_window(const Dims& d, const WS& full, int64_t r0, int64_t n, int32_t S) {
+    WS w = full;
+    const int64_t p0 = r0 * S;
+    w.P = n * S;
+    w.B = n;
+    // point-major rows: fp32, or bf16 at half the floats (every width here is even)
+    auto pts = [&](int64_t& off, int64_t width, bool act) {
+        if (off >= 0) off += act && d.bf ? p0 * width / 2 : p0 * width;
+    };
+    auto rows = [&](int64_t& off, int64_t width) {
+        if (off >= 0) off += r0 * width;
+    };
+    pts(w.X0, d.K0p, false);
+    pts(w.X0b, d.K0p, true);
+    pts(w.X0s, 4 * d.K0p, true);
+    for (auto& o : w.Hb) pts(o, d.W, true);
+    for (auto& o : w.Db) pts(o, d.W, true);
+    pts(w.G, d.NG, true);
+    pts(w.DG, d.NG, true);
+    pts(w.Q, d.NQ, true);
+    pts(w.DQ, d.NQ, true);
+    pts(w.S2, d.H, true);
+    pts(w.DS2, d.H, true);
+    pts(w.S3, d.H, true);
+    pts(w.DS3, d.H, true);
+    pts(w.hsave, 8, false);
+    rows(w.rb0, d.W);
+    rows(w.rb4, d.W);
+    rows(w.rbQ, d.NQ);
+    rows(w.skyh, d.H);
+    rows(w.sky, 4);
+    return w;
+}
+
 }  // namespace spn

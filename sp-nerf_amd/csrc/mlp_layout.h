@@ -93,5 +93,9 @@ struct WS {
     int64_t total;
 };
 WS ws_layout(const Dims& d, int64_t n_rays, int32_t n_samples, int32_t flags);
+// The forward's buffers of `full` (a layout for n_total rays) restricted to rays [r0, r0 + n): the
+// point-major rows from point r0·S on, the per-ray rows from ray r0 on (spnerf_mlp_forward_window;
+// the backward buffers are left as laid out — the backward runs over all n_total rays)
+WS ws_window(const Dims& d, const WS& full, int64_t r0, int64_t n, int32_t S);
 
 }  // namespace spn

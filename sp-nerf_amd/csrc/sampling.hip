@@ -6,6 +6,8 @@
 //                    one wavefront per ray, with NO host synchronisation (the reference copies
 //                    valid_depth to the host every step, :101-104)
 //  * k_sample_pdf / k_sample_3sigma / k_sort_rows — the standalone drop-ins.
+//  * k_merge_rows  — the main pass's MLP rows gathered into the sorted depth order from pass 1's
+//                    rows and the guided samples' rows (each point evaluated once), and back.
 // Inverse-CDF sampling keeps the CDF in LDS and binary-searches it per sample; cumsum is
 // accumulated in double as torch's CPU cumsum does.
 #include "common.h"
@@ -250,9 +252,72 @@ __global__ __launch_bounds__(256) void k_sort_rows(int64_t B, int n, const float
         for (int e = lane; e < n; e += 64) out[ray * n + e] = buf[wv][e];
 }
 
+// The main pass's samples are the union of the stratified depths and the guided ones, sorted
+// (rendering.py:165-168).  Its points at the stratified depths are pass 1's points (:147, :168:
+// the same o + d·z), so their MLP rows are computed once: the rows of the two segments (pass 1's
+// s1 per ray, then the guided s2 per ray, spnerf_mlp_forward_window) are gathered into the sorted
+// order here, and the backward scatters the sorted rows' gradients back to the segments.  The
+// sorted position of element e of z_unsort = [z | sorted z_2] (the reference's z_vals_unsort) is
+// its rank #{f : z[f] < z[e]} + #{f < e : z[f] == z[e]} — a permutation into ascending order, so
+// the rows land where torch.sort puts their depths (equal depths are the same point: equal rows).
+__global__ __launch_bounds__(256) void k_merge_rows(int64_t B, int s1, int s2, const float* __restrict__ zu,
+                                                    const float* __restrict__ in, int n_out, float* __restrict__ out,
+                                                    int bwd) {
+    __shared__ float zs[4][256];
+    __shared__ int src[4][256];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t ray = (int64_t)blockIdx.x * 4 + wv;
+    const bool active = ray < B;
+    const int n = s1 + s2;
+    for (int e = lane; e < n; e += 64) zs[wv][e] = active ? zu[ray * n + e] : 0.f;
+    __syncthreads();
+    for (int e = lane; e < n; e += 64) {
+        const float v = zs[wv][e];
+        int rank = 0;
+        for (int f = 0; f < n; ++f) {
+            const float w = zs[wv][f];
+            rank += (w < v) || (w == v && f < e);
+        }
+        src[wv][rank] = e;
+    }
+    __syncthreads();
+    if (!active) return;  // no barriers below
+    const int64_t nn = (int64_t)n * n_out;
+    for (int64_t i = lane; i < nn; i += 64) {
+        const int t = (int)(i / n_out), col = (int)(i - (int64_t)t * n_out);
+        const int e = src[wv][t];
+        const int64_t row = e < s1 ? ray * s1 + e : B * s1 + ray * s2 + (e - s1);
+        if (!bwd) out[(ray * n + t) * n_out + col] = in[row * n_out + col];
+        else out[row * n_out + col] = in[(ray * n + t) * n_out + col];
+    }
+}
+
 }  // namespace spn
 
 using namespace spn;
+
+static int32_t merge_rows(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* in, int32_t n_out,
+                          float* out, int bwd, hipStream_t s) {
+    SPN_ARG(z_unsort && in && out, "merge_samples: NULL pointer");
+    SPN_ARG(s1 >= 1 && s2 >= 1 && s1 + s2 <= 256 && n_out >= 1 && n_rays >= 0, "merge_samples: bad sizes");
+    SPN_ARG(n_rays * (s1 + s2) * (int64_t)n_out < (1ll << 40), "merge_samples: too large");
+    if (n_rays == 0) return SPNERF_OK;
+    ProfScope prof("merge_samples", s, 0.0, (double)n_rays * (s1 + s2) * (8.0 * n_out + 4.0));
+    hipLaunchKernelGGL(k_merge_rows, dim3((unsigned)((n_rays + 3) / 4)), dim3(256), 0, s, n_rays, s1, s2, z_unsort, in,
+                       n_out, out, bwd);
+    SPN_HIP(hipGetLastError());
+    return SPNERF_OK;
+}
+
+extern "C" int32_t spnerf_merge_samples(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* out_seg,
+                                        int32_t n_out, float* out_sorted, void* stream) {
+    return merge_rows(n_rays, s1, s2, z_unsort, out_seg, n_out, out_sorted, 0, (hipStream_t)stream);
+}
+
+extern "C" int32_t spnerf_merge_samples_backward(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort,
+                                                 const float* d_sorted, int32_t n_out, float* d_seg, void* stream) {
+    return merge_rows(n_rays, s1, s2, z_unsort, d_sorted, n_out, d_seg, 1, (hipStream_t)stream);
+}
 
 static spnerf_rng rng_or_null(const spnerf_rng* r) { return r ? *r : spnerf_rng{nullptr, 0, 0, 0}; }
 

@@ -8,9 +8,12 @@ reference (rendering.py)         here                                      kerne
 ==============================  ========================================  =====================
 stratified z  :131-144           ``stratified``                            k_stratified
 inference pass 1 :157            σ-only MLP + weights-only composite       mlp + composite
+                                 (training: the saving MLP's window 0)     mlp_forward_window
 GenerateGuidedSamples :92-116    ``spnerf_sample_guided`` (+ sort, merge)  k_guided
   + sort / merge :165-167
 inference pass 2 :169            full MLP + composite                      mlp + composite
+                                 (training: the guided points only, the    mlp_forward_window,
+                                 rows merged in sorted order)              k_merge_rows
 fine pass :186-216               sample_pdf + sort + fine MLP/composite    k_sample_pdf, k_sort_rows
 solar correction :171-177        σ+sun MLP + weights-only composite        mlp + composite
 sample_pdf :14-55                ``sample_pdf``                            k_sample_pdf
@@ -23,7 +26,12 @@ import torch
 
 from . import _lib
 from .rng import begin_render, current_random_source, device_key
-from .spnerf import inference_rays, pack_for_render
+from .spnerf import _result, composite, guided_main_pass, inference_rays, mlp_saves, pack_for_render
+
+# Training renders with guided sampling evaluate each main-pass point once (spnerf._GuidedMain):
+# False = the reference's two evaluations of the stratified points (pass 1 σ-only, then the
+# sorted union) — the A/B arm and the parity cross-check of tests/test_gpu_reuse.py
+REUSE_PASS1 = True
 
 
 def stratified(rays: torch.Tensor, n_samples: int, u: torch.Tensor = None, rng=None) -> torch.Tensor:
@@ -175,7 +183,21 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
         rays_t = models["t"](ts) if ts is not None else None                       # rendering.py:156
     sem = semantics if model.sem else None
     pk = pack_for_render(model)   # every pass of this render reads the same packed weights
-    if args.guidedsample:
+    if args.guidedsample and REUSE_PASS1 and mlp_saves(model, rays_t if model.beta else None):
+        # training: pass 1's rows ARE the main pass's rows at the stratified depths — one saving
+        # forward in two windows, composited in the sorted order (spnerf._GuidedMain)
+        cnf = None if clamp_near_far is None else clamp_near_far.reshape(2).to(rays.device, torch.float32).contiguous()
+
+        def guide(out1, z1):
+            rgb1, depth1, w1, T1, sem1 = composite(model, out1, z1, args.noise_std, weights_only=True)
+            return _guided({"depth": depth1, "weights": w1}, z1, N_samples, rays, mode, valid_depth, target_depths,
+                           target_std, cnf)
+
+        out, z_vals, z_unsort = guided_main_pass(model, rays, z_vals, sem if model.sem else None,
+                                                 rays_t if model.beta else None, guide, pk)
+        rgb, depth, w, T, sem_l = composite(model, out, z_vals, args.noise_std)
+        result = _result(model, out, z_vals, rgb, depth, w, T, sem_l, z_unsort)
+    elif args.guidedsample:
         with torch.no_grad():   # pass 1 feeds only the detached guided depths (rendering.py:164)
             res1 = inference_rays(model, args, rays, z_vals, 3, sem, rays_t, mode="sigma", pack=pk)
         cnf = None if clamp_near_far is None else clamp_near_far.reshape(2).to(rays.device, torch.float32).contiguous()

@@ -391,47 +391,145 @@ class _MLP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_out):
         rays, labels, temb = ctx.saved_tensors
-        model = ctx.model
-        params = model.canonical_parameters()
-        B, S = ctx.shape
-        gt = torch.empty_like(temb) if (temb is not None and ctx.needs_input_grad[6]) else None
         if ctx.ws is None:
             raise RuntimeError("SPNeRF MLP backward called twice on the same forward (its activations are freed)")
-        d_out = d_out.contiguous()
-        flags = ctx.flags
-        grad = model.flat_grad_target(params)
-        direct = grad is not None
-        pack = ctx.pack
-        # A render with several saving passes (main + solar correction) over one bf16 trunk: each
-        # backward leaves the trunk's weight gradients, and one GEMM per layer over all the passes'
-        # points runs when the backward pass ends (half the launches and split reductions)
-        defer = (direct and pack.nsave > 1 and model.precision == "bf16" and model.defer_trunk_wgrad
-                 and _lib.lib().spnerf_mlp_trunk_wgrad(ctypes.byref(model.cfg()), 0, None, None, None, None, None,
-                                                       None) == 1)
-        if direct:   # add straight into the .grad views (the library's fixed-order reductions)
-            flags |= SPNERF_MLP_ACCUMULATE
-        else:
-            grad = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=rays.device)
-        if defer:
-            flags |= SPNERF_MLP_DEFER_TRUNK_WGRAD
-        _lib.check(_lib.lib().spnerf_mlp_backward(ctypes.byref(model.cfg()), _lib.ptr(ctx.packed), _lib.ptr(rays),
-                                                  rays.stride(0), B, S, _lib.ptr(labels), _lib.ptr(temb), flags,
-                                                  _lib.ptr(ctx.ws), _lib.ptr(d_out), _lib.ptr(grad),
-                                                  _lib.ptr(gt), _lib.stream_of(rays)), "mlp_backward")
-        if defer:
-            if not pack.deferred:
-                torch.autograd.Variable._execution_engine.queue_callback(pack.flush_trunk_wgrad)
-            pack.deferred.append((ctx.ws, B, S, ctx.flags, grad, torch.cuda.current_stream(rays.device)))
-        ctx.pack.done()
+        B, S = ctx.shape
+        gt, grads = _mlp_backward(ctx.model, ctx.pack, ctx.packed, ctx.ws, ctx.flags, rays, labels, temb, B, S,
+                                  d_out.contiguous(), temb is not None and ctx.needs_input_grad[6])
         ctx.pack = ctx.packed = None
         ctx.ws = None
-        if direct:
-            return (None, None, None, None, None, None, gt, None, *([None] * len(params)))
-        grads, off = [], 0
-        for p in params:
-            grads.append(grad[off:off + p.numel()].view_as(p))
-            off += p.numel()
         return (None, None, None, None, None, None, gt, None, *grads)
+
+
+def _mlp_backward(model, pack, packed, ws, fwd_flags, rays, labels, temb, B, S, d_out, temb_grad):
+    """spnerf_mlp_backward of one saving forward's workspace: the parameter gradients straight into
+    the model's flat gradient (``use_flat_grads``) or returned per parameter, and the t-embedding's.
+    Returns (grad_t_emb or None, per-parameter gradients or Nones)."""
+    params = model.canonical_parameters()
+    gt = torch.empty_like(temb) if temb_grad else None
+    flags = fwd_flags
+    grad = model.flat_grad_target(params)
+    direct = grad is not None
+    # A render with several saving passes (main + solar correction) over one bf16 trunk: each
+    # backward leaves the trunk's weight gradients, and one GEMM per layer over all the passes'
+    # points runs when the backward pass ends (half the launches and split reductions)
+    defer = (direct and pack.nsave > 1 and model.precision == "bf16" and model.defer_trunk_wgrad
+             and _lib.lib().spnerf_mlp_trunk_wgrad(ctypes.byref(model.cfg()), 0, None, None, None, None, None,
+                                                   None) == 1)
+    if direct:   # add straight into the .grad views (the library's fixed-order reductions)
+        flags |= SPNERF_MLP_ACCUMULATE
+    else:
+        grad = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=rays.device)
+    if defer:
+        flags |= SPNERF_MLP_DEFER_TRUNK_WGRAD
+    _lib.check(_lib.lib().spnerf_mlp_backward(ctypes.byref(model.cfg()), _lib.ptr(packed), _lib.ptr(rays),
+                                              rays.stride(0), B, S, _lib.ptr(labels), _lib.ptr(temb), flags,
+                                              _lib.ptr(ws), _lib.ptr(d_out), _lib.ptr(grad),
+                                              _lib.ptr(gt), _lib.stream_of(rays)), "mlp_backward")
+    if defer:
+        if not pack.deferred:
+            torch.autograd.Variable._execution_engine.queue_callback(pack.flush_trunk_wgrad)
+        pack.deferred.append((ws, B, S, fwd_flags, grad, torch.cuda.current_stream(rays.device)))
+    pack.done()
+    if direct:
+        return gt, [None] * len(params)
+    grads, off = [], 0
+    for p in params:
+        grads.append(grad[off:off + p.numel()].view_as(p))
+        off += p.numel()
+    return gt, grads
+
+
+class _GuidedMain(torch.autograd.Function):
+    """render_rays' guided main pass (rendering.py:157-170) with every point evaluated ONCE.
+
+    The reference runs the MLP over the 64 stratified depths (pass 1: its depth and weights place
+    the guided samples) and then again over the sorted union of those depths and the 64 guided
+    ones; the union's stratified points are pass 1's points (the same o + d·z, :147 / :168), so
+    their MLP rows are the same.  Here pass 1 is the first window of ONE saving forward
+    (``spnerf_mlp_forward_window``: rays [0, B) of a (2B rays, S) workspace), ``guide`` composites
+    its σ (weights only, no gradient, :157 feeds only the detached guided depths) and draws the
+    guided depths, the guided points are the second window (rays [B, 2B)), and
+    ``spnerf_merge_samples`` gathers both windows' rows into the sorted order the composite reads.
+    The backward scatters the sorted rows' gradients back (``spnerf_merge_samples_backward``) and
+    runs ONE MLP backward over the 2B "rays" (the rays / labels / t-embeddings repeated).  Draws
+    happen in the reference's order: pass 1's σ noise, the guided windows, then the caller's."""
+
+    @staticmethod
+    def forward(ctx, model, pack, rays, z1, labels, temb, guide, *params):
+        cfg = model.cfg()
+        B, S = z1.shape
+        dev = rays.device
+        NO = model.number_of_outputs
+        flags = SPNERF_MLP_SAVE
+        L = _lib.lib()
+        wsb = L.spnerf_mlp_workspace_bytes(ctypes.byref(cfg), 2 * B, S, flags)
+        if wsb < 0:
+            _lib.check(-1, "workspace_bytes")
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
+        seg = torch.empty(2 * B * S, NO, dtype=torch.float32, device=dev)
+        packed = pack.buf
+
+        def window(r0, z):
+            _lib.check(L.spnerf_mlp_forward_window(ctypes.byref(cfg), _lib.ptr(packed), _lib.ptr(rays), rays.stride(0), 3,
+                                                   2 * B, r0, B, S, _lib.ptr(z), _lib.ptr(labels), _lib.ptr(temb), flags,
+                                                   _lib.ptr(ws), _lib.ptr(seg[r0 * S:(r0 + B) * S]),
+                                                   _lib.stream_of(rays)), "mlp_forward_window")
+
+        window(0, z1)
+        z_sorted, z_unsort = guide(seg[:B * S], z1)
+        z2 = z_unsort[:, S:].contiguous()
+        window(B, z2)
+        out = torch.empty(B * 2 * S, NO, dtype=torch.float32, device=dev)
+        _lib.check(L.spnerf_merge_samples(B, S, S, _lib.ptr(z_unsort), _lib.ptr(seg), NO, _lib.ptr(out),
+                                          _lib.stream_of(rays)), "merge_samples")
+        pack.pending += 1
+        pack.nsave += 1
+        ctx.model, ctx.ws, ctx.pack, ctx.packed, ctx.B, ctx.S = model, ws, pack, packed, B, S
+        ctx.rays2 = torch.cat([rays, rays])
+        ctx.labels2 = None if labels is None else torch.cat([labels, labels])
+        ctx.temb2 = None if temb is None else torch.cat([temb, temb])
+        ctx.z_unsort = z_unsort
+        ctx.mark_non_differentiable(z_sorted, z_unsort)
+        return out, z_sorted, z_unsort
+
+    @staticmethod
+    def backward(ctx, d_out, _dzs, _dzu):
+        if ctx.ws is None:
+            raise RuntimeError("SPNeRF MLP backward called twice on the same forward (its activations are freed)")
+        B, S, NO = ctx.B, ctx.S, ctx.model.number_of_outputs
+        d_out = d_out.contiguous()
+        d_seg = torch.empty(2 * B * S, NO, dtype=torch.float32, device=d_out.device)
+        _lib.check(_lib.lib().spnerf_merge_samples_backward(B, S, S, _lib.ptr(ctx.z_unsort), _lib.ptr(d_out), NO,
+                                                            _lib.ptr(d_seg), _lib.stream_of(d_out)),
+                   "merge_samples_backward")
+        temb_grad = ctx.temb2 is not None and ctx.needs_input_grad[5]
+        gt2, grads = _mlp_backward(ctx.model, ctx.pack, ctx.packed, ctx.ws, SPNERF_MLP_SAVE, ctx.rays2, ctx.labels2,
+                                   ctx.temb2, 2 * B, S, d_seg, temb_grad)
+        ctx.pack = ctx.packed = ctx.ws = None
+        gt = None if gt2 is None else gt2[:B] + gt2[B:]
+        return (None, None, None, None, None, gt, None, *grads)
+
+
+def mlp_saves(model: SPNeRF, temb=None) -> bool:
+    """Whether run_mlp would run a saving (differentiable) forward."""
+    return torch.is_grad_enabled() and (any(p.requires_grad for p in model.canonical_parameters()) or
+                                        (temb is not None and temb.requires_grad))
+
+
+def guided_main_pass(model: SPNeRF, rays, z1, labels, temb, guide, pack: "WeightPack"):
+    """The guided main pass's MLP rows in sorted depth order (see _GuidedMain): returns (out,
+    z_sorted, z_unsort) with out (B·2S, number_of_outputs)."""
+    _lib.require_device(rays, z1, labels, temb)
+    rays = rays.contiguous().float()
+    z1 = z1.contiguous().float()
+    if labels is not None:
+        labels = labels.reshape(-1).to(torch.int64).contiguous()
+    if temb is not None:
+        temb = temb.contiguous().float()
+    if not pack.owned:
+        raise _lib.SpnerfError("guided_main_pass needs a render pack of its own (pack_for_render under grad)")
+    return _GuidedMain.apply(model, pack, rays, z1, labels, temb, guide, *model.canonical_parameters())
 
 
 def run_mlp(model: SPNeRF, rays: torch.Tensor, z: torch.Tensor, dir_offset: int, labels=None, temb=None,

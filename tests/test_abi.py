@@ -21,7 +21,7 @@ def header_symbols():
 def test_library_loads_and_exports_every_declared_symbol():
     L = _lib.lib()
     syms = header_symbols()
-    assert len(syms) == 36
+    assert len(syms) == 39
     for s in syms:
         assert hasattr(L, s), s
     assert sorted(_lib.SIGNATURES) == syms, "ctypes signature table out of sync with the header"
