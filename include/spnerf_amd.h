@@ -200,14 +200,14 @@ int32_t spnerf_sample_3sigma(int64_t n_rays, int32_t n, const float* low, const 
 /* row-wise ascending sort of (n_rays, n) floats, n <= 256 (torch.sort(-1) values) */
 int32_t spnerf_sort_rows(int64_t n_rays, int32_t n, const float* in, float* out, void* stream);
 /* rendering.py:165-168: the main pass's rows in the sorted depth order, gathered from two segments
- * of MLP rows — s1 per ray (pass 1's stratified samples, rows [0, n_rays*s1)) then s2 per ray (the
- * guided samples, rows [n_rays*s1, n_rays*(s1+s2))) — by the ranks of z_unsort = [z | sorted z_2]
- * (n_rays, s1+s2), the reference's z_vals_unsort.  out_sorted (n_rays*(s1+s2), n_out).  The
- * backward scatters the sorted rows' gradients d_sorted back into the segments' rows d_seg. */
-int32_t spnerf_merge_samples(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* out_seg,
-                             int32_t n_out, float* out_sorted, void* stream);
+ * of MLP rows — out1 (n_rays*s1, n_out): pass 1's stratified samples, s1 per ray; out2
+ * (n_rays*s2, n_out): the guided samples, s2 per ray — by the ranks of z_unsort = [z | sorted
+ * z_2] (n_rays, s1+s2), the reference's z_vals_unsort.  out_sorted (n_rays*(s1+s2), n_out).  The
+ * backward scatters the sorted rows' gradients d_sorted back into the segments' rows. */
+int32_t spnerf_merge_samples(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* out1,
+                             const float* out2, int32_t n_out, float* out_sorted, void* stream);
 int32_t spnerf_merge_samples_backward(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort,
-                                      const float* d_sorted, int32_t n_out, float* d_seg, void* stream);
+                                      const float* d_sorted, int32_t n_out, float* d_out1, float* d_out2, void* stream);
 
 /* ---- RPC camera rays: get_rays + normalize_rays + get_sun_dirs (datasets/satellite_scene.py:21-68,
  *      :415-425, :449-473; modules/utils.py:59-100).  rpc = 90 host doubles: row/col/lat/lon/alt

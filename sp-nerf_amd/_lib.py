@@ -81,9 +81,10 @@ SIGNATURES = {
                                     POINTER(Rng), c_void_p]),
     "spnerf_sample_3sigma": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "spnerf_sort_rows": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
-    "spnerf_merge_samples": (c_int32, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "spnerf_merge_samples": (c_int32, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                       c_void_p]),
     "spnerf_merge_samples_backward": (c_int32, [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
-                                                c_void_p]),
+                                                c_void_p, c_void_p]),
     "spnerf_rpc_rays": (c_int32, [POINTER(c_double), c_double, c_double, c_double, c_int32, c_int32, c_int32, c_int32,
                                   c_void_p, c_int64, POINTER(c_float), c_float, POINTER(c_float), c_void_p, c_int32,
                                   c_void_p]),

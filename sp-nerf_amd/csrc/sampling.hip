@@ -260,9 +260,10 @@ __global__ __launch_bounds__(256) void k_sort_rows(int64_t B, int n, const float
 // sorted position of element e of z_unsort = [z | sorted z_2] (the reference's z_vals_unsort) is
 // its rank #{f : z[f] < z[e]} + #{f < e : z[f] == z[e]} — a permutation into ascending order, so
 // the rows land where torch.sort puts their depths (equal depths are the same point: equal rows).
+// bwd = 0: sorted ← segments; 1: segments ← sorted (the pointers' roles swap, not their types)
 __global__ __launch_bounds__(256) void k_merge_rows(int64_t B, int s1, int s2, const float* __restrict__ zu,
-                                                    const float* __restrict__ in, int n_out, float* __restrict__ out,
-                                                    int bwd) {
+                                                    float* __restrict__ seg1, float* __restrict__ seg2,
+                                                    float* __restrict__ sorted, int n_out, int bwd) {
     __shared__ float zs[4][256];
     __shared__ int src[4][256];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -286,9 +287,11 @@ __global__ __launch_bounds__(256) void k_merge_rows(int64_t B, int s1, int s2, c
     for (int64_t i = lane; i < nn; i += 64) {
         const int t = (int)(i / n_out), col = (int)(i - (int64_t)t * n_out);
         const int e = src[wv][t];
-        const int64_t row = e < s1 ? ray * s1 + e : B * s1 + ray * s2 + (e - s1);
-        if (!bwd) out[(ray * n + t) * n_out + col] = in[row * n_out + col];
-        else out[row * n_out + col] = in[(ray * n + t) * n_out + col];
+        // the segment row of element e: seg1 row ray·s1 + e, or seg2 row ray·s2 + (e - s1)
+        float* sp = e < s1 ? seg1 + (ray * s1 + e) * n_out + col : seg2 + (ray * s2 + (e - s1)) * n_out + col;
+        float* so = sorted + (ray * n + t) * n_out + col;
+        if (!bwd) *so = *sp;
+        else *sp = *so;
     }
 }
 
@@ -296,27 +299,28 @@ __global__ __launch_bounds__(256) void k_merge_rows(int64_t B, int s1, int s2, c
 
 using namespace spn;
 
-static int32_t merge_rows(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* in, int32_t n_out,
-                          float* out, int bwd, hipStream_t s) {
-    SPN_ARG(z_unsort && in && out, "merge_samples: NULL pointer");
+static int32_t merge_rows(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, float* seg1, float* seg2,
+                          float* sorted, int32_t n_out, int bwd, hipStream_t s) {
+    SPN_ARG(z_unsort && seg1 && seg2 && sorted, "merge_samples: NULL pointer");
     SPN_ARG(s1 >= 1 && s2 >= 1 && s1 + s2 <= 256 && n_out >= 1 && n_rays >= 0, "merge_samples: bad sizes");
-    SPN_ARG(n_rays * (s1 + s2) * (int64_t)n_out < (1ll << 40), "merge_samples: too large");
     if (n_rays == 0) return SPNERF_OK;
     ProfScope prof("merge_samples", s, 0.0, (double)n_rays * (s1 + s2) * (8.0 * n_out + 4.0));
-    hipLaunchKernelGGL(k_merge_rows, dim3((unsigned)((n_rays + 3) / 4)), dim3(256), 0, s, n_rays, s1, s2, z_unsort, in,
-                       n_out, out, bwd);
+    hipLaunchKernelGGL(k_merge_rows, dim3((unsigned)((n_rays + 3) / 4)), dim3(256), 0, s, n_rays, s1, s2, z_unsort, seg1,
+                       seg2, sorted, n_out, bwd);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
 
-extern "C" int32_t spnerf_merge_samples(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* out_seg,
-                                        int32_t n_out, float* out_sorted, void* stream) {
-    return merge_rows(n_rays, s1, s2, z_unsort, out_seg, n_out, out_sorted, 0, (hipStream_t)stream);
+extern "C" int32_t spnerf_merge_samples(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort, const float* out1,
+                                        const float* out2, int32_t n_out, float* out_sorted, void* stream) {
+    return merge_rows(n_rays, s1, s2, z_unsort, const_cast<float*>(out1), const_cast<float*>(out2), out_sorted, n_out, 0,
+                      (hipStream_t)stream);
 }
 
 extern "C" int32_t spnerf_merge_samples_backward(int64_t n_rays, int32_t s1, int32_t s2, const float* z_unsort,
-                                                 const float* d_sorted, int32_t n_out, float* d_seg, void* stream) {
-    return merge_rows(n_rays, s1, s2, z_unsort, d_sorted, n_out, d_seg, 1, (hipStream_t)stream);
+                                                 const float* d_sorted, int32_t n_out, float* d_out1, float* d_out2,
+                                                 void* stream) {
+    return merge_rows(n_rays, s1, s2, z_unsort, d_out1, d_out2, const_cast<float*>(d_sorted), n_out, 1, (hipStream_t)stream);
 }
 
 static spnerf_rng rng_or_null(const spnerf_rng* r) { return r ? *r : spnerf_rng{nullptr, 0, 0, 0}; }

@@ -26,7 +26,8 @@ import torch
 
 from . import _lib
 from .rng import begin_render, current_random_source, device_key
-from .spnerf import _result, composite, guided_main_pass, inference_rays, mlp_saves, pack_for_render
+from .spnerf import (_result, composite, guided_inference_pass, guided_main_pass, inference_rays, mlp_saves,
+                     pack_for_render)
 
 # Training renders with guided sampling evaluate each main-pass point once (spnerf._GuidedMain):
 # False = the reference's two evaluations of the stratified points (pass 1 σ-only, then the
@@ -183,9 +184,10 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
         rays_t = models["t"](ts) if ts is not None else None                       # rendering.py:156
     sem = semantics if model.sem else None
     pk = pack_for_render(model)   # every pass of this render reads the same packed weights
-    if args.guidedsample and REUSE_PASS1 and mlp_saves(model, rays_t if model.beta else None):
-        # training: pass 1's rows ARE the main pass's rows at the stratified depths — one saving
-        # forward in two windows, composited in the sorted order (spnerf._GuidedMain)
+    if args.guidedsample and REUSE_PASS1:
+        # pass 1's rows ARE the main pass's rows at the stratified depths: each point is evaluated
+        # once and the rows are composited in the sorted order (training: one saving forward in
+        # two windows, spnerf._GuidedMain; no gradient: two forwards, guided_inference_pass)
         cnf = None if clamp_near_far is None else clamp_near_far.reshape(2).to(rays.device, torch.float32).contiguous()
 
         def guide(out1, z1):
@@ -193,8 +195,9 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
             return _guided({"depth": depth1, "weights": w1}, z1, N_samples, rays, mode, valid_depth, target_depths,
                            target_std, cnf)
 
-        out, z_vals, z_unsort = guided_main_pass(model, rays, z_vals, sem if model.sem else None,
-                                                 rays_t if model.beta else None, guide, pk)
+        t_in = rays_t if model.beta else None
+        run = guided_main_pass if mlp_saves(model, t_in) else guided_inference_pass
+        out, z_vals, z_unsort = run(model, rays, z_vals, sem if model.sem else None, t_in, guide, pk)
         rgb, depth, w, T, sem_l = composite(model, out, z_vals, args.noise_std)
         result = _result(model, out, z_vals, rgb, depth, w, T, sem_l, z_unsort)
     elif args.guidedsample:

@@ -481,8 +481,8 @@ class _GuidedMain(torch.autograd.Function):
         z2 = z_unsort[:, S:].contiguous()
         window(B, z2)
         out = torch.empty(B * 2 * S, NO, dtype=torch.float32, device=dev)
-        _lib.check(L.spnerf_merge_samples(B, S, S, _lib.ptr(z_unsort), _lib.ptr(seg), NO, _lib.ptr(out),
-                                          _lib.stream_of(rays)), "merge_samples")
+        _lib.check(L.spnerf_merge_samples(B, S, S, _lib.ptr(z_unsort), _lib.ptr(seg), _lib.ptr(seg[B * S:]), NO,
+                                          _lib.ptr(out), _lib.stream_of(rays)), "merge_samples")
         pack.pending += 1
         pack.nsave += 1
         ctx.model, ctx.ws, ctx.pack, ctx.packed, ctx.B, ctx.S = model, ws, pack, packed, B, S
@@ -501,7 +501,7 @@ class _GuidedMain(torch.autograd.Function):
         d_out = d_out.contiguous()
         d_seg = torch.empty(2 * B * S, NO, dtype=torch.float32, device=d_out.device)
         _lib.check(_lib.lib().spnerf_merge_samples_backward(B, S, S, _lib.ptr(ctx.z_unsort), _lib.ptr(d_out), NO,
-                                                            _lib.ptr(d_seg), _lib.stream_of(d_out)),
+                                                            _lib.ptr(d_seg), _lib.ptr(d_seg[B * S:]), _lib.stream_of(d_out)),
                    "merge_samples_backward")
         temb_grad = ctx.temb2 is not None and ctx.needs_input_grad[5]
         gt2, grads = _mlp_backward(ctx.model, ctx.pack, ctx.packed, ctx.ws, SPNERF_MLP_SAVE, ctx.rays2, ctx.labels2,
@@ -515,6 +515,22 @@ def mlp_saves(model: SPNeRF, temb=None) -> bool:
     """Whether run_mlp would run a saving (differentiable) forward."""
     return torch.is_grad_enabled() and (any(p.requires_grad for p in model.canonical_parameters()) or
                                         (temb is not None and temb.requires_grad))
+
+
+def guided_inference_pass(model: SPNeRF, rays, z1, labels, temb, guide, pack: "WeightPack"):
+    """The no-gradient twin of ``guided_main_pass``: pass 1 runs every head over the stratified
+    depths (instead of σ alone), the second forward only the guided ones, and
+    ``spnerf_merge_samples`` gathers both into the sorted order — each point evaluated once."""
+    B, S = z1.shape
+    with torch.no_grad():
+        out1 = run_mlp(model, rays, z1, 3, labels, temb, pack=pack)
+        z_sorted, z_unsort = guide(out1, z1)
+        out2 = run_mlp(model, rays, z_unsort[:, S:].contiguous(), 3, labels, temb, pack=pack)
+        out = torch.empty(B * 2 * S, model.number_of_outputs, dtype=torch.float32, device=rays.device)
+        _lib.check(_lib.lib().spnerf_merge_samples(B, S, S, _lib.ptr(z_unsort), _lib.ptr(out1), _lib.ptr(out2),
+                                                   model.number_of_outputs, _lib.ptr(out), _lib.stream_of(out1)),
+                   "merge_samples")
+    return out, z_sorted, z_unsort
 
 
 def guided_main_pass(model: SPNeRF, rays, z1, labels, temb, guide, pack: "WeightPack"):

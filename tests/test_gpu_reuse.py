@@ -123,11 +123,19 @@ def test_reuse_beta_t_embedding_gradient():
 
 
 def _merge(z_unsort, seg, s1, s2, bwd=False):
+    """forward: the two segments (rows [0, B·s1) and the rest of ``seg``) → sorted rows;
+    backward: sorted rows ``seg`` → the two segments, returned as one tensor"""
     B = z_unsort.shape[0]
     NO = seg.shape[1]
     out = torch.full((B * (s1 + s2), NO), float("nan"), device=DEV)
-    fn = _lib.lib().spnerf_merge_samples_backward if bwd else _lib.lib().spnerf_merge_samples
-    _lib.check(fn(B, s1, s2, _lib.ptr(z_unsort), _lib.ptr(seg), NO, _lib.ptr(out), _lib.stream_of(seg)), "merge")
+    L = _lib.lib()
+    if bwd:
+        rc = L.spnerf_merge_samples_backward(B, s1, s2, _lib.ptr(z_unsort), _lib.ptr(seg), NO, _lib.ptr(out),
+                                             _lib.ptr(out[B * s1:]), _lib.stream_of(seg))
+    else:
+        rc = L.spnerf_merge_samples(B, s1, s2, _lib.ptr(z_unsort), _lib.ptr(seg), _lib.ptr(seg[B * s1:]), NO,
+                                    _lib.ptr(out), _lib.stream_of(seg))
+    _lib.check(rc, "merge")
     torch.cuda.synchronize()
     return out
 
@@ -156,3 +164,23 @@ def test_merge_rows_is_the_sort_permutation(s1, s2):
     assert torch.equal(torch.sort(back.reshape(-1))[0], torch.sort(d.reshape(-1))[0])
     fwd_again = _merge(zu, back.to(DEV).contiguous(), s1, s2).cpu()
     assert torch.equal(fwd_again, d)
+
+
+@pytest.mark.parametrize("name,precision", [("c3_test_w64", "fp32"), ("c3_w512", "fp32"), ("c3_w512", "bf16")])
+def test_reuse_no_grad_render_equals_two_evaluations(name, precision):
+    """Renders without gradients (evaluation): pass 1 with every head, then the guided points
+    only (guided_inference_pass) — per point the same kernels' arithmetic as the main pass over
+    the sorted union, so the renders are bit for bit those of the two-evaluation schedule."""
+    outs = []
+    for reuse in (True, False):
+        old = rendering.REUSE_PASS1
+        rendering.REUSE_PASS1 = reuse
+        try:
+            with torch.no_grad():
+                _, res, _ = run_case(name, precision)
+        finally:
+            rendering.REUSE_PASS1 = old
+        outs.append({k: v.cpu().numpy() for k, v in res.items() if torch.is_tensor(v)})
+    assert sorted(outs[0]) == sorted(outs[1])
+    for k in outs[1]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)

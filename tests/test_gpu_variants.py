@@ -510,8 +510,9 @@ def test_training_heads_kernel_agree(sem, n, n_samples, guided):
 
 
 def test_training_heads_kernel_launches():
-    """heads_epi 2 replaces the forward's head GEMM launches by one heads launch per pass (main
-    and solar)."""
+    """heads_epi 2 replaces the forward's head GEMM launches by one heads launch per forward: the
+    guided main pass's two windows (pass 1's stratified points, then the guided ones) and the
+    solar pass."""
     from spnerf_amd import _lib as L
     L.prof_reset()
     L.prof_enable(True)
@@ -521,4 +522,4 @@ def test_training_heads_kernel_launches():
         L.prof_enable(False)
     classes = L.prof_classes()
     assert "heads_train" in classes, classes
-    assert L.prof_read("heads_train")["launches"] == 2   # main and solar pass
+    assert L.prof_read("heads_train")["launches"] == 3   # main pass windows 0 and 1, solar pass
