@@ -69,6 +69,10 @@ typedef struct spnerf_rng {
 
 /* composite flags */
 #define SPNERF_COMP_WEIGHTS_ONLY 1  /* weights, transparency, depth only (no rgb / sem)      */
+#define SPNERF_COMP_SUN_COLUMN 2    /* with WEIGHTS_ONLY: `rgb` receives the sun-visibility column
+                                     * (n_rays, n_samples) of `out` (the solar pass's sun_sc,
+                                     * rendering.py:177) and the backward's g_rgb is its gradient,
+                                     * written into d_out's sun column (no separate slice gradient) */
 
 /* ---- library ---------------------------------------------------------------------------- */
 const char* spnerf_last_error(void);
@@ -96,7 +100,8 @@ int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed,
                            void* workspace, float* out, void* stream);
 /* spnerf_mlp_forward over rays [ray_begin, ray_begin + n_rays) of a workspace laid out for
  * n_rays_total rays (spnerf_mlp_workspace_bytes(cfg, n_rays_total, n_samples, flags)): rays, z,
- * labels, t_emb and out are the window's own rows.  Windows filled at different times make ONE
+ * labels, t_emb and out are the window's own rows; depth j of ray r is z[r * z_stride + j]
+ * (z_stride 0 = n_samples).  Windows filled at different times make ONE
  * saving forward whose backward runs over all n_rays_total rays — render_rays' guided main pass
  * (rendering.py:159-170) evaluates its stratified half in pass 1 (window 0, whose sigma feeds
  * the guided windows) and only the guided half afterwards (window 1, the rays repeated), instead
@@ -104,8 +109,8 @@ int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed,
 int32_t spnerf_mlp_forward_window(const spnerf_model_cfg* cfg, const void* packed,
                                   const float* rays, int32_t ray_stride, int32_t dir_offset,
                                   int64_t n_rays_total, int64_t ray_begin, int64_t n_rays, int32_t n_samples,
-                                  const float* z, const int64_t* labels, const float* t_emb, int32_t flags,
-                                  void* workspace, float* out, void* stream);
+                                  const float* z, int32_t z_stride, const int64_t* labels, const float* t_emb,
+                                  int32_t flags, void* workspace, float* out, void* stream);
 /* Gradients of sum(d_out * out) w.r.t. every parameter, written (overwritten, or added with
  * SPNERF_MLP_ACCUMULATE in `flags`) into `grad_flat` (canonical order, torch shapes,
  * contiguous) and w.r.t. t_emb (n_rays, t_dim, overwritten).  The workspace of a SAVE forward

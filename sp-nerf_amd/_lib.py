@@ -20,6 +20,7 @@ SPNERF_MLP_SUN_ONLY = 4
 SPNERF_MLP_ACCUMULATE = 8
 SPNERF_MLP_DEFER_TRUNK_WGRAD = 16
 SPNERF_COMP_WEIGHTS_ONLY = 1
+SPNERF_COMP_SUN_COLUMN = 2
 
 
 class ModelCfg(ctypes.Structure):
@@ -55,8 +56,8 @@ SIGNATURES = {
     "spnerf_mlp_forward": (c_int32, [POINTER(ModelCfg), c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p,
                                      c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "spnerf_mlp_forward_window": (c_int32, [POINTER(ModelCfg), c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int64,
-                                            c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
-                                            c_void_p]),
+                                            c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
+                                            c_void_p, c_void_p]),
     "spnerf_mlp_backward": (c_int32, [POINTER(ModelCfg), c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p,
                                       c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "spnerf_composite_forward": (c_int32, [c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_float, c_int32,

@@ -25,6 +25,10 @@ struct CompArgs {
     float *rgb, *depth, *w, *T, *sem;
     const float *g_rgb, *g_depth, *g_w, *g_T, *g_sem;
     float* d_out;
+    // weights-only passes with SPNERF_COMP_SUN_COLUMN: the sun-visibility column out (forward),
+    // its gradient into d_out's sun column (backward) — the solar pass's sun_sc (rendering.py:177)
+    float* sun_out;
+    const float* g_sun;
 };
 
 __device__ __forceinline__ float relu_t(float x) { return x != x ? x : (x > 0.f ? x : 0.f); }
@@ -119,6 +123,8 @@ __global__ __launch_bounds__(256) void k_composite_fwd(CompArgs a) {
     float* rows = sh_rows + (threadIdx.x >> 6) * (S * NO);
     if (a.weights_only) {   // σ is the only column read: stride loads of one column
         for (int e = lane; e < S; e += 64) rows[e * NO + 3] = a.out[(ray * S + e) * NO + 3];
+        if (a.sun_out)
+            for (int e = lane; e < S; e += 64) a.sun_out[ray * S + e] = a.out[(ray * S + e) * NO + 4];
         wave_lds_sync();
     } else {
         stage_rows(a.out + ray * (int64_t)(S * NO), rows, S * NO, lane);
@@ -255,6 +261,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(CompArgs a) {
         }
         if (col && a.g_sem)
             for (int c = 0; c < a.n_sem; ++c) dO[a.sem_col + c] = a.g_sem[ray * a.n_sem + c] / (float)S;
+        if (!col && a.g_sun) dO[4] = a.g_sun[p];
         const float dT = dw * st.al[j] + (a.g_T ? a.g_T[p] : 0.f);
         dal[j] = dw * st.T[j];
         q[j] = st.T[j] * dT;
@@ -339,6 +346,11 @@ extern "C" int32_t spnerf_composite_forward(int64_t n_rays, int32_t n_samples, c
     a.z = z; a.out = out; a.noise = noise; a.noise_std = noise_std;
     if (!noise && rng && noise_std != 0.f) a.rng = *rng;
     a.rgb = rgb; a.depth = depth; a.w = weights; a.T = transparency; a.sem = sem_logits;
+    if (flags & SPNERF_COMP_SUN_COLUMN) {
+        SPN_ARG(wo && rgb, "composite_forward: SPNERF_COMP_SUN_COLUMN needs SPNERF_COMP_WEIGHTS_ONLY and rgb");
+        a.sun_out = rgb;
+        a.rgb = nullptr;
+    }
     return run_comp(a, true, (hipStream_t)stream);
 }
 
@@ -355,5 +367,10 @@ extern "C" int32_t spnerf_composite_backward(int64_t n_rays, int32_t n_samples, 
     if (!noise && rng && noise_std != 0.f) a.rng = *rng;
     a.g_rgb = g_rgb; a.g_depth = g_depth; a.g_w = g_weights; a.g_T = g_transparency; a.g_sem = g_sem;
     a.d_out = d_out;
+    if (flags & SPNERF_COMP_SUN_COLUMN) {
+        SPN_ARG(wo, "composite_backward: SPNERF_COMP_SUN_COLUMN needs SPNERF_COMP_WEIGHTS_ONLY");
+        a.g_sun = g_rgb;
+        a.g_rgb = nullptr;
+    }
     return run_comp(a, false, (hipStream_t)stream);
 }

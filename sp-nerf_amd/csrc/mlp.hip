@@ -147,14 +147,15 @@ __global__ __launch_bounds__(256) void k_pack_dev(const PackPiece* __restrict__ 
 // X0s = [hi | lo | hi | lo] (hi = bf16(v), lo = bf16(v − hi), row length 4·K0p) is written when
 // non-null.  o + dir*z is evaluated as two rounded ops like the reference
 // (no FMA contraction: sin(2^9 x) amplifies a 1-ulp difference in x by 512).
-__global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, const float* __restrict__ z, int S,
+__global__ void k_encode(const float* __restrict__ rays, int rs, int dir_off, const float* __restrict__ z, int S, int ldz,
                          int64_t P, int n_freq, int K0, int K0p, float* __restrict__ X0, bf16* __restrict__ X0b,
                          bf16* __restrict__ X0s) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= P * K0p) return;
     const int64_t p = i / K0p;
     const int c = (int)(i % K0p);
-    const float v = c < K0 ? pe_value(rays + (p / S) * rs, dir_off, z[p], c, n_freq, K0) : 0.f;
+    const int64_t r = p / S;
+    const float v = c < K0 ? pe_value(rays + r * rs, dir_off, z[r * ldz + (p - r * S)], c, n_freq, K0) : 0.f;
     if (X0) X0[i] = v;
     const bf16 hi = (bf16)v;
     if (X0b) X0b[i] = hi;
@@ -1187,6 +1188,7 @@ struct Ctx {
     const float* rays = nullptr;
     const float* z = nullptr;
     int rs = 0, dir_off = 0;
+    int ldz = 0;                    // z's row stride per ray (S: contiguous rows)
     float* out = nullptr;           // the forward's output rows (the fused trunk + heads write them)
     bool* heads_done = nullptr;     // set when the trunk launch ran the fused heads too
     bool* heads_epi_done = nullptr;  // set when the head GEMMs' epilogues wrote the narrow heads
@@ -1509,7 +1511,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
             a.X0b = c.hb(c.w.X0b);
             if (first == 0) {
                 if (pe_inline_on(c, save)) {
-                    a.rays = c.rays; a.rs = c.rs; a.dir_off = c.dir_off; a.z = c.z;
+                    a.rays = c.rays; a.rs = c.rs; a.dir_off = c.dir_off; a.z = c.z; a.ldz = c.ldz;
                     a.n_freq = d.K0 == 3 ? 0 : d.K0 / 6; a.K0 = d.K0;
                     if (save) a.X0b_out = c.hb(c.w.X0b);
                 } else {
@@ -1702,7 +1704,7 @@ static int32_t forward_gemms(const Ctx& c, bool save, int mode, hipStream_t s, b
 
 static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays, int rs, int dir_off,
                            int64_t n_rays, int S, const float* z, const int64_t* labels, const float* temb, int flags,
-                           float* ws, float* out, hipStream_t s, int64_t n_total = -1, int64_t r0 = 0) {
+                           float* ws, float* out, hipStream_t s, int64_t n_total = -1, int64_t r0 = 0, int ldz = 0) {
     // n_total >= 0: rays [r0, r0 + n_rays) of a workspace laid out for n_total rays (forward_window)
     Ctx c{d, packed_layout(d),
           n_total < 0 ? ws_layout(d, n_rays, S, flags) : ws_window(d, ws_layout(d, n_total, S, flags), r0, n_rays, S),
@@ -1733,7 +1735,7 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
     }
     // positional encoding (fp32 for layer 0, plus a bf16 copy for the skip layer / dW_0); the
     // fused inference trunk with layer 0 computes it in its staging instead
-    c.rays = rays; c.rs = rs; c.dir_off = dir_off; c.z = z;
+    c.rays = rays; c.rs = rs; c.dir_off = dir_off; c.z = z; c.ldz = ldz > 0 ? ldz : S;
     if (!pe_inline_on(c, save)) {
         const int64_t n = P * d.K0p;
         // bf16 MLP, layer 0 on bf16 planes: a separate GEMM reads the planes X0s; inside the
@@ -1741,7 +1743,7 @@ static int32_t mlp_forward(const Dims& d, const float* packed, const float* rays
         const bool l0t = trunk_l0_on(c, save);
         const bool planes = d.bf && g_l0_split && !l0t;
         ProfScope prof("encode", s, 0.0, (planes ? 10.0 : 4.0 + (d.bf ? 2.0 : 0.0)) * n);
-        hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rays, rs, dir_off, z, S, P,
+        hipLaunchKernelGGL(k_encode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rays, rs, dir_off, z, S, c.ldz, P,
                            d.K0 == 3 ? 0 : d.K0 / 6, d.K0, d.K0p, planes ? nullptr : c.at(c.w.X0),
                            d.bf ? c.hb(c.w.X0b) : nullptr, planes ? c.hb(c.w.X0s) : nullptr);
         SPN_HIP(hipGetLastError());
@@ -2612,8 +2614,8 @@ extern "C" int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* p
 extern "C" int32_t spnerf_mlp_forward_window(const spnerf_model_cfg* cfg, const void* packed, const float* rays,
                                              int32_t ray_stride, int32_t dir_offset, int64_t n_rays_total,
                                              int64_t ray_begin, int64_t n_rays, int32_t n_samples, const float* z,
-                                             const int64_t* labels, const float* t_emb, int32_t flags, void* workspace,
-                                             float* out, void* stream) {
+                                             int32_t z_stride, const int64_t* labels, const float* t_emb, int32_t flags,
+                                             void* workspace, float* out, void* stream) {
     Dims d;
     SPN_TRY(make_dims(cfg, &d));
     SPN_ARG(packed && rays && z && workspace && out, "mlp_forward_window: NULL pointer");
@@ -2623,8 +2625,9 @@ extern "C" int32_t spnerf_mlp_forward_window(const spnerf_model_cfg* cfg, const 
     SPN_ARG((ray_begin * n_samples) % 2 == 0, "mlp_forward_window: the window must start at an even point");
     SPN_ARG(n_rays_total * n_samples < (1ll << 31) / std::max(d.NQ, d.NG), "mlp_forward_window: too many points");
     SPN_ARG(dir_offset == 3 || dir_offset == 8, "mlp_forward_window: dir_offset must be 3 (view) or 8 (sun)");
+    SPN_ARG(z_stride == 0 || z_stride >= n_samples, "mlp_forward_window: z_stride %d < n_samples %d", z_stride, n_samples);
     return mlp_forward(d, (const float*)packed, rays, ray_stride, dir_offset, n_rays, n_samples, z, labels, t_emb, flags,
-                       (float*)workspace, out, (hipStream_t)stream, n_rays_total, ray_begin);
+                       (float*)workspace, out, (hipStream_t)stream, n_rays_total, ray_begin, z_stride);
 }
 
 extern "C" int32_t spnerf_mlp_backward(const spnerf_model_cfg* cfg, const void* packed, const float* rays,

@@ -260,38 +260,76 @@ __global__ __launch_bounds__(256) void k_sort_rows(int64_t B, int n, const float
 // sorted position of element e of z_unsort = [z | sorted z_2] (the reference's z_vals_unsort) is
 // its rank #{f : z[f] < z[e]} + #{f < e : z[f] == z[e]} — a permutation into ascending order, so
 // the rows land where torch.sort puts their depths (equal depths are the same point: equal rows).
+// One 256-thread block per ray (n = s1 + s2 <= 256: one element per thread for the ranks).  The
+// ray's rows move through LDS so that every global access is a contiguous run of the ray's rows,
+// all issued up front: forward the two segments' runs (s1·n_out and s2·n_out floats) in and the
+// sorted run out, backward the reverse.  The ranks are formed while the rows are in flight.
 // bwd = 0: sorted ← segments; 1: segments ← sorted (the pointers' roles swap, not their types)
 __global__ __launch_bounds__(256) void k_merge_rows(int64_t B, int s1, int s2, const float* __restrict__ zu,
                                                     float* __restrict__ seg1, float* __restrict__ seg2,
                                                     float* __restrict__ sorted, int n_out, int bwd) {
-    __shared__ float zs[4][256];
-    __shared__ int src[4][256];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t ray = (int64_t)blockIdx.x * 4 + wv;
-    const bool active = ray < B;
+    extern __shared__ __attribute__((aligned(16))) float msm[];
+    const int tid = threadIdx.x;
+    const int64_t ray = blockIdx.x;
     const int n = s1 + s2;
-    for (int e = lane; e < n; e += 64) zs[wv][e] = active ? zu[ray * n + e] : 0.f;
-    __syncthreads();
-    for (int e = lane; e < n; e += 64) {
-        const float v = zs[wv][e];
-        int rank = 0;
-        for (int f = 0; f < n; ++f) {
-            const float w = zs[wv][f];
-            rank += (w < v) || (w == v && f < e);
+    const int n4 = (n + 3) & ~3;  // z padded with +inf to whole float4s (never below a finite depth)
+    float* zs = msm;                                    // [n4]
+    int* rank_of = reinterpret_cast<int*>(msm + n4);    // [n]
+    int* src = rank_of + n;                             // [n]: sorted position → element
+    float* rows = msm + n4 + 2 * n;                     // [n · n_out]
+    const float inv = 1.f / (float)n_out;
+    const int n1 = s1 * n_out, nn = n * n_out;
+    float* g1 = seg1 + ray * (int64_t)n1;
+    float* g2 = seg2 + ray * (int64_t)(s2 * n_out);
+    float* gs = sorted + ray * (int64_t)nn;
+    // the depths first, then (up to 256·U values) the rows: the depths' wait does not wait for them
+    const float zv = tid < n ? zu[ray * n + tid] : INFINITY;
+    constexpr int U = 8;
+    const bool fits = nn <= 256 * U;
+    auto src_of = [&](int i) -> float* { return bwd ? gs + i : (i < n1 ? g1 + i : g2 + (i - n1)); };
+    float v[U];
+    if (fits) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = tid + 256 * u;
+            v[u] = i < nn ? *src_of(i) : 0.f;
         }
-        src[wv][rank] = e;
+    }
+    if (tid < n4) zs[tid] = zv;
+    __syncthreads();
+    if (tid < n) {
+        int rank = 0;
+#pragma unroll 4
+        for (int f = 0; f < n4; f += 4) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(zs + f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rank += (w[q] < zv) || (w[q] == zv && f + q < tid);
+        }
+        rank_of[tid] = rank;
+        src[rank] = tid;
+    }
+    // the rows into LDS (element e's row at rows[e · n_out]: segment order forward, sorted order
+    // backward)
+    if (fits) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (tid + 256 * u < nn) rows[tid + 256 * u] = v[u];
+    } else {
+        for (int i = tid; i < nn; i += 256) rows[i] = *src_of(i);
     }
     __syncthreads();
-    if (!active) return;  // no barriers below
-    const int64_t nn = (int64_t)n * n_out;
-    for (int64_t i = lane; i < nn; i += 64) {
-        const int t = (int)(i / n_out), col = (int)(i - (int64_t)t * n_out);
-        const int e = src[wv][t];
-        // the segment row of element e: seg1 row ray·s1 + e, or seg2 row ray·s2 + (e - s1)
-        float* sp = e < s1 ? seg1 + (ray * s1 + e) * n_out + col : seg2 + (ray * s2 + (e - s1)) * n_out + col;
-        float* so = sorted + (ray * n + t) * n_out + col;
-        if (!bwd) *so = *sp;
-        else *sp = *so;
+    if (!bwd) {
+        for (int i = tid; i < nn; i += 256) {
+            const int t = (int)(((float)i + 0.5f) * inv), col = i - t * n_out;  // i / n_out (exact: i < 2^16)
+            gs[i] = rows[src[t] * n_out + col];
+        }
+    } else {
+        for (int i = tid; i < nn; i += 256) {
+            const int e = (int)(((float)i + 0.5f) * inv), col = i - e * n_out;
+            const float x = rows[rank_of[e] * n_out + col];
+            if (i < n1) g1[i] = x;
+            else g2[i - n1] = x;
+        }
     }
 }
 
@@ -305,8 +343,10 @@ static int32_t merge_rows(int64_t n_rays, int32_t s1, int32_t s2, const float* z
     SPN_ARG(s1 >= 1 && s2 >= 1 && s1 + s2 <= 256 && n_out >= 1 && n_rays >= 0, "merge_samples: bad sizes");
     if (n_rays == 0) return SPNERF_OK;
     ProfScope prof("merge_samples", s, 0.0, (double)n_rays * (s1 + s2) * (8.0 * n_out + 4.0));
-    hipLaunchKernelGGL(k_merge_rows, dim3((unsigned)((n_rays + 3) / 4)), dim3(256), 0, s, n_rays, s1, s2, z_unsort, seg1,
-                       seg2, sorted, n_out, bwd);
+    const size_t lds = sizeof(float) * ((size_t)(s1 + s2) * (3 + n_out) + 3);
+    SPN_ARG(lds <= 64 * 1024, "merge_samples: %d samples x %d outputs too large", s1 + s2, n_out);
+    hipLaunchKernelGGL(k_merge_rows, dim3((unsigned)n_rays), dim3(256), lds, s, n_rays, s1, s2, z_unsort, seg1, seg2, sorted,
+                       n_out, bwd);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -77,6 +77,7 @@ struct TrunkArgs {
     const float* rays = nullptr;
     const float* z = nullptr;
     int rs = 0, dir_off = 0, n_freq = 0, K0 = 0;
+    int ldz = 0;  // z's row stride per ray (sample j of ray r at z[r·ldz + j]); 0 = S (contiguous)
     // training with the inline encoding (k_trunk_bf16 only): the staging also writes each point's
     // bf16 PE row (the hi plane = k_encode's X0b) here, for the weight gradients of layer 0 and the
     // skip layer's PE columns

@@ -217,8 +217,9 @@ __global__ __launch_bounds__(T2Geo<TM>::NT, T2Geo<TM>::WGS) void k_trunk2_bf16(
                 const int64_t pr = std::min<int64_t>(p0 + row, g.P - 1);
                 float xv[8];
                 if (g.rays) {  // block-uniform: encode o + dir·z here (pe_value, as k_encode)
-                    const float* rp = g.rays + (pr / g.S) * g.rs;
-                    const float zz = g.z[pr];
+                    const int64_t rr = pr / g.S;
+                    const float* rp = g.rays + rr * g.rs;
+                    const float zz = g.z[rr * g.ldz + (pr - rr * g.S)];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) xv[e] = pe_value(rp, g.dir_off, zz, q * 8 + e, g.n_freq, g.K0);
                 } else {
@@ -505,6 +506,7 @@ int32_t trunk2_bf16(const TrunkArgs& a, hipStream_t s, bool save, double flop, d
     const int TM = trunk2_tm(a);
     const int ntiles = cdiv(a.P, TM);
     TrunkArgs ad = a;
+    if (ad.ldz == 0) ad.ldz = ad.S;  // contiguous z rows
     ad.dbg = g_trunk_dbg;
     ad.nt = save ? (g_trunk_nt & 1) : 0;
     const bool l0 = a.X0 || a.rays;
@@ -533,6 +535,7 @@ int32_t trunk2_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const Pac
     const int ntiles = cdiv(a.P, 128);
     Trunk2HeadsArgs ad;
     static_cast<TrunkArgs&>(ad) = a;
+    if (ad.ldz == 0) ad.ldz = ad.S;  // contiguous z rows
     ad.dbg = 0;
     ad.nt = 0;
     const bool l0 = a.X0 || a.rays;

@@ -259,8 +259,9 @@ __global__ __launch_bounds__(512) void k_trunk_bf16(std::conditional_t<(VAR & 40
                 const int64_t pr = std::min<int64_t>(p0 + row, g.P - 1);
                 float xv[8];
                 if (g.rays) {  // block-uniform: encode o + dir·z here (pe_value, as k_encode)
-                    const float* ray = g.rays + (int64_t)((int)pr / g.S) * g.rs;
-                    const float zz = g.z[pr];
+                    const int rr = (int)pr / g.S;
+                    const float* ray = g.rays + (int64_t)rr * g.rs;
+                    const float zz = g.z[(int64_t)rr * g.ldz + ((int)pr - rr * g.S)];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) xv[e] = NOPE ? ray[e & 3] * zz : pe_value(ray, g.dir_off, zz, q * 8 + e, g.n_freq, g.K0);
                 } else {
@@ -1120,6 +1121,7 @@ int32_t trunk1_heads_bf16(const TrunkArgs& a, const HeadsFusedArgs& h, const Pac
     const int ntiles = cdiv(a.P, 128);
     TrunkHeadsArgs ad;
     static_cast<TrunkArgs&>(ad) = a;
+    if (ad.ldz == 0) ad.ldz = ad.S;  // contiguous z rows
     ad.dbg = 0;
     ad.nt = 0;
     ad.hg = h;
@@ -1148,6 +1150,7 @@ int32_t trunk_bf16(const TrunkArgs& a, hipStream_t s, double flop, double bytes)
     SPN_ARG(!(a.X0 || a.rays) || (a.Wf[0] && trunk_l0_supported(a.K0p, save, a.zround != 0)), "trunk_bf16: layer 0 unsupported for K0p=%d",
             a.K0p);
     TrunkArgs ad = a;
+    if (ad.ldz == 0) ad.ldz = ad.S;  // contiguous z rows
     ad.dbg = g_trunk_dbg;
     ad.nt = (g_trunk_nt & 1) | ((g_trunk_nt & 4) ? 2 : 0);  // H copy-outs / register-D stores non-temporal
     const int ntiles = cdiv(a.P, tm);

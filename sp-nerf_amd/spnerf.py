@@ -19,8 +19,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_ACCUMULATE, SPNERF_MLP_DEFER_TRUNK_WGRAD, SPNERF_MLP_SAVE,
-                   SPNERF_MLP_SIGMA_ONLY, SPNERF_MLP_SUN_ONLY)
+from ._lib import (SPNERF_COMP_SUN_COLUMN, SPNERF_COMP_WEIGHTS_ONLY, SPNERF_MLP_ACCUMULATE, SPNERF_MLP_DEFER_TRUNK_WGRAD,
+                   SPNERF_MLP_SAVE, SPNERF_MLP_SIGMA_ONLY, SPNERF_MLP_SUN_ONLY)
 from .rng import current_random_source, device_key
 
 
@@ -472,14 +472,13 @@ class _GuidedMain(torch.autograd.Function):
 
         def window(r0, z):
             _lib.check(L.spnerf_mlp_forward_window(ctypes.byref(cfg), _lib.ptr(packed), _lib.ptr(rays), rays.stride(0), 3,
-                                                   2 * B, r0, B, S, _lib.ptr(z), _lib.ptr(labels), _lib.ptr(temb), flags,
-                                                   _lib.ptr(ws), _lib.ptr(seg[r0 * S:(r0 + B) * S]),
+                                                   2 * B, r0, B, S, _lib.ptr(z), z.stride(0), _lib.ptr(labels),
+                                                   _lib.ptr(temb), flags, _lib.ptr(ws), _lib.ptr(seg[r0 * S:(r0 + B) * S]),
                                                    _lib.stream_of(rays)), "mlp_forward_window")
 
         window(0, z1)
         z_sorted, z_unsort = guide(seg[:B * S], z1)
-        z2 = z_unsort[:, S:].contiguous()
-        window(B, z2)
+        window(B, z_unsort[:, S:])   # the sorted guided depths, read in place (row stride 2S)
         out = torch.empty(B * 2 * S, NO, dtype=torch.float32, device=dev)
         _lib.check(L.spnerf_merge_samples(B, S, S, _lib.ptr(z_unsort), _lib.ptr(seg), _lib.ptr(seg[B * S:]), NO,
                                           _lib.ptr(out), _lib.stream_of(rays)), "merge_samples")
@@ -491,6 +490,7 @@ class _GuidedMain(torch.autograd.Function):
         ctx.temb2 = None if temb is None else torch.cat([temb, temb])
         ctx.z_unsort = z_unsort
         ctx.mark_non_differentiable(z_sorted, z_unsort)
+        ctx.set_materialize_grads(False)   # the depth outputs take no gradient: no zero fills for them
         return out, z_sorted, z_unsort
 
     @staticmethod
@@ -498,6 +498,8 @@ class _GuidedMain(torch.autograd.Function):
         if ctx.ws is None:
             raise RuntimeError("SPNeRF MLP backward called twice on the same forward (its activations are freed)")
         B, S, NO = ctx.B, ctx.S, ctx.model.number_of_outputs
+        if d_out is None:   # the rows took no gradient (the backward still consumes the workspace)
+            d_out = torch.zeros(B * 2 * S, NO, dtype=torch.float32, device=ctx.rays2.device)
         d_out = d_out.contiguous()
         d_seg = torch.empty(2 * B * S, NO, dtype=torch.float32, device=d_out.device)
         _lib.check(_lib.lib().spnerf_merge_samples_backward(B, S, S, _lib.ptr(ctx.z_unsort), _lib.ptr(d_out), NO,
@@ -593,12 +595,16 @@ def max_points_per_call(model: SPNeRF) -> int:
 
 class _Composite(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, out, z, noise, noise_std, sem_col, n_sem, weights_only, rng=None, rng_keep=None):
+    def forward(ctx, out, z, noise, noise_std, sem_col, n_sem, weights_only, rng=None, rng_keep=None, sun_col=False):
         B, S = z.shape
         NO = out.shape[1]
         dev = out.device
         f = SPNERF_COMP_WEIGHTS_ONLY if weights_only else 0
-        rgb = torch.empty(B, 3, device=dev) if not weights_only else torch.empty(0, device=dev)
+        if weights_only and sun_col:   # the first output is then the sun column (B, S) of out
+            f |= SPNERF_COMP_SUN_COLUMN
+            rgb = torch.empty(B, S, device=dev)
+        else:
+            rgb = torch.empty(B, 3, device=dev) if not weights_only else torch.empty(0, device=dev)
         sem = torch.empty(B, n_sem, device=dev) if (n_sem and not weights_only) else torch.empty(0, device=dev)
         depth = torch.empty(B, device=dev)
         w = torch.empty(B, S, device=dev)
@@ -626,10 +632,13 @@ class _Composite(torch.autograd.Function):
                                                         _lib.ptr(g_depth), _lib.ptr(g_w), _lib.ptr(g_T),
                                                         _lib.ptr(g_sem), _lib.ptr(d_out), _lib.rng_ref(ctx.rng),
                                                         _lib.stream_of(out)), "composite_backward")
-        return d_out, None, None, None, None, None, None, None, None
+        return d_out, None, None, None, None, None, None, None, None, None
 
 
-def composite(model: SPNeRF, out: torch.Tensor, z: torch.Tensor, noise_std: float, weights_only=False):
+def composite(model: SPNeRF, out: torch.Tensor, z: torch.Tensor, noise_std: float, weights_only=False, sun_col=False):
+    """inference()'s compositing (spnerf.py:109-157).  ``sun_col`` (weights-only passes): the
+    first output is the sun-visibility column of ``out`` (B, S), whose gradient the composite
+    backward writes into d_out's sun column (the solar pass's sun_sc, rendering.py:177)."""
     B, S = z.shape
     key, keep = device_key(z.device)   # on-device σ noise: a slot per inference call, drawn or not
     noise = None if key is not None else current_random_source().noise((B, S), z.device, noise_std)   # spnerf.py:122
@@ -638,14 +647,14 @@ def composite(model: SPNeRF, out: torch.Tensor, z: torch.Tensor, noise_std: floa
     sem_col = 8 + (1 if model.beta else 0)
     n_sem = model.num_sem_classes if model.sem else 0
     return _Composite.apply(out, z.contiguous(), noise, noise_std, sem_col, n_sem, weights_only,
-                            key if noise_std != 0 else None, keep)
+                            key if noise_std != 0 else None, keep, sun_col)
 
 
-def _result(model, out, z, rgb, depth, w, T, sem, z_unsort=None):
+def _result(model, out, z, rgb, depth, w, T, sem, z_unsort=None, sun=None):
     B, S = z.shape
     o = out.view(B, S, model.number_of_outputs)
-    res = {"rgb": rgb, "depth": depth, "weights": w, "transparency": T, "albedo": o[..., :3], "sun": o[..., 4:5],
-           "sky": o[..., 5:8], "z_vals": z}
+    res = {"rgb": rgb, "depth": depth, "weights": w, "transparency": T, "albedo": o[..., :3],
+           "sun": o[..., 4:5] if sun is None else sun.view(B, S, 1), "sky": o[..., 5:8], "z_vals": z}
     if z_unsort is not None:
         res["z_vals_unsort"] = z_unsort
     col = 8
@@ -664,6 +673,9 @@ def inference_rays(model: SPNeRF, args, rays, z_vals, dir_offset=3, semantics=No
     the weights packed once for a whole render (``pack_for_render``)."""
     out = run_mlp(model, rays, z_vals, dir_offset, semantics if model.sem else None, rays_t if model.beta else None,
                   sigma_only=mode == "sigma", sun_only=mode == "sun", pack=pack)
+    if mode == "sun":   # the solar pass: sun_sc straight from the composite (its gradient fused there)
+        sun, depth, w, T, sem = composite(model, out, z_vals, args.noise_std, weights_only=True, sun_col=True)
+        return _result(model, out, z_vals, torch.empty(0, device=out.device), depth, w, T, sem, z_vals_unsort, sun=sun)
     rgb, depth, w, T, sem = composite(model, out, z_vals, args.noise_std, weights_only=mode != "full")
     return _result(model, out, z_vals, rgb, depth, w, T, sem, z_vals_unsort)
 
