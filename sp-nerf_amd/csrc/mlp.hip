@@ -22,6 +22,7 @@
 #include "common.h"
 #include "gemm_bf16.h"
 #include "gemm_f32.h"
+#include "heads_dx.h"
 #include "mlp_layout.h"
 #include "trunk.h"
 #include "wave.h"
@@ -36,7 +37,8 @@ struct PackPiece {
     const float* src;
     // bf: 1 = bf16 destination (dst in bf16 units); 2 = bf16 in the fused trunk's MFMA fragment
     // order (trunk_frag_off, dst_ld = the layer's padded K; transposed: element [c][r]); 5 = the same for 32 features per
-    // wave (frag_off NA = 1: the fused heads' 256-wide layers); 3 = split into bf16 planes
+    // wave (frag_off NA = 1: the fused heads' 256-wide layers); 7 = frag_off NA = 2 (64 features per wave; the
+    // heads' dX chain, transposed only); 3 = split into bf16 planes
     // [hi | hi | lo | lo] of width dst_ld / 4 each (hi = bf16(v), lo = bf16(v − hi)); 4 = the
     // same planes in the fused trunk's fragment order (dst_ld = 4·K0p); 6 = a narrow head's
     // [32][cols] hi/lo-row A operand (PackedOffs::Fnar16; rows = 32, nsrc source rows)
@@ -69,7 +71,7 @@ __device__ __forceinline__ void pack_block(const PackPiece pc, int t, float* pac
     const int tcols = (pc.cols + kPackTC - 1) / kPackTC;
     const int r0 = (t / tcols) * kPackTR, c0 = (t % tcols) * kPackTC;
     const int tid = threadIdx.x;
-    if (pc.transpose && pc.bf <= 2) {
+    if (pc.transpose && (pc.bf <= 2 || pc.bf == 5 || pc.bf == 7)) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const int rr = (tid >> 6) + 4 * e, cc = tid & 63;
@@ -82,7 +84,10 @@ __device__ __forceinline__ void pack_block(const PackPiece pc, int t, float* pac
             const int rr = tid & 31, cc = (tid >> 5) + 8 * e;
             const int r = r0 + rr, c = c0 + cc;
             if (r < pc.rows && c < pc.cols) {
-                const int64_t o = pc.dst + (pc.bf == 2 ? trunk_frag_off(c, r, pc.dst_ld) : (int64_t)c * pc.dst_ld + r);
+                const int64_t o = pc.dst + (pc.bf == 2   ? trunk_frag_off(c, r, pc.dst_ld)
+                                            : pc.bf == 5 ? frag_off(c, r, pc.dst_ld, 1)
+                                            : pc.bf == 7 ? frag_off(c, r, pc.dst_ld, 2)
+                                                         : (int64_t)c * pc.dst_ld + r);
                 if (pc.bf) reinterpret_cast<bf16*>(packed)[o] = (bf16)tileT[cc][rr];
                 else packed[o] = pc.rnd ? (float)(bf16)tileT[cc][rr] : tileT[cc][rr];
             }
@@ -1170,6 +1175,15 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
             SPN_TRY(narrow(x.r2W, 3, H, k.Fnar16 + (int64_t)32 * W));
             SPN_TRY(narrow(x.s4W, 1, H, k.Fnar16 + (int64_t)32 * (W + H)));
         }
+        if (k.BG16 >= 0) {  // the heads' fused dX chain: transposed, fragment order
+            SPN_TRY(piece(x.s3W, 0, H, H, k.Bs3_16, H, 1, 5));
+            SPN_TRY(piece(x.s2W, 0, H, H, k.Bs2_16, H, 1, 5));
+            // K index q of Q: sun_v.0 rows, then rgb.0 rows (k += H: (H / 16) k-steps of 2 · 512)
+            SPN_TRY(piece(x.s1W, 0, H, W, k.BQ16, d.NQ, 1, 7));
+            SPN_TRY(piece(x.r1W, 0, H, W, k.BQ16 + (int64_t)(H / 16) * 2 * 512, d.NQ, 1, 7));
+            SPN_TRY(piece(x.featW, 0, W, W, k.BG16, d.NG, 1, 7));
+            if (d.sem) SPN_TRY(piece(x.m1W, 0, H, W, k.BG16 + (int64_t)(W / 16) * 2 * 512, d.NG, 1, 7));
+        }
     }
     return launch_pack(v, packed, s);
 }
@@ -1880,6 +1894,29 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         }
         SPN_TRY(sb.run(s2));
     }
+    // 3 - 5 (their dX GEMMs): the training heads' fused dX chain (heads_dx_bf16.hip, option
+    // heads_dx) — dS2, dZQ's sun half, dZG's feat half and dZ_{L-1} in ONE launch, bit for bit the
+    // four GEMMs below; their weight gradients then follow on s2 as before
+    const int NQ = mode == 0 ? d.NQ : H;
+    const int NG = mode == 0 ? d.NG : W;
+    bool hdx = false;
+    if constexpr (BF) {
+        HeadsDxArgs h;
+        h.dS3 = dS3; h.DS2 = buf(c.w.DS2); h.DQ = buf(c.w.DQ); h.DL = buf(c.w.Db[d.L - 1]);
+        h.dS2 = dS2; h.dZQ = dZQ; h.dZG = dZG; h.dZL = buf(c.w.dZa);
+        h.hpre = hpre; h.wsig = c.pk(c.k.wsig); h.packed16 = c.pk16(0);
+        h.Bs3 = c.k.Bs3_16; h.Bs2 = c.k.Bs2_16; h.BQ = c.k.BQ16; h.BG = c.k.BG16;
+        h.P = P; h.ldQ = d.NQ; h.ldG = d.NG; h.HP = d.HP; h.kQ = d.NQ; h.kG = d.NG;
+        h.mode = mode; h.sem = d.sem ? 1 : 0;
+        hdx = g_heads_dx && !zs && !d.beta && W == 512 && H == 256 && (mode == 0 || mode == 2) && heads_dx_bf16_ok(h);
+        if (hdx) {
+            const double flop = 2.0 * P * ((double)H * H * 2 + (double)NQ * W + (double)NG * W);
+            const double in = 2.0 * P * (3.0 * H + (mode == 0 ? H : 0) + (mode == 0 && d.sem ? H : 0) + W) + 4.0 * P;
+            const double out = 2.0 * P * (2.0 * H + 2.0 * W);
+            SPN_TRY(heads_dx_bf16(h, s, flop, in + out));
+            SPN_TRY(stream_dep(sd, s, s2));
+        }
+    }
     // 3. sun_v_net chain: dZ_S2 = (dZ_S3 · Ws3) ⊙ DS2 ; dZ_S1 = (dZ_S2 · Ws2) ⊙ DQ[:, :H]
     {
         // deferred (SPNERF_MLP_DEFER_TRUNK_WGRAD): sun_v_net.4 / .2's weight gradients run in
@@ -1889,17 +1926,20 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         NT g;
         g.A = dS3; g.lda = H; g.K1 = H; g.B = G::w(c, c.k.Ws3T, c.k.Ws3T16); g.ldb = H; g.C = dS2; g.ldc = H;
         g.M = (int)P; g.N = H; g.K = H; g.Dmul = buf(c.w.DS2); g.ld_dmul = H;
-        SPN_TRY(G::nt(g, s));
-        SPN_TRY(stream_dep(sd, s, s2));
+        if (!hdx) {
+            SPN_TRY(G::nt(g, s));
+            SPN_TRY(stream_dep(sd, s, s2));
+        }
         if (!c.defer || !SPN_DEFER_SUNV)
             SPN_TRY(tn_grad<T>(c, dS2, H, H, Qb, d.NQ, nullptr, 0, H, H, s2, {red(0, H, H, gp(x.s2W), H, gp(x.s2b))}));
         NT g2 = g;
         g2.A = dS2; g2.B = G::w(c, c.k.Ws2T, c.k.Ws2T16); g2.C = dZQ; g2.ldc = d.NQ; g2.Dmul = buf(c.w.DQ); g2.ld_dmul = d.NQ;
-        SPN_TRY(G::nt(g2, s));
-        SPN_TRY(stream_dep(sd, s, s2));
+        if (!hdx) {
+            SPN_TRY(G::nt(g2, s));
+            SPN_TRY(stream_dep(sd, s, s2));
+        }
     }
     // 4. feat: dF = dZ_Q · WQ → dZG[:, :W];  dWQ = dZ_Q^T · feat
-    const int NQ = mode == 0 ? d.NQ : H;
     // deferred (SPNERF_MLP_DEFER_TRUNK_WGRAD, option defer_heads): the G / Q weight gradients run in
     // spnerf_mlp_trunk_wgrad, over every pass's points in one GEMM each
     const bool heads_def = c.defer && defer_heads_for(P);
@@ -1921,11 +1961,12 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         NT g;
         g.A = dZQ; g.lda = d.NQ; g.K1 = NQ; g.B = G::w(c, c.k.WQT, c.k.WQT16); g.ldb = d.NQ; g.C = dZG; g.ldc = d.NG;
         g.M = (int)P; g.N = W; g.K = NQ;
-        SPN_TRY(G::nt(g, s));
-        SPN_TRY(stream_dep(sd, s, s2));
+        if (!hdx) {
+            SPN_TRY(G::nt(g, s));
+            SPN_TRY(stream_dep(sd, s, s2));
+        }
     }
     // 5. H_L: dH_L = dZ_G · WG + dσ ⊗ w_σ ;  dZ_{L-1} = dH_L ⊙ D_L ;  dWG = dZ_G^T · H_L
-    const int NG = mode == 0 ? d.NG : W;
     // trunk dZ buffers in rotation: the dX GEMM of layer i writes the buffer whose dZ_{i+2} the
     // side stream's weight gradient of layer i+2 read (it waits for that, not for layer i+1's)
     T* dzb[3] = {buf(c.w.dZa), buf(c.w.dZb), buf(c.w.dZc)};
@@ -1948,8 +1989,10 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         g.r1_a = hpre; g.r1_lda = d.HP; g.r1_v = c.pk(c.k.wsig);
         g.Dmul = buf(c.w.Db[d.L - 1]); g.ld_dmul = W;
         if constexpr (BF) g.dmul_z = zs ? 1 : 0;
-        SPN_TRY(G::nt(g, s));
-        SPN_TRY(stream_dep(sd, s, s2));
+        if (!hdx) {
+            SPN_TRY(G::nt(g, s));
+            SPN_TRY(stream_dep(sd, s, s2));
+        }
     }
     // 6. trunk, top to bottom
     const T* X0 = BF ? buf(c.w.X0b) : buf(c.w.X0);
@@ -2421,7 +2464,7 @@ using namespace spn;
 
 static int* option_slot(const char* name) {
     const std::string n(name);
-    // The product library's switches (at most 15): the default kernels and their one documented
+    // The product library's switches (16): the default kernels and their one documented
     // alternate each (INTEGRATION.md §Kernel selection).
     if (n == "fused_trunk") return &g_fused_trunk;        // 0: layer-by-layer trunk GEMMs
     if (n == "trunk_tile") return &g_trunk_tile;          // 64 / 128-point training tiles
@@ -2433,6 +2476,7 @@ static int* option_slot(const char* name) {
     if (n == "tn_group_last") return &g_tn_group_last;    // cap of the last group (bench.py: 2 when N > 1)
     if (n == "defer_heads") return &g_defer_heads;        // the heads' weight gradients in the group launch
     if (n == "fused_bwd") return &g_fused_bwd;            // 0: the dX chain layer by layer
+    if (n == "heads_dx") return &g_heads_dx;              // 0: the heads' dX as four GEMMs
     if (n == "tn_bf16_variant") return &g_tn16_variant;   // 1: 128x128 TN tiles, 2: register-staged 256x256
     if (n == "tn_bf16_k64") return &g_tn16_k64;           // 0: N = 512, K = 64 weight gradients on 128x128 tiles
     if (n == "nt_f32_variant") return &g_nt_variant;      // the fp32 (parity) NT GEMM tilings

@@ -63,6 +63,11 @@ struct PackedOffs {
     // ~2^-17): σ [32][W] rows 0/1; albedo [32][H] rows 0/1, 2/3, 8/9 (r, g, b); sun visibility
     // [32][H] rows 0/1; zero elsewhere.  Fnar16 + narrow_off(0 / 1 / 2)
     int64_t Fnar16 = -1;
+    // the training heads' fused dX chain (heads_dx_bf16.hip): the TRANSPOSED weights in fragment
+    // order, element [n][k] = W[k][n] — sun_v 3 / 2 (32 features per wave, K = H), Q (64 per wave,
+    // K = NQ: sun_v.0 rows then rgb.0 rows) and G (64 per wave, K = NG: feat rows then semantic
+    // hidden rows); -1 where the fused dX chain does not apply
+    int64_t Bs3_16 = -1, Bs2_16 = -1, BQ16 = -1, BG16 = -1;
     int64_t total;
 };
 struct Packed : PackedOffs {

@@ -523,3 +523,33 @@ def test_training_heads_kernel_launches():
     classes = L.prof_classes()
     assert "heads_train" in classes, classes
     assert L.prof_read("heads_train")["launches"] == 3   # main pass windows 0 and 1, solar pass
+
+
+@pytest.mark.parametrize("sem,n,n_samples,guided", [(True, 300, 64, True), (False, 97, 40, False), (True, 97, 40, False),
+                                                    (True, 1, 16, False)])
+def test_heads_dx_chain_bitwise_equal(sem, n, n_samples, guided):
+    """The heads' fused dX chain (k_heads_dx_bf16, option heads_dx 1: dS2, dZQ's sun half, dF and
+    dZ_{L-1} in one launch, the main pass's every head and the solar pass's sun chain) equals the
+    four layer-by-layer DMA GEMMs (heads_dx 0) bit for bit: the same MFMA sums in the same K order,
+    the same epilogue arithmetic.  Sample counts that leave a partial 64-point tile included."""
+    r0, g0 = _render_train_heads({"heads_dx": 0}, sem, n, n_samples, guided)
+    r1, g1 = _render_train_heads({"heads_dx": 1}, sem, n, n_samples, guided)
+    assert sorted(r0) == sorted(r1) and sorted(g0) == sorted(g1)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        assert torch.equal(g0[k], g1[k]), (k, (g0[k] - g1[k]).abs().max().item(), g0[k].abs().max().item())
+
+
+def test_heads_dx_chain_launches():
+    """One heads dX launch per saving forward's backward (the guided main pass's two windows share
+    one backward; the solar pass has its own)."""
+    from spnerf_amd import _lib as L
+    L.prof_reset()
+    L.prof_enable(True)
+    try:
+        _render_train_heads({"heads_dx": 1}, True, 300, 64, True)
+    finally:
+        L.prof_enable(False)
+    assert L.prof_read("heads_dx")["launches"] == 2
