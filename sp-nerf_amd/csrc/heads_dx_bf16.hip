@@ -31,8 +31,10 @@
 
 namespace spn {
 
-// option "heads_dx": 1 = this launch (where heads_dx_bf16_ok), 0 (default) = the four GEMMs — measured
-// slower in the step (C4 22.05 -> 22.26 ms, same call), kept as the documented bit-identical alternate
+#ifdef SPN_ABLATIONS   // measured slower than the four GEMMs: an ablation-build kernel
+
+// option "heads_dx" (ablation build): 1 = this launch (where heads_dx_bf16_ok), 0 (default) = the four
+// GEMMs — this launch measured slower in the step (C4 22.05 -> 22.26 ms, same call)
 int g_heads_dx = 0;
 
 #ifndef HDX_ABL
@@ -375,5 +377,14 @@ int32_t heads_dx_bf16(const HeadsDxArgs& a, hipStream_t s, double flop, double b
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }
+
+#else   // product build: the heads' dX runs as the four GEMMs
+int g_heads_dx = 0;
+bool heads_dx_bf16_ok(const HeadsDxArgs&) { return false; }
+int32_t heads_dx_bf16(const HeadsDxArgs&, hipStream_t, double, double) {
+    SPN_ARG(false, "heads_dx_bf16: the fused heads dX chain is an ablation-build kernel (-DSPN_ABLATIONS)");
+    return SPNERF_OK;
+}
+#endif
 
 }  // namespace spn

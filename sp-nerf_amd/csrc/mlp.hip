@@ -2464,7 +2464,7 @@ using namespace spn;
 
 static int* option_slot(const char* name) {
     const std::string n(name);
-    // The product library's switches (16): the default kernels and their one documented
+    // The product library's switches (at most 15): the default kernels and their one documented
     // alternate each (INTEGRATION.md §Kernel selection).
     if (n == "fused_trunk") return &g_fused_trunk;        // 0: layer-by-layer trunk GEMMs
     if (n == "trunk_tile") return &g_trunk_tile;          // 64 / 128-point training tiles
@@ -2476,7 +2476,6 @@ static int* option_slot(const char* name) {
     if (n == "tn_group_last") return &g_tn_group_last;    // cap of the last group (bench.py: 2 when N > 1)
     if (n == "defer_heads") return &g_defer_heads;        // the heads' weight gradients in the group launch
     if (n == "fused_bwd") return &g_fused_bwd;            // 0: the dX chain layer by layer
-    if (n == "heads_dx") return &g_heads_dx;              // 0: the heads' dX as four GEMMs
     if (n == "tn_bf16_variant") return &g_tn16_variant;   // 1: 128x128 TN tiles, 2: register-staged 256x256
     if (n == "tn_bf16_k64") return &g_tn16_k64;           // 0: N = 512, K = 64 weight gradients on 128x128 tiles
     if (n == "nt_f32_variant") return &g_nt_variant;      // the fp32 (parity) NT GEMM tilings
@@ -2521,6 +2520,7 @@ static int* option_slot(const char* name) {
     if (n == "trunk2") return &g_trunk2;
     if (n == "trunk2_tile") return &g_trunk2_tile;
     if (n == "emu_bf16") return &g_emu_bf16;
+    if (n == "heads_dx") return &g_heads_dx;
 #endif
     return nullptr;
 }

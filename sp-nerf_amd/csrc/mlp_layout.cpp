@@ -171,7 +171,7 @@ Packed packed_layout(const Dims& d) {
             k.Fs2_16 = take16((int64_t)H * H);
             k.Fs3_16 = take16((int64_t)H * H);
             k.Fnar16 = take16((int64_t)32 * (W + 2 * H));
-            if (!d.beta) {  // the training heads' fused dX chain
+            if (!d.beta && kAblBuild) {  // the training heads' fused dX chain (an ablation-build kernel)
                 k.Bs3_16 = take16((int64_t)H * H);
                 k.Bs2_16 = take16((int64_t)H * H);
                 k.BQ16 = take16((int64_t)W * d.NQ);

@@ -124,7 +124,7 @@ PRODUCT_OPTIONS = ("fused_trunk", "trunk_tile", "trunk_heads", "heads_epi", "tru
                    "pack_table", "prof_shapes")
 ABLATION_OPTIONS = ("trunk_dbg", "trunk_var", "trunk_dreg", "trunk_bwd_dreg", "tn_bf16_pf", "tn_bf16_quad",
                     "tn_bf16_m16", "tn_bf16_rounds", "zsave", "trunk2", "trunk2_tile", "nt_bf16_ip", "tn_bf16_ip",
-                    "emu_bf16", "bwd_streams", "heads_variant", "fused_heads", "tile_rowsum")
+                    "emu_bf16", "bwd_streams", "heads_variant", "fused_heads", "tile_rowsum", "heads_dx")
 
 
 def test_kernel_options_roundtrip_and_reject_unknown_names():
