@@ -74,7 +74,7 @@ __global__ __launch_bounds__(512) void k_heads_bf16(HeadsFusedArgs g, PackedOffs
 // the trunk's tile loop spilled (64-bit values reloaded from scratch behind the copy-out stores)
 // and the main pass took 5.78 ms against 2.78 + 1.72 ms for the two launches.
 static_assert(SB_N * 4 <= RQ_BYTES, "the training heads' biases in the RQ area");
-template <bool RQ1>
+template <bool RQ1, bool SOL>
 __global__ __launch_bounds__(512) void k_heads_train_bf16(HeadsFusedArgs g, PackedOffs k, int ntiles) {
     __shared__ __attribute__((aligned(16))) char smem[LDS];
     const int tid = threadIdx.x;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(512) void k_heads_train_bf16(HeadsFusedArgs g, Pack
         __syncthreads();
         const int next = tile + (int)gridDim.x;
         // (past the last tile: this tile's rows again, never stored — no branch around the loads)
-        heads_tile_train<RQ1>(g, k, smem, ost, part, sbias, p0, [&] { load_hl((int64_t)std::min(next, ntiles - 1) * TM); });
+        heads_tile_train<RQ1, SOL>(g, k, smem, ost, part, sbias, p0, [&] { load_hl((int64_t)std::min(next, ntiles - 1) * TM); });
         __syncthreads();  // the next tile restages the image
     }
 }
@@ -123,7 +123,8 @@ __global__ __launch_bounds__(512) void k_heads_train_bf16(HeadsFusedArgs g, Pack
 bool heads_train_bf16_ok(const HeadsFusedArgs& h, const PackedOffs& k) {
     return h.HL && (h.mode == 0 || h.mode == 2) && h.NO <= OST_LD && h.C <= 3 && h.G && h.Q && h.DQ && h.S2 && h.DS2 &&
            h.S3 && h.DS3 && h.hsave && (h.mode != 0 || h.C == 0 || h.DG) && h.ldG % 8 == 0 && h.ldQ % 8 == 0 &&
-           k.Fnar16 >= 0 && k.Ffeat16 >= 0 && k.FQ16 >= 0 && k.Fs2_16 >= 0 && k.Fs3_16 >= 0 && (h.C == 0 || k.Fsem16 >= 0);
+           k.Fnar16 >= 0 && k.Ffeat16 >= 0 && k.FQ16 >= 0 && k.FQs16 >= 0 && k.Fs2_16 >= 0 && k.Fs3_16 >= 0 &&
+           (h.C == 0 || k.Fsem16 >= 0);
 }
 
 int32_t heads_train_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream_t s, double flop, double bytes) {
@@ -140,10 +141,16 @@ int32_t heads_train_bf16(const HeadsFusedArgs& a, const PackedOffs& k, hipStream
 #endif
     ProfScope prof("heads_train", s, flop, bytes);
     // every 128-point tile within one ray (S a multiple of 128): the Q epilogue's per-ray rows from LDS
-    if (SPN_HEADS_RQ_OST && a.S % TM == 0)
-        hipLaunchKernelGGL(k_heads_train_bf16<true>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, k, ntiles);
-    else
-        hipLaunchKernelGGL(k_heads_train_bf16<false>, dim3(std::min(ntiles, num_cus())), dim3(512), 0, s, ad, k, ntiles);
+    // the solar pass (mode 2) in its own instance (sun1 alone in Q: half its MFMAs)
+    const dim3 grid(std::min(ntiles, num_cus())), block(512);
+    const bool rq1 = SPN_HEADS_RQ_OST && a.S % TM == 0;
+    if (a.mode == 2) {
+        if (rq1) hipLaunchKernelGGL((k_heads_train_bf16<true, true>), grid, block, 0, s, ad, k, ntiles);
+        else hipLaunchKernelGGL((k_heads_train_bf16<false, true>), grid, block, 0, s, ad, k, ntiles);
+    } else {
+        if (rq1) hipLaunchKernelGGL((k_heads_train_bf16<true, false>), grid, block, 0, s, ad, k, ntiles);
+        else hipLaunchKernelGGL((k_heads_train_bf16<false, false>), grid, block, 0, s, ad, k, ntiles);
+    }
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
 }

@@ -552,7 +552,8 @@ __device__ __forceinline__ void stage_rows_ost(GA& g, KA& k, float* ost, int64_t
     }
 }
 
-template <bool RQ1, typename GA, typename KA, typename Prefetch>
+// SOL: the solar pass (g.mode 2), its own instance: sun1 alone in Q, no semantic / albedo heads
+template <bool RQ1, bool SOL, typename GA, typename KA, typename Prefetch>
 __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float* ost, float* part, const float* sbias,
                                                  int64_t p0, Prefetch&& prefetch) {
     constexpr int D1 = 8;  // ring depth of the 256-wide layers (sem hidden, sun_v 2 / 3)
@@ -563,7 +564,7 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     const int dbg = kTrunkAbl ? g.dbg : 0;
     const float* Pk = g.packed;
     const bf16* P16 = reinterpret_cast<const bf16*>(g.packed);
-    const bool full = g.mode == 0;
+    constexpr bool full = !SOL;   // (g.mode == 0 in the full instance, 2 in the solar one)
     const int C = full ? g.C : 0;
     const int rows = (int)std::min<int64_t>(TM, g.P - p0);
     auto stream = [&](int64_t off, int nks, int NA) {
@@ -643,10 +644,12 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
     }
     // feat = W_f H_L + b (linear) → the image (to G[:, 0..W) during Q's k-loop)
     u32x4 ring2q[D2][2];  // Q's weights
+    u32x4 ring1q[D1][1];  // ... the solar pass's: sun1 alone, 32 features per wave (FQs16)
     {
         f32x16 acc[2][NJ];
         layer_mm_d<2, D2>(stream(k.Ffeat16, HW / 16, 2), HW / 16, smem, lane, acc, ring2f, nodrain);
-        layer_prime_n<2, D2>(stream(k.FQ16, HW / 16, 2), ring2q);
+        if constexpr (full) layer_prime_n<2, D2>(stream(k.FQ16, HW / 16, 2), ring2q);
+        else layer_prime_n<1, D1>(stream(k.FQs16, HW / 16, 1), ring1q);
         __syncthreads();  // every wave is done reading H_L
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -664,10 +667,58 @@ __device__ __forceinline__ void heads_tile_train(GA& g, KA& k, char* smem, float
         __syncthreads();
     }
     // [sun1 | rgb1] = sin(W_Q feat + b + per-ray sun rows) → the image and DQ; feat leaves for G
-    // in 8 slices behind Q's k-step groups (the solar pass keeps sun1: waves 0..3's features)
+    // in 8 slices behind Q's k-step groups.  The solar pass needs sun1 alone: its 256 features
+    // over the 8 waves (32 each, the same MFMA per feature: the same sums), half the MFMAs
     u32x4 ring1s2[D1][1];  // sun_v 2's weights
     u32x4 afr[HH / 16 / 8];  // albedo's narrow A fragments
-    {
+    if constexpr (!full) {
+        f32x16 acc[1][NJ];
+        const auto rsF = rsrc(g.G, g.ldG);
+        layer_mm_d<1, D1>(stream(k.FQs16, HW / 16, 1), HW / 16, smem, lane, acc, ring1q,
+                          [&](int grp) {
+                              constexpr int PER = 16 / (HW / 16 / D1);  // feat's 16 chunks per thread over the groups
+                              image_out<64, PER>(smem, rsF, g.ldG, tid, PER * grp);
+                          });
+        layer_prime_n<1, D1>(stream(k.Fs2_16, HH / 16, 1), ring1s2);
+        __syncthreads();  // every wave is done reading feat (its copy-out included)
+        const auto rsD = rsrc_r(g.DQ, g.ldQ);
+        const int rlast = (int)(g.P - 1 - p0);  // P < 2^31 / 512 (host check)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            u32x2 yq[4];
+            const int64_t ray = ((int)p0 + std::min(32 * j + er32, rlast)) / g.S;
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 32 * w + 8 * gq + 4 * eh;
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + SB_Q + f0);
+                // (RQ1: the tile's one ray's row staged in ost, f0 >> 3 = 4w + gq, f0 & 7 = 4·eh)
+                const f32x4 rv = RQ1 ? *reinterpret_cast<const f32x4*>(ost + (4 * w + gq) * OST_LD + 8 + 4 * eh)
+                                     : ld4(g.rbQ + ray * (2 * HH) + f0);
+                float y[4], cs[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sincos((acc[0][j][4 * gq + e] + bv[e]) + rv[e], &y[e], &cs[e]);
+#if SPN_HEADS_DCOLS
+                put4(32 * j + er32, f0, cs);
+#else
+                put4(32 * j + er32, f0, y);
+#endif
+                yq[gq] = u32x2{pack2(y[0], y[1]), pack2(y[2], y[3])};
+                if (!SPN_HEADS_DCOLS) yq[gq] = u32x2{pack2(cs[0], cs[1]), pack2(cs[2], cs[3])};
+            }
+#if SPN_HEADS_DCOLS
+            cols_out<1>(smem, rsD, g.ldQ, 32 * w, j, lane);
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int f0 = 32 * w + 8 * gq + 4 * eh;
+                *reinterpret_cast<u32x2*>(smem + img_off(32 * j + er32, f0 >> 3) + 8 * ((f0 >> 2) & 1)) = yq[gq];
+            }
+#else
+            store_rows16(rsD, g.ldQ, 32 * w, 32 * j + er32, eh, yq);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+    } else {
         f32x16 acc[2][NJ];
         const auto rsF = rsrc(g.G, g.ldG);
         layer_mm_d<2, D2>(stream(k.FQ16, HW / 16, 2), HW / 16, smem, lane, acc, ring2q,

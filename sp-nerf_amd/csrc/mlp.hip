@@ -1166,6 +1166,7 @@ static int32_t pack_params(const Dims& d, const float* const* prm, float* packed
             SPN_TRY(piece(x.r1W, 0, H, W, k.FQ16 + (int64_t)H * W, W, 0, 2));  // rows H.. of Q (64-row waves)
             SPN_TRY(piece(x.s2W, 0, H, H, k.Fs2_16, H, 0, 5));
             SPN_TRY(piece(x.s3W, 0, H, H, k.Fs3_16, H, 0, 5));
+            SPN_TRY(piece(x.s1W, 0, H, W, k.FQs16, W, 0, 5));   // the solar pass's Q (sun_v.0 alone)
             auto narrow = [&](int pi, int nsrc, int K, int64_t dst) {
                 SPN_TRY(piece(pi, 0, 32, K, dst, K, 0, 6));
                 v.back().nsrc = nsrc;

@@ -170,6 +170,7 @@ Packed packed_layout(const Dims& d) {
             k.FQ16 = take16((int64_t)2 * H * W);
             k.Fs2_16 = take16((int64_t)H * H);
             k.Fs3_16 = take16((int64_t)H * H);
+            k.FQs16 = take16((int64_t)H * W);
             k.Fnar16 = take16((int64_t)32 * (W + 2 * H));
             if (!d.beta && kAblBuild) {  // the training heads' fused dX chain (an ablation-build kernel)
                 k.Bs3_16 = take16((int64_t)H * H);

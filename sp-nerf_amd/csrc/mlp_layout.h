@@ -58,6 +58,8 @@ struct PackedOffs {
     // [H][W] and sun_v 2 / 3 [H][H] with 32 features per wave, feat [W][W] and Q = [sun_v.0 ;
     // rgb.0] [2H][W] with 64 per wave; -1 where the fused heads do not apply
     int64_t Fsem16 = -1, Ffeat16 = -1, FQ16 = -1, Fs2_16 = -1, Fs3_16 = -1;
+    // the training heads' solar pass: sun_v.0's rows alone [H][W], 32 features per wave
+    int64_t FQs16 = -1;
     // the narrow heads as 32-row MFMA A operands (fragment order, 32 features per wave), each
     // weight row split into a bf16 hi row and a bf16 lo row (hi + lo carries the fp32 weight to
     // ~2^-17): σ [32][W] rows 0/1; albedo [32][H] rows 0/1, 2/3, 8/9 (r, g, b); sun visibility
