@@ -16,13 +16,14 @@ CLASSES = [(r"k_gemm_nt_bf16d<true", "gemm_nt_bf16d_dmul"), (r"k_gemm_nt_bf16d<"
            (r"k_gemm_nt_bf16w", "gemm_nt_bf16w"), (r"k_gemm_nt_bf16<", "gemm_nt_bf16"),
            (r"k_gemm_tn_bf16_k64", "gemm_tn_bf16k"), (r"k_gemm_tn_bf16d", "gemm_tn_bf16d"), (r"k_gemm_tn_bf16w", "gemm_tn_bf16w"), (r"k_gemm_tn_bf16\b", "gemm_tn_bf16"),
            (r"k_gemm_nt_w<|k_gemm_nt<", "gemm_nt_f32"), (r"k_gemm_tn<", "gemm_tn_f32"),
-           (r"k_trunk_bf16<128, 2048", "trunk_bf16_train"), (r"k_trunk_bf16<128, 4096", "trunk_heads_bf16"), (r"k_trunk_bf16<128", "trunk_bf16"), (r"k_trunk_bf16<64", "trunk_bf16_train"),
+           (r"k_trunk_bf16<128, 2048", "trunk_bf16_train"), (r"k_trunk_bf16<128, (4096|36864)", "trunk_heads_bf16"), (r"k_trunk_bf16<128", "trunk_bf16"), (r"k_trunk_bf16<64", "trunk_bf16_train"),
            (r"k_trunk2_bf16<\d+, (true|false), true", "trunk_bf16_train"),
            (r"k_trunk2_bf16<\d+, (true|false), false, true", "trunk_heads_bf16"), (r"k_trunk2_bf16<", "trunk_bf16"),
            (r"k_trunk_bwd_bf16", "trunk_bwd_bf16"), (r"k_heads_train_bf16", "heads_train"), (r"k_heads_bf16", "heads_fused"),
            (r"k_heads_fwd", "heads_fwd"), (r"k_heads_bwd", "heads_bwd"), (r"k_tn_skinny", "tn_skinny"),
            (r"k_reduce_slabs", "reduce_slabs"), (r"k_encode", "encode"), (r"k_composite_fwd", "composite_fwd"),
-           (r"k_composite_bwd", "composite_bwd"), (r"k_ray_rowsum", "ray_rowsum")]
+           (r"k_composite_bwd", "composite_bwd"), (r"k_ray_rowsum", "ray_rowsum"),
+           (r"k_merge_rows", "merge_samples"), (r"k_heads_dx_bf16", "heads_dx")]
 
 
 def class_of(name):
