@@ -1957,8 +1957,9 @@ static int32_t backward_points(const Ctx& c, int mode, const float* packed, cons
         } else {
             SPN_TRY(tn_grad<T>(c, dZQ, d.NQ, H, Gb, d.NG, nullptr, 0, W, W, s2, {red(0, H, W, gp(x.s1W), ld(x.s1W), gp(x.s1b))}));
         }
-        // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns
-        SPN_TRY(ray_rowsum<T>(dZQ, d.NQ, 0, NQ, S, n_rays, c.at(c.w.RQ), d.NQ, s2));
+        // per-ray sums of dZ_Q feed the sun-direction / time-embedding columns (sun_v.0's and β.0's
+        // blocks of RQ; rgb.0 has no per-ray input, so its block is not summed without β)
+        SPN_TRY(ray_rowsum<T>(dZQ, d.NQ, 0, d.beta ? NQ : H, S, n_rays, c.at(c.w.RQ), d.NQ, s2));
         NT g;
         g.A = dZQ; g.lda = d.NQ; g.K1 = NQ; g.B = G::w(c, c.k.WQT, c.k.WQT16); g.ldb = d.NQ; g.C = dZG; g.ldc = d.NG;
         g.M = (int)P; g.N = W; g.K = NQ;

@@ -260,12 +260,13 @@ __global__ __launch_bounds__(256) void k_sort_rows(int64_t B, int n, const float
 // sorted position of element e of z_unsort = [z | sorted z_2] (the reference's z_vals_unsort) is
 // its rank #{f : z[f] < z[e]} + #{f < e : z[f] == z[e]} — a permutation into ascending order, so
 // the rows land where torch.sort puts their depths (equal depths are the same point: equal rows).
-// One 256-thread block per ray (n = s1 + s2 <= 256: one element per thread for the ranks).  The
+// One 128-thread block per ray (n = s1 + s2 <= 256: up to two elements per thread for the ranks;
+// small blocks: every ray of a 4 096-ray batch resident at once, one latency round).  The
 // ray's rows move through LDS so that every global access is a contiguous run of the ray's rows,
 // all issued up front: forward the two segments' runs (s1·n_out and s2·n_out floats) in and the
 // sorted run out, backward the reverse.  The ranks are formed while the rows are in flight.
 // bwd = 0: sorted ← segments; 1: segments ← sorted (the pointers' roles swap, not their types)
-__global__ __launch_bounds__(256) void k_merge_rows(int64_t B, int s1, int s2, const float* __restrict__ zu,
+__global__ __launch_bounds__(128) void k_merge_rows(int64_t B, int s1, int s2, const float* __restrict__ zu,
                                                     float* __restrict__ seg1, float* __restrict__ seg2,
                                                     float* __restrict__ sorted, int n_out, int bwd) {
     extern __shared__ __attribute__((aligned(16))) float msm[];
@@ -282,49 +283,57 @@ __global__ __launch_bounds__(256) void k_merge_rows(int64_t B, int s1, int s2, c
     float* g1 = seg1 + ray * (int64_t)n1;
     float* g2 = seg2 + ray * (int64_t)(s2 * n_out);
     float* gs = sorted + ray * (int64_t)nn;
-    // the depths first, then (up to 256·U values) the rows: the depths' wait does not wait for them
-    const float zv = tid < n ? zu[ray * n + tid] : INFINITY;
-    constexpr int U = 8;
-    const bool fits = nn <= 256 * U;
+    // the depths first, then (up to 128·U values) the rows: the depths' wait does not wait for them
+    constexpr int NT = 128, U = 16;
+    float zv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) zv[h] = tid + NT * h < n ? zu[ray * n + tid + NT * h] : INFINITY;
+    const bool fits = nn <= NT * U;
     auto src_of = [&](int i) -> float* { return bwd ? gs + i : (i < n1 ? g1 + i : g2 + (i - n1)); };
     float v[U];
     if (fits) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int i = tid + 256 * u;
+            const int i = tid + NT * u;
             v[u] = i < nn ? *src_of(i) : 0.f;
         }
     }
-    if (tid < n4) zs[tid] = zv;
-    __syncthreads();
-    if (tid < n) {
-        int rank = 0;
-#pragma unroll 4
-        for (int f = 0; f < n4; f += 4) {
-            const f32x4 w = *reinterpret_cast<const f32x4*>(zs + f);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) rank += (w[q] < zv) || (w[q] == zv && f + q < tid);
+    for (int h = 0; h < 2; ++h)
+        if (tid + NT * h < n4) zs[tid + NT * h] = zv[h];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int e = tid + NT * h;
+        if (e < n) {
+            int rank = 0;
+#pragma unroll 4
+            for (int f = 0; f < n4; f += 4) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(zs + f);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) rank += (w[q] < zv[h]) || (w[q] == zv[h] && f + q < e);
+            }
+            rank_of[e] = rank;
+            src[rank] = e;
         }
-        rank_of[tid] = rank;
-        src[rank] = tid;
     }
     // the rows into LDS (element e's row at rows[e · n_out]: segment order forward, sorted order
     // backward)
     if (fits) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (tid + 256 * u < nn) rows[tid + 256 * u] = v[u];
+            if (tid + NT * u < nn) rows[tid + NT * u] = v[u];
     } else {
-        for (int i = tid; i < nn; i += 256) rows[i] = *src_of(i);
+        for (int i = tid; i < nn; i += NT) rows[i] = *src_of(i);
     }
     __syncthreads();
     if (!bwd) {
-        for (int i = tid; i < nn; i += 256) {
+        for (int i = tid; i < nn; i += NT) {
             const int t = (int)(((float)i + 0.5f) * inv), col = i - t * n_out;  // i / n_out (exact: i < 2^16)
             gs[i] = rows[src[t] * n_out + col];
         }
     } else {
-        for (int i = tid; i < nn; i += 256) {
+        for (int i = tid; i < nn; i += NT) {
             const int e = (int)(((float)i + 0.5f) * inv), col = i - e * n_out;
             const float x = rows[rank_of[e] * n_out + col];
             if (i < n1) g1[i] = x;
@@ -345,7 +354,7 @@ static int32_t merge_rows(int64_t n_rays, int32_t s1, int32_t s2, const float* z
     ProfScope prof("merge_samples", s, 0.0, (double)n_rays * (s1 + s2) * (8.0 * n_out + 4.0));
     const size_t lds = sizeof(float) * ((size_t)(s1 + s2) * (3 + n_out) + 3);
     SPN_ARG(lds <= 64 * 1024, "merge_samples: %d samples x %d outputs too large", s1 + s2, n_out);
-    hipLaunchKernelGGL(k_merge_rows, dim3((unsigned)n_rays), dim3(256), lds, s, n_rays, s1, s2, z_unsort, seg1, seg2, sorted,
+    hipLaunchKernelGGL(k_merge_rows, dim3((unsigned)n_rays), dim3(128), lds, s, n_rays, s1, s2, z_unsort, seg1, seg2, sorted,
                        n_out, bwd);
     SPN_HIP(hipGetLastError());
     return SPNERF_OK;
