@@ -105,7 +105,7 @@ int32_t spnerf_mlp_forward(const spnerf_model_cfg* cfg, const void* packed,
  * saving forward whose backward runs over all n_rays_total rays — render_rays' guided main pass
  * (rendering.py:159-170) evaluates its stratified half in pass 1 (window 0, whose sigma feeds
  * the guided windows) and only the guided half afterwards (window 1, the rays repeated), instead
- * of evaluating the stratified points twice.  ray_begin * n_samples must be even. */
+ * of evaluating the stratified points twice. */
 int32_t spnerf_mlp_forward_window(const spnerf_model_cfg* cfg, const void* packed,
                                   const float* rays, int32_t ray_stride, int32_t dir_offset,
                                   int64_t n_rays_total, int64_t ray_begin, int64_t n_rays, int32_t n_samples,

@@ -2668,7 +2668,6 @@ extern "C" int32_t spnerf_mlp_forward_window(const spnerf_model_cfg* cfg, const 
     SPN_ARG(n_rays >= 0 && n_samples > 0 && ray_stride >= 11, "mlp_forward_window: bad sizes");
     SPN_ARG(ray_begin >= 0 && n_rays_total >= ray_begin + n_rays, "mlp_forward_window: rays [%lld, %lld) outside %lld",
             (long long)ray_begin, (long long)(ray_begin + n_rays), (long long)n_rays_total);
-    SPN_ARG((ray_begin * n_samples) % 2 == 0, "mlp_forward_window: the window must start at an even point");
     SPN_ARG(n_rays_total * n_samples < (1ll << 31) / std::max(d.NQ, d.NG), "mlp_forward_window: too many points");
     SPN_ARG(dir_offset == 3 || dir_offset == 8, "mlp_forward_window: dir_offset must be 3 (view) or 8 (sun)");
     SPN_ARG(z_stride == 0 || z_stride >= n_samples, "mlp_forward_window: z_stride %d < n_samples %d", z_stride, n_samples);

@@ -184,3 +184,28 @@ def test_reuse_no_grad_render_equals_two_evaluations(name, precision):
     assert sorted(outs[0]) == sorted(outs[1])
     for k in outs[1]:
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_reuse_odd_window_offsets(precision):
+    """37 rays x 33 samples: window 1 starts at an odd point (B·S = 1 221), every buffer row of the
+    workspace still aligned; renders bit for bit the two-evaluation schedule's in fp32 (bf16: the
+    pass-1 σ bound above), gradients within the same bounds."""
+    from test_gpu_variants import _render_train_heads
+    old = rendering.REUSE_PASS1
+    out = []
+    try:
+        for reuse in (True, False):
+            rendering.REUSE_PASS1 = reuse
+            out.append(_render_train_heads({}, True, 37, 33, True, precision=precision))
+    finally:
+        rendering.REUSE_PASS1 = old
+    (r1, g1), (r0, g0) = out
+    for k in r0:
+        if precision == "fp32":
+            assert torch.equal(r0[k], r1[k]), k
+        else:
+            assert gu.rel_err(r1[k].numpy(), r0[k].numpy()) < 5e-4, k
+    num = sum(float(((g1[k] - g0[k]).double() ** 2).sum()) for k in g0)
+    den = sum(float((g0[k].double() ** 2).sum()) for k in g0)
+    assert (num / den) ** 0.5 < (1e-5 if precision == "fp32" else 6e-3)

@@ -450,7 +450,7 @@ def test_heads_in_gemm_epilogue_agree(beta):
         assert (g0[k] - g1[k]).abs().max().item() <= 1e-4 * scale + 1e-30, k
 
 
-def _render_train_heads(opts, sem, n, n_samples, guided):
+def _render_train_heads(opts, sem, n, n_samples, guided, precision="bf16"):
     """A bf16 training render (solar pass on, semantic head optional) and its gradients."""
     old = {k: _lib.get_option(k) for k in opts}
     for k, v in opts.items():
@@ -467,7 +467,7 @@ def _render_train_heads(opts, sem, n, n_samples, guided):
                       target_depths=torch.stack([rays[:, 7] * 0.5, torch.ones(n, device=DEV)], 1),
                       target_std=torch.full((n,), 0.01, device=DEV))
         labels = torch.randint(0, 3, (n,), generator=g).to(DEV) if sem else None
-        model = make_model(ModelDims(width=512, sem=sem), 9, "bf16")
+        model = make_model(ModelDims(width=512, sem=sem), 9, precision)
         torch.manual_seed(7)
         res = spnerf_amd.render_rays({"coarse": model}, args, rays, None, semantics=labels, mode="train", **kw)
         loss = sum((v.float() ** 2).mean() for k, v in sorted(res.items()) if v.requires_grad)
