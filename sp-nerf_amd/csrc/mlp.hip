@@ -800,7 +800,10 @@ __global__ void k_ray_rowsum(const T* __restrict__ in, int ld, int c0, int N, in
 }
 
 // Same sum for bf16 rows with N, ld, c0 multiples of 8: one block per ray, a thread owns 8
-// columns (16-B loads) in one of 256/(N/8) row phases; phases combined in a fixed order.
+// columns (16-B loads) in one of 256/(N/8) row phases; phases combined in a fixed order.  A
+// thread's rows load 8 at a time before they are summed (in the same order): one HBM latency per
+// 8 rows instead of one per row (two launches per step: C4 0.138 -> 0.135 ms, C4@512 0.044 ->
+// 0.037 ms, bit-identical; the same batching in the skinny reductions measured level)
 __global__ __launch_bounds__(256) void k_ray_rowsum16(const bf16* __restrict__ in, int ld, int c0, int N, int S,
                                                       float* __restrict__ out, int ldo) {
     __shared__ float part[256 * 8];
@@ -811,11 +814,22 @@ __global__ __launch_bounds__(256) void k_ray_rowsum16(const bf16* __restrict__ i
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (ph < nph) {
         const bf16* p = in + ray * S * (int64_t)ld + c0 + 8 * q;
-        for (int i = ph; i < S; i += nph) {
-            float f[8];
-            unpack8(ldg16(p + (int64_t)i * ld), f);
+        for (int i0 = ph; i0 < S; i0 += 8 * nph) {
+            u32x4 v[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] += f[e];
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * nph;
+                v[u] = i < S ? ldg16(p + (int64_t)i * ld) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (i0 + u * nph < S) {
+                    float f[8];
+                    unpack8(v[u], f);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) acc[e] += f[e];
+                }
+            }
         }
     }
 #pragma unroll
