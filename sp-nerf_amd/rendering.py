@@ -160,6 +160,25 @@ def GenerateGuidedSamples(res, z_vals, N_samples, perturb, near, far, mode='test
     return z2
 
 
+def _empty_batch(models, args, rays, ts, semantics, mode, valid_depth, target_depths, target_std, clamp_near_far):
+    """An empty batch: the outputs of a one-ray placeholder render sliced to zero rows, so that they
+    keep the reference's keys, trailing shapes and autograd connection (a backward through them
+    leaves every parameter gradient zero).  The library's entry points take device pointers, which
+    an empty tensor does not have; the placeholder ray (origin 0, direction -z, near 1, far 2, sun
+    +z) keeps every value finite, so the zero gradients it receives stay zero."""
+    one = torch.zeros(1, rays.shape[1], device=rays.device)
+    one[0, 5], one[0, 6], one[0, 7] = -1.0, 1.0, 2.0
+    if rays.shape[1] >= 11:
+        one[0, 10] = 1.0
+
+    def pick(t, fill):
+        return None if t is None else torch.full((1,) + tuple(t.shape[1:]), fill, dtype=t.dtype, device=t.device)
+
+    out = render_rays(models, args, one, pick(ts, 0), pick(semantics, 0), mode, pick(valid_depth, 0),
+                      pick(target_depths, 1.5), pick(target_std, 0.1), clamp_near_far=clamp_near_far)
+    return {k: v[:0] for k, v in out.items()}
+
+
 def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth=None, target_depths=None,
                 target_std=None, *, clamp_near_far=None):
     """rendering.py:119-218 for the coarse SP-NeRF model; returns the same dictionary
@@ -172,6 +191,9 @@ def render_rays(models, args, rays, ts, semantics=None, mode='test', valid_depth
     _lib.require_device(rays)
     rays = rays.contiguous().float()
     B = rays.shape[0]
+    if B == 0:
+        return _empty_batch(models, args, rays, ts, semantics, mode, valid_depth, target_depths, target_std,
+                            clamp_near_far)
     begin_render(rays.device)         # a keyed on-device random source starts a new step
     key, keep = device_key(rays.device)
     if key is not None:
